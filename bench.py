@@ -1,0 +1,217 @@
+#!/usr/bin/env python
+"""Headline benchmark: rendered frames/sec at 512x512 with ~100k Gaussians (BASELINE.json).
+
+One step = one pass of the rasterizer hot path (preprocess -> tile binning -> per-tile depth
+sort -> 32-channel front-to-back compositing) over a batch of `--batch` frames of the synthetic
+GUAVA-like avatar (config 2: P=100,000 Gaussians, 512x512, one camera per frame), with every
+input resident in HBM before the timed region.  N GPUs: one process per GPU, each renders its
+own `--batch` frames (frames are independent -> weak scaling, no collective in the data path;
+torch.distributed is used only for the barrier and the max-over-ranks time).
+
+Prints ONE JSON line (rank 0) with the contract fields plus:
+  roofline      -- render_fwd kernel: algorithmic bytes per launch / average launch time from HIP
+                   events recorded on the launch stream inside the timed region;
+  cpu_baseline  -- the CPU oracle (a port of the reference algorithm) timed on a bounded sample of
+                   the same workload on this host's cores (rank 0, N=1 only).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+C = 32
+
+
+def _args():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--batch", type=int, default=32, help="frames per step per GPU")
+    ap.add_argument("--config", default="c2", choices=["c2", "c5"])
+    ap.add_argument("--fast-exp", action="store_true", help="hardware exp (not bit-exact)")
+    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--stages", action="store_true", help="also time every stage (extra events)")
+    return ap.parse_args()
+
+
+def _workload(cfg):
+    if cfg == "c5":
+        return dict(P=300000, W=1024, H=1024, gpt=3, name="guava-avatar-synth-300k-1024")
+    return dict(P=100000, W=512, H=512, gpt=1, name="guava-avatar-synth-100k-512")
+
+
+def _render_alg_bytes(P_vis, W, H):
+    # render_fwd compulsory traffic per frame: per visible Gaussian its 32 features (128 B) +
+    # means2D (8) + conic/opacity (16) + 1/depth (4); per pixel 32 channels + inverse depth out
+    # (132 B) + final_T + n_contrib (8 B) kept for backward.
+    return 156.0 * P_vis + 140.0 * W * H
+
+
+def _path_alg_bytes(P, W, H):
+    # SURVEY.md 8(d) / BASELINE.md: B_fwd = 176*P + 132*H*W per frame
+    return 176.0 * P + 132.0 * W * H
+
+
+def cpu_baseline(scene, cams, W, H, budget_s):
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle  # CPU restatement of the reference algorithm (checker / baseline only)
+    threads = max(1, min(16, os.cpu_count() or 1))
+    oracle.set_threads(threads)
+    bg = np.zeros(C, np.float32)
+    t0 = time.perf_counter()
+    frames = 0
+    while True:
+        cam = cams[frames % len(cams)]
+        oracle.forward(scene["means3D"], scene["colors"], scene["opacities"], scene["scales"],
+                       scene["rotations"], None, cam["viewmatrix"], cam["projmatrix"], W, H,
+                       cam["tanfovx"], cam["tanfovy"], bg)
+        frames += 1
+        el = time.perf_counter() - t0
+        if el >= budget_s or frames >= 64:
+            break
+    return dict(value=frames / el, unit="frames/s", cores=threads, kind="port",
+                sample=f"{frames} frames of the same {W}x{H} workload through the C oracle "
+                       f"(preprocess+bin+sort+render, OpenMP {threads} threads) in {el:.1f}s")
+
+
+def main():
+    a = _args()
+    import torch
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+
+    from guava_renderer_amd import _lib, scenes
+    from guava_renderer_amd.batch import BatchRasterizer, profile_enable, profile_read
+    _lib.set_exact_exp(not a.fast_exp)
+
+    wl = _workload(a.config)
+    P, W, H, B = wl["P"], wl["W"], wl["H"], a.batch
+    scene = scenes.avatar_cloud(P, seed=0, gaussians_per_texel=wl["gpt"])
+    P = scene["means3D"].shape[0]
+    cams_all = scenes.frame_cameras(B * world, W, H, seed=1000)
+    cams = cams_all[rank * B:(rank + 1) * B]
+
+    t = lambda x: torch.tensor(np.ascontiguousarray(x), device=dev)  # noqa: E731
+    means, colors = t(scene["means3D"]), t(scene["colors"])
+    opac, scales, rots = t(scene["opacities"]), t(scene["scales"]), t(scene["rotations"])
+    views = t(np.stack([c["viewmatrix"].reshape(16) for c in cams]))
+    projs = t(np.stack([c["projmatrix"].reshape(16) for c in cams]))
+    tanf = t(np.array([[c["tanfovx"], c["tanfovy"]] for c in cams], np.float32))
+    bgs = torch.zeros((B, C), dtype=torch.float32, device=dev)
+
+    # size the instance capacity from one probe batch
+    probe = BatchRasterizer(B, P, W, H, R_capacity=24 * P * B, device=dev)
+    probe.forward(means, colors, opac, scales, rots, views, projs, tanf, bgs)
+    R_probe, ovf = probe.status()
+    assert not ovf, "probe overflow"
+    del probe
+    torch.cuda.empty_cache()
+    rast = BatchRasterizer(B, P, W, H, R_capacity=int(R_probe * 1.25) + 1024, device=dev)
+
+    def step():
+        return rast.forward(means, colors, opac, scales, rots, views, projs, tanf, bgs)
+
+    for _ in range(a.warmup):
+        step()
+    torch.cuda.synchronize(dev)
+    R_total, ovf = rast.status()
+    assert not ovf
+    P_vis = int((rast.radii > 0).sum().item())
+    profile_read()  # reset accumulators
+    profile_enable(("preprocess", "scan", "bin_count", "tile_scan", "bin_scatter", "tile_sort",
+                    "render_fwd") if a.stages else ("render_fwd",))
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        step()
+    torch.cuda.synchronize(dev)
+    el = time.perf_counter() - t0
+    if dist is not None:
+        dist.barrier()
+    prof = profile_read()
+    profile_enable(())
+    R_after, ovf = rast.status()
+    assert not ovf, "capacity overflow inside the timed region"
+    if dist is not None:
+        tt = torch.tensor([el], dtype=torch.float64, device=dev)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        el = float(tt.item())
+
+    frames = world * B * a.steps
+    fps = frames / el
+    ms_step = 1000.0 * el / a.steps
+    rms, rcnt = prof.get("render_fwd", (0.0, 0))
+    render_ms = rms / max(rcnt, 1)
+    bytes_launch = _render_alg_bytes(P_vis / B, W, H) * B
+    achieved = bytes_launch / (render_ms * 1e-3) / 1e9 if render_ms > 0 else None
+    traffic = None
+    pmc_path = os.path.join(ROOT, "profiles", "pmc_render_fwd.json")
+    if os.path.exists(pmc_path):
+        try:
+            pm = json.load(open(pmc_path))
+            if pm.get("config") == wl["name"] and pm.get("batch") == B:
+                traffic = pm.get("hbm_bytes_per_launch")
+        except Exception:  # noqa: BLE001
+            traffic = None
+
+    out = {
+        "metric": "rendered frames/sec @512x512, ~100k Gaussians" if a.config == "c2"
+                  else "rendered frames/sec @1024x1024, ~300k Gaussians",
+        "value": round(fps, 2),
+        "unit": "frames/s",
+        "n_gpus": world,
+        "steps": a.steps,
+        "warmup": a.warmup,
+        "ms_per_step": round(ms_step, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f32",
+        "data": "synthetic (SMPL-X-template avatar cloud, GUAVA attribute distributions, "
+                "one orbit camera per frame)",
+        "config": {"workload": wl["name"], "gaussians": P, "image": [W, H], "channels": C,
+                   "frames_per_step_per_gpu": B, "global_batch": B * world,
+                   "parallelism": f"frame-sharded x{world}",
+                   "exp": "hw" if a.fast_exp else "exact-poly",
+                   "instances_per_step": R_total, "visible_gaussians_per_frame": P_vis / B},
+        "roofline": {"bound": "hbm", "kernel": "render_fwd",
+                     "achieved": round(achieved, 1) if achieved else None,
+                     "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": round(achieved / HBM_PEAK_GBS, 4) if achieved else None,
+                     "traffic": traffic, "alg_bytes_per_launch": bytes_launch,
+                     "avg_launch_ms": round(render_ms, 4)},
+        "path_roofline": {"alg_bytes_per_frame": _path_alg_bytes(P, W, H),
+                          "achieved_GBs": round(_path_alg_bytes(P, W, H) * fps / 1e9, 1),
+                          "frac": round(_path_alg_bytes(P, W, H) * fps / 1e9 / HBM_PEAK_GBS, 4)},
+    }
+    if a.stages:
+        out["stage_ms_per_step"] = {k: round(v[0] / max(v[1], 1), 4) for k, v in prof.items()}
+    if rank == 0 and world == 1 and not a.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline(scene, cams, W, H, a.cpu_seconds)
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

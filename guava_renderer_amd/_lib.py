@@ -1,0 +1,98 @@
+"""Loader for the gfx950 rasterizer library (guava_renderer_amd/lib/libgsr.so, C ABI include/gsr.h).
+
+There is no CPU fallback: if the library is missing or fails to load, every entry point raises.
+"""
+import ctypes
+import os
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "lib", "libgsr.so")
+
+# every symbol declared in include/gsr.h
+EXPORTS = ("gsr_version", "gsr_last_error", "gsr_set_exact_exp", "gsr_geometry_bytes",
+           "gsr_image_bytes", "gsr_binning_bytes", "gsr_mark_visible", "gsr_forward",
+           "gsr_backward", "gsr_batch_workspace_bytes", "gsr_forward_batch",
+           "gsr_backward_batch", "gsr_batch_status", "gsr_profile_enable", "gsr_profile_read")
+
+ALLOC_FN = ctypes.CFUNCTYPE(ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t)
+
+_vp = ctypes.c_void_p
+_i = ctypes.c_int
+_i64 = ctypes.c_int64
+_f = ctypes.c_float
+_sz = ctypes.c_size_t
+
+_lib = None
+
+
+class GsrError(RuntimeError):
+    pass
+
+
+def load(path=None):
+    """Load libgsr.so (building it first when hipcc is available and the .so is absent)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    path = path or LIB_PATH
+    # torch-ROCm ships its own libamdhip64 (soname libamdhip64.so.7) and loads it by the
+    # unversioned name; load torch first so libgsr.so binds to that same HIP runtime instead of
+    # pulling /opt/rocm's copy into the process as a second runtime.
+    import torch  # noqa: F401
+    if not os.path.exists(path):
+        try:
+            from . import build as _build
+            _build.build(verbose=False)
+        except Exception as e:  # noqa: BLE001
+            raise GsrError(f"libgsr.so not found at {path} and could not be built: {e}") from e
+    L = ctypes.CDLL(path)
+    L.gsr_version.restype = ctypes.c_char_p
+    L.gsr_last_error.restype = ctypes.c_char_p
+    L.gsr_set_exact_exp.argtypes = [_i]
+    L.gsr_set_exact_exp.restype = _i
+    L.gsr_geometry_bytes.argtypes = [_i]
+    L.gsr_geometry_bytes.restype = _sz
+    L.gsr_image_bytes.argtypes = [_i, _i]
+    L.gsr_image_bytes.restype = _sz
+    L.gsr_binning_bytes.argtypes = [_i64]
+    L.gsr_binning_bytes.restype = _sz
+    L.gsr_mark_visible.argtypes = [_i, _vp, _vp, _vp, _vp, _vp]
+    L.gsr_mark_visible.restype = _i
+    L.gsr_forward.argtypes = [ALLOC_FN, ALLOC_FN, ALLOC_FN, _vp, _i, _i, _i, _vp, _i, _i, _vp, _vp,
+                              _vp, _vp, _vp, _f, _vp, _vp, _vp, _vp, _vp, _f, _f, _i, _vp, _vp, _i,
+                              _vp, _i, _vp]
+    L.gsr_forward.restype = _i
+    L.gsr_backward.argtypes = [_i, _i, _i, _i, _vp, _i, _i, _vp, _vp, _vp, _vp, _vp, _f, _vp, _vp,
+                               _vp, _vp, _vp, _f, _f, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp,
+                               _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i, _i, _vp]
+    L.gsr_backward.restype = _i
+    L.gsr_batch_workspace_bytes.argtypes = [_i, _i, _i, _i, _i64]
+    L.gsr_batch_workspace_bytes.restype = _sz
+    L.gsr_forward_batch.argtypes = [_i, _i, _i, _i, _vp, _i64, _vp, _i64, _vp, _i64, _vp, _i64, _vp,
+                                    _i64, _f, _vp, _vp, _vp, _vp, _i64, _vp, _i64, _vp, _vp, _vp, _i,
+                                    _vp]
+    L.gsr_forward_batch.restype = _i
+    L.gsr_backward_batch.argtypes = [_i, _i, _i, _i, _vp, _i64, _vp, _i64, _vp, _i64, _vp, _i64, _vp,
+                                     _i64, _f, _vp, _vp, _vp, _vp, _i64, _vp, _i64, _vp, _vp, _vp, _vp,
+                                     _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i, _vp]
+    L.gsr_backward_batch.restype = _i
+    L.gsr_batch_status.argtypes = [_vp, _i, _i, ctypes.POINTER(_i64), ctypes.POINTER(_i), _vp]
+    L.gsr_batch_status.restype = _i
+    L.gsr_profile_enable.argtypes = [ctypes.c_uint32]
+    L.gsr_profile_enable.restype = _i
+    L.gsr_profile_read.argtypes = [ctypes.POINTER(ctypes.c_double), ctypes.POINTER(_i), _i]
+    L.gsr_profile_read.restype = _i
+    _lib = L
+    return L
+
+
+def check(rc, what):
+    """Raise with the library's message for a negative return code; return rc otherwise."""
+    if rc < 0:
+        msg = load().gsr_last_error().decode(errors="replace")
+        raise GsrError(f"{what} failed ({-rc}): {msg}")
+    return rc
+
+
+def set_exact_exp(on=True):
+    return load().gsr_set_exact_exp(1 if on else 0)

@@ -1,0 +1,429 @@
+// capi.hip -- host driver behind include/gsr.h: carves the scratch arenas, sequences the kernels
+// on the caller's HIP stream and reports errors.  The single-frame entry points keep the
+// reference's one host synchronisation (num_rendered sizes the binning buffer,
+// rasterizer_impl.cu:284-288); the batch entry points have none.
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/gsr.h"
+#include "gsr_internal.h"
+
+using namespace gsr;
+
+namespace {
+
+thread_local std::string g_err;
+int g_exact_exp = 1;
+
+int fail(gsr_status st, const std::string& msg) {
+    g_err = msg;
+    return -(int)st;
+}
+
+#define HIP_TRY(expr)                                                                        \
+    do {                                                                                     \
+        hipError_t e_ = (expr);                                                              \
+        if (e_ != hipSuccess)                                                                \
+            return fail(GSR_ERR_HIP, std::string(#expr) + ": " + hipGetErrorString(e_));     \
+    } while (0)
+
+#define STAGE(debug, stream, name)                                                           \
+    do {                                                                                     \
+        hipError_t e_ = hipGetLastError();                                                   \
+        if (e_ == hipSuccess && (debug)) e_ = hipStreamSynchronize(stream);                  \
+        if (e_ != hipSuccess)                                                                \
+            return fail(GSR_ERR_HIP, std::string(name) + ": " + hipGetErrorString(e_));      \
+    } while (0)
+
+// ---- stage profiling (HIP events on the launch stream) ----
+constexpr int kStages = GSR_NUM_STAGES;
+uint32_t g_prof_mask = 0;
+struct EvPair { hipEvent_t a, b; int stage; };
+std::vector<EvPair> g_ev_pool;
+size_t g_ev_used = 0;
+double g_prof_ms[kStages] = {0};
+int g_prof_cnt[kStages] = {0};
+
+struct StageTimer {
+    EvPair* p = nullptr;
+    hipStream_t s;
+    StageTimer(int stage, hipStream_t st) : s(st) {
+        if (!(g_prof_mask & (1u << stage))) return;
+        if (g_ev_used == g_ev_pool.size()) {
+            EvPair e;
+            if (hipEventCreate(&e.a) != hipSuccess || hipEventCreate(&e.b) != hipSuccess) return;
+            g_ev_pool.push_back(e);
+        }
+        p = &g_ev_pool[g_ev_used++];
+        p->stage = stage;
+        hipEventRecord(p->a, s);
+    }
+    ~StageTimer() {
+        if (p) hipEventRecord(p->b, s);
+    }
+};
+
+inline size_t align_up(size_t x) { return (x + 255) & ~(size_t)255; }
+
+template <typename T>
+inline T* take(char* base, size_t& off, size_t count) {
+    off = align_up(off);
+    T* p = base ? reinterpret_cast<T*>(base + off) : nullptr;
+    off += sizeof(T) * count;
+    return p;
+}
+
+}  // namespace
+
+namespace gsr {
+
+size_t carve_geom(char* base, const Dims& d, GeomArena* g) {
+    const size_t n = (size_t)d.B * d.P;
+    size_t off = 0;
+    GeomArena a;
+    a.ctrl = take<uint32_t>(base, off, kCtrlWords);
+    a.depth = take<float>(base, off, n);
+    a.invdepth = take<float>(base, off, n);
+    a.radii = take<int>(base, off, n);
+    a.means2D = take<float2>(base, off, n);
+    a.cov3D = take<float>(base, off, 6 * n);
+    a.conic = take<float4>(base, off, n);
+    a.rect = take<uint2>(base, off, n);
+    a.ext = take<float2>(base, off, n);
+    a.tiles = take<uint32_t>(base, off, n);
+    a.offsets = take<uint32_t>(base, off, n);
+    a.blocksums = take<uint32_t>(base, off, (size_t)d.B * d.nblk + 1);
+    if (g) *g = a;
+    return align_up(off) + 256;
+}
+
+size_t carve_image(char* base, const Dims& d, ImageArena* im) {
+    const size_t npx = (size_t)d.B * d.W * d.H;
+    const size_t nt = (size_t)d.B * d.T;
+    size_t off = 0;
+    ImageArena a;
+    a.final_T = take<float>(base, off, npx);
+    a.n_contrib = take<uint32_t>(base, off, npx);
+    a.ranges = take<uint2>(base, off, nt);
+    a.tile_count = take<uint32_t>(base, off, nt);
+    a.large_list = take<uint32_t>(base, off, nt);
+    if (im) *im = a;
+    return align_up(off) + 256;
+}
+
+size_t carve_bin(char* base, int64_t R, BinArena* b) {
+    const size_t n = (size_t)(R > 0 ? R : 1);
+    size_t off = 0;
+    BinArena a;
+    a.point_list = take<uint32_t>(base, off, n);
+    a.keys = take<uint64_t>(base, off, n);
+    a.inst_slot = take<uint32_t>(base, off, n);
+    if (b) *b = a;
+    return align_up(off) + 256;
+}
+
+}  // namespace gsr
+
+namespace {
+
+// Shared forward sequence once R is known and the binning arena exists.
+int run_binning_and_render(const Dims& d, const Inputs& in, const GeomArena& g, const ImageArena& im,
+                           const BinArena& bn, const Outputs& o, int debug, hipStream_t s) {
+    { StageTimer st_(2, s); launch_bin_count(d, g, im, bn, s); }
+    STAGE(debug, s, "bin_count");
+    { StageTimer st_(3, s); launch_tile_scan(d, g, im, s); }
+    STAGE(debug, s, "tile_scan");
+    { StageTimer st_(4, s); launch_bin_scatter(d, g, im, bn, s); }
+    STAGE(debug, s, "bin_scatter");
+    { StageTimer st_(5, s); launch_tile_sort(d, g, im, bn, s); }
+    STAGE(debug, s, "tile_sort");
+    { StageTimer st_(6, s); launch_render_fwd(d, in, g, im, bn, o, g_exact_exp != 0, s); }
+    STAGE(debug, s, "render_fwd");
+    return 0;
+}
+
+}  // namespace
+
+extern "C" {
+
+const char* gsr_version(void) { return "gsr-gfx950 0.1"; }
+const char* gsr_last_error(void) { return g_err.c_str(); }
+int gsr_set_exact_exp(int on) {
+    int prev = g_exact_exp;
+    g_exact_exp = on ? 1 : 0;
+    return prev;
+}
+
+size_t gsr_geometry_bytes(int P) { return carve_geom(nullptr, make_dims(1, P, 16, 16), nullptr); }
+size_t gsr_image_bytes(int width, int height) {
+    return carve_image(nullptr, make_dims(1, 1, width, height), nullptr);
+}
+size_t gsr_binning_bytes(int64_t R) { return carve_bin(nullptr, R, nullptr); }
+
+int gsr_mark_visible(int P, const float* means3D, const float* viewmatrix, const float* projmatrix,
+                     uint8_t* present, void* stream) {
+    if (P < 0) return fail(GSR_ERR_ARG, "P < 0");
+    launch_mark_visible(P, means3D, viewmatrix, projmatrix, present, (hipStream_t)stream);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return fail(GSR_ERR_HIP, std::string("mark_visible: ") + hipGetErrorString(e));
+    return 0;
+}
+
+int gsr_forward(gsr_alloc_fn geometryBuffer, gsr_alloc_fn binningBuffer, gsr_alloc_fn imageBuffer,
+                void* alloc_ctx, int P, int D, int M, const float* background, int width, int height,
+                const float* means3D, const float* shs, const float* colors_precomp,
+                const float* opacities, const float* scales, float scale_modifier,
+                const float* rotations, const float* cov3D_precomp, const float* viewmatrix,
+                const float* projmatrix, const float* cam_pos, float tan_fovx, float tan_fovy,
+                int prefiltered, float* out_color, float* depth, int antialiasing, int* radii,
+                int debug, void* stream) {
+    (void)D; (void)M; (void)shs; (void)cam_pos;
+    hipStream_t s = (hipStream_t)stream;
+    if (P < 0 || width <= 0 || height <= 0) return fail(GSR_ERR_ARG, "bad P/width/height");
+    if (width > 16 * 65535 || height > 16 * 65535) return fail(GSR_ERR_ARG, "image too large");
+    const Dims d = make_dims(1, P, width, height);
+    GeomArena g;
+    ImageArena im;
+    char* gb = geometryBuffer(alloc_ctx, carve_geom(nullptr, d, nullptr));
+    if (!gb) return fail(GSR_ERR_ALLOC, "geometryBuffer allocation failed");
+    carve_geom(gb, d, &g);
+    char* ib = imageBuffer(alloc_ctx, carve_image(nullptr, d, nullptr));
+    if (!ib) return fail(GSR_ERR_ALLOC, "imageBuffer allocation failed");
+    carve_image(ib, d, &im);
+    if (colors_precomp == nullptr)
+        return fail(GSR_ERR_NO_COLORS, "For non-RGB, provide precomputed Gaussian colors!");
+    if (((uintptr_t)colors_precomp & 15) != 0) return fail(GSR_ERR_ARG, "colors_precomp must be 16-byte aligned");
+    if (cov3D_precomp == nullptr && (scales == nullptr || rotations == nullptr))
+        return fail(GSR_ERR_ARG, "scales/rotations or cov3D_precomp required");
+
+    Inputs in{};
+    in.means3D = means3D; in.s_means = 0;
+    in.scales = scales; in.s_scales = 0;
+    in.rot = rotations; in.s_rot = 0;
+    in.opac = opacities; in.s_opac = 0;
+    in.cov3D_pre = cov3D_precomp; in.s_cov = 0;
+    in.colors = colors_precomp; in.s_colors = 0;
+    in.view = viewmatrix; in.proj = projmatrix;
+    in.tan_dev = nullptr; in.tanx = tan_fovx; in.tany = tan_fovy;
+    in.bg = background; in.s_bg = 0;
+    in.scale_mod = scale_modifier;
+    in.prefiltered = prefiltered; in.antialiasing = antialiasing;
+    Outputs o{out_color, depth, radii};
+
+    HIP_TRY(hipMemsetAsync(g.ctrl, 0, kCtrlWords * 4, s));
+    HIP_TRY(hipMemsetAsync(im.tile_count, 0, (size_t)d.T * 4, s));
+    { StageTimer st_(0, s); launch_preprocess(d, in, g, o, s); }
+    STAGE(debug, s, "preprocess");
+    { StageTimer st_(1, s); launch_scan_blocksums(d, g, (int64_t)0xFFFFFFF0u, s); }
+    STAGE(debug, s, "scan");
+    uint32_t ctrl_h[4] = {0, 0, 0, 0};
+    HIP_TRY(hipMemcpyAsync(ctrl_h, g.ctrl, sizeof(ctrl_h), hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    if (ctrl_h[kCtrlError] & 1u)
+        return fail(GSR_ERR_PREFILTERED, "Point is filtered although prefiltered is set. This shouldn't happen!");
+    if (ctrl_h[kCtrlOverflow]) return fail(GSR_ERR_CAPACITY, "instance count exceeds 2^32");
+    const int64_t R = ctrl_h[kCtrlRLo];
+    char* bb = binningBuffer(alloc_ctx, carve_bin(nullptr, R, nullptr));
+    if (!bb) return fail(GSR_ERR_ALLOC, "binningBuffer allocation failed");
+    BinArena bn;
+    carve_bin(bb, R, &bn);
+    int rc = run_binning_and_render(d, in, g, im, bn, o, debug, s);
+    if (rc < 0) return rc;
+    return (int)R;
+}
+
+int gsr_backward(int P, int D, int M, int R, const float* background, int width, int height,
+                 const float* means3D, const float* shs, const float* colors_precomp,
+                 const float* opacities, const float* scales, float scale_modifier,
+                 const float* rotations, const float* cov3D_precomp, const float* viewmatrix,
+                 const float* projmatrix, const float* campos, float tan_fovx, float tan_fovy,
+                 const int* radii, char* geom_buffer, char* binning_buffer, char* image_buffer,
+                 const float* dL_dpix, const float* dL_invdepths, float* dL_dmean2D,
+                 float* dL_dconic, float* dL_dopacity, float* dL_dcolor, float* dL_dinvdepth,
+                 float* dL_dmean3D, float* dL_dcov3D, float* dL_dsh, float* dL_dscale,
+                 float* dL_drot, int antialiasing, int debug, void* stream) {
+    (void)D; (void)M; (void)shs; (void)campos; (void)radii; (void)dL_dsh;
+    hipStream_t s = (hipStream_t)stream;
+    if (P <= 0) return 0;
+    if (colors_precomp == nullptr)
+        return fail(GSR_ERR_NO_COLORS, "For non-RGB, provide precomputed Gaussian colors!");
+    const Dims d = make_dims(1, P, width, height);
+    GeomArena g;
+    ImageArena im;
+    BinArena bn;
+    carve_geom(geom_buffer, d, &g);
+    carve_image(image_buffer, d, &im);
+    carve_bin(binning_buffer, R, &bn);
+    Inputs in{};
+    in.means3D = means3D;
+    in.scales = scales;
+    in.rot = rotations;
+    in.opac = opacities;
+    in.cov3D_pre = cov3D_precomp;
+    in.colors = colors_precomp;
+    in.view = viewmatrix; in.proj = projmatrix;
+    in.tan_dev = nullptr; in.tanx = tan_fovx; in.tany = tan_fovy;
+    in.bg = background;
+    in.scale_mod = scale_modifier;
+    in.antialiasing = antialiasing;
+    Grads gr{};
+    gr.dL_dpix = dL_dpix;
+    gr.dL_dinvdepth = dL_invdepths;
+    gr.dL_dmean2D = dL_dmean2D;
+    gr.dL_dconic = dL_dconic;
+    gr.dL_dopacity = dL_dopacity;
+    gr.dL_dcolors = dL_dcolor;
+    gr.dL_dinvdepth_g = dL_invdepths ? dL_dinvdepth : nullptr;
+    gr.dL_dmeans3D = dL_dmean3D;
+    gr.dL_dcov3D = dL_dcov3D;
+    gr.dL_dscale = (cov3D_precomp == nullptr) ? dL_dscale : nullptr;
+    gr.dL_drot = (cov3D_precomp == nullptr) ? dL_drot : nullptr;
+    { StageTimer st_(7, s); launch_render_bwd(d, in, g, im, bn, gr, g_exact_exp != 0, s); }
+    STAGE(debug, s, "render_bwd");
+    { StageTimer st_(8, s); launch_preprocess_bwd(d, in, g, gr, s); }
+    STAGE(debug, s, "preprocess_bwd");
+    return 0;
+}
+
+size_t gsr_batch_workspace_bytes(int B, int P, int width, int height, int64_t R_capacity) {
+    const Dims d = make_dims(B, P, width, height);
+    return carve_geom(nullptr, d, nullptr) + carve_image(nullptr, d, nullptr) +
+           carve_bin(nullptr, R_capacity, nullptr);
+}
+
+static void carve_workspace(char* ws, const Dims& d, int64_t R_cap, GeomArena* g, ImageArena* im,
+                            BinArena* bn) {
+    const size_t gsz = carve_geom(nullptr, d, nullptr);
+    const size_t isz = carve_image(nullptr, d, nullptr);
+    carve_geom(ws, d, g);
+    carve_image(ws + gsz, d, im);
+    carve_bin(ws + gsz + isz, R_cap, bn);
+}
+
+int gsr_forward_batch(int B, int P, int width, int height, const float* means3D,
+                      int64_t means_stride, const float* colors, int64_t colors_stride,
+                      const float* opacities, int64_t opac_stride, const float* scales,
+                      int64_t scales_stride, const float* rotations, int64_t rot_stride,
+                      float scale_modifier, const float* viewmatrices, const float* projmatrices,
+                      const float* tanfov, const float* backgrounds, int64_t bg_stride,
+                      char* workspace, int64_t R_capacity, float* out_color, float* out_invdepth,
+                      int* radii, int antialiasing, void* stream) {
+    hipStream_t s = (hipStream_t)stream;
+    if (B <= 0 || P <= 0 || width <= 0 || height <= 0 || !workspace || !tanfov)
+        return fail(GSR_ERR_ARG, "bad batch arguments");
+    if (!colors) return fail(GSR_ERR_NO_COLORS, "For non-RGB, provide precomputed Gaussian colors!");
+    if (((uintptr_t)colors & 15) != 0 || ((colors_stride * 4) & 15) != 0)
+        return fail(GSR_ERR_ARG, "colors must be 16-byte aligned per frame");
+    const Dims d = make_dims(B, P, width, height);
+    GeomArena g;
+    ImageArena im;
+    BinArena bn;
+    carve_workspace(workspace, d, R_capacity, &g, &im, &bn);
+    Inputs in{};
+    in.means3D = means3D; in.s_means = means_stride;
+    in.scales = scales; in.s_scales = scales_stride;
+    in.rot = rotations; in.s_rot = rot_stride;
+    in.opac = opacities; in.s_opac = opac_stride;
+    in.cov3D_pre = nullptr; in.s_cov = 0;
+    in.colors = colors; in.s_colors = colors_stride;
+    in.view = viewmatrices; in.proj = projmatrices;
+    in.tan_dev = tanfov;
+    in.bg = backgrounds; in.s_bg = bg_stride;
+    in.scale_mod = scale_modifier;
+    in.prefiltered = 0; in.antialiasing = antialiasing;
+    Outputs o{out_color, out_invdepth, radii};
+    HIP_TRY(hipMemsetAsync(g.ctrl, 0, kCtrlWords * 4, s));
+    HIP_TRY(hipMemsetAsync(im.tile_count, 0, (size_t)d.B * d.T * 4, s));
+    { StageTimer st_(0, s); launch_preprocess(d, in, g, o, s); }
+    { StageTimer st_(1, s); launch_scan_blocksums(d, g, R_capacity, s); }
+    int rc = run_binning_and_render(d, in, g, im, bn, o, 0, s);
+    if (rc < 0) return rc;
+    return 0;
+}
+
+int gsr_backward_batch(int B, int P, int width, int height, const float* means3D,
+                       int64_t means_stride, const float* colors, int64_t colors_stride,
+                       const float* opacities, int64_t opac_stride, const float* scales,
+                       int64_t scales_stride, const float* rotations, int64_t rot_stride,
+                       float scale_modifier, const float* viewmatrices, const float* projmatrices,
+                       const float* tanfov, const float* backgrounds, int64_t bg_stride,
+                       char* workspace, int64_t R_capacity, const float* dL_dpix,
+                       const float* dL_dinvdepth, float* dL_dmean2D, float* dL_dconic,
+                       float* dL_dopacity, float* dL_dcolor, float* dL_dinvdepth_g,
+                       float* dL_dmean3D, float* dL_dcov3D, float* dL_dscale, float* dL_drot,
+                       int antialiasing, void* stream) {
+    hipStream_t s = (hipStream_t)stream;
+    if (B <= 0 || P <= 0 || !workspace || !tanfov) return fail(GSR_ERR_ARG, "bad batch arguments");
+    const Dims d = make_dims(B, P, width, height);
+    GeomArena g;
+    ImageArena im;
+    BinArena bn;
+    carve_workspace(workspace, d, R_capacity, &g, &im, &bn);
+    Inputs in{};
+    in.means3D = means3D; in.s_means = means_stride;
+    in.scales = scales; in.s_scales = scales_stride;
+    in.rot = rotations; in.s_rot = rot_stride;
+    in.opac = opacities; in.s_opac = opac_stride;
+    in.colors = colors; in.s_colors = colors_stride;
+    in.view = viewmatrices; in.proj = projmatrices;
+    in.tan_dev = tanfov;
+    in.bg = backgrounds; in.s_bg = bg_stride;
+    in.scale_mod = scale_modifier;
+    in.antialiasing = antialiasing;
+    Grads gr{};
+    gr.dL_dpix = dL_dpix;
+    gr.dL_dinvdepth = dL_dinvdepth;
+    gr.dL_dmean2D = dL_dmean2D;
+    gr.dL_dconic = dL_dconic;
+    gr.dL_dopacity = dL_dopacity;
+    gr.dL_dcolors = dL_dcolor;
+    gr.dL_dinvdepth_g = dL_dinvdepth ? dL_dinvdepth_g : nullptr;
+    gr.dL_dmeans3D = dL_dmean3D;
+    gr.dL_dcov3D = dL_dcov3D;
+    gr.dL_dscale = dL_dscale;
+    gr.dL_drot = dL_drot;
+    { StageTimer st_(7, s); launch_render_bwd(d, in, g, im, bn, gr, g_exact_exp != 0, s); }
+    { StageTimer st_(8, s); launch_preprocess_bwd(d, in, g, gr, s); }
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return fail(GSR_ERR_HIP, std::string("backward_batch: ") + hipGetErrorString(e));
+    return 0;
+}
+
+int gsr_profile_enable(uint32_t stage_mask) {
+    g_prof_mask = stage_mask;
+    return 0;
+}
+
+int gsr_profile_read(double* ms, int* counts, int n) {
+    for (size_t i = 0; i < g_ev_used; i++) {
+        EvPair& e = g_ev_pool[i];
+        HIP_TRY(hipEventSynchronize(e.b));
+        float t = 0.f;
+        HIP_TRY(hipEventElapsedTime(&t, e.a, e.b));
+        g_prof_ms[e.stage] += t;
+        g_prof_cnt[e.stage] += 1;
+    }
+    g_ev_used = 0;
+    for (int i = 0; i < n && i < kStages; i++) {
+        if (ms) ms[i] = g_prof_ms[i];
+        if (counts) counts[i] = g_prof_cnt[i];
+    }
+    for (int i = 0; i < kStages; i++) { g_prof_ms[i] = 0; g_prof_cnt[i] = 0; }
+    return 0;
+}
+
+int gsr_batch_status(const char* workspace, int B, int P, int64_t* R_total, int* overflow,
+                     void* stream) {
+    hipStream_t s = (hipStream_t)stream;
+    uint32_t ctrl_h[4] = {0, 0, 0, 0};
+    HIP_TRY(hipMemcpyAsync(ctrl_h, workspace, sizeof(ctrl_h), hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    (void)B; (void)P;
+    if (R_total) *R_total = ctrl_h[kCtrlRLo];
+    if (overflow) *overflow = ctrl_h[kCtrlOverflow] ? 1 : 0;
+    return 0;
+}
+
+}  // extern "C"

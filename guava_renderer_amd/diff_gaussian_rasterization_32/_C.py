@@ -1,0 +1,174 @@
+"""The native `_C` surface of diff_gaussian_rasterization_32, over the gfx950 C ABI (libgsr.so).
+
+Same functions, positional signatures, return tuples and error behaviour as the reference's
+pybind module (/root/reference/submodules/diff-gaussian-rasterization-32/ext.cpp:15-19,
+rasterize_points.cu:36-124 (forward), :127-223 (backward), :225-244 (mark_visible)).
+Tensors are allocated by the torch (HIP) caching allocator; the three scratch buffers are uint8
+tensors resized through the C ABI's allocator callbacks, exactly as resizeFunctional does
+(rasterize_points.cu:27-33), and handed back to backward by autograd.
+Differences by design: scratch buffers live on means3D's device (the reference uses the current
+device); kernels run on the current HIP stream of that device.
+"""
+import ctypes
+
+import torch
+
+from .. import _lib
+
+NUM_CHANNELS = 32
+
+
+def _ptr(t):
+    """Device pointer of a tensor, or None for an empty tensor (reference: data<float>() of an
+    empty tensor is nullptr)."""
+    if t is None or t.numel() == 0:
+        return None
+    return t.data_ptr()
+
+
+def _dev_f32(t, device, name):
+    if t is None or t.numel() == 0:
+        return t
+    if t.device != device:
+        raise RuntimeError(f"{name} must be on {device} (got {t.device})")
+    if t.dtype != torch.float32:
+        raise RuntimeError(f"{name} must be float32 (got {t.dtype})")
+    return t.contiguous()
+
+
+def _stream(device):
+    return ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)
+
+
+class _Resizer:
+    """Holds a growable uint8 tensor; called by the C ABI with the requested size."""
+
+    def __init__(self, device):
+        self.t = torch.empty((0,), dtype=torch.uint8, device=device)
+        self.cb = _lib.ALLOC_FN(self._cb)
+
+    def _cb(self, ctx, n):
+        self.t.resize_((int(n),))
+        return self.t.data_ptr()
+
+
+def rasterize_gaussians(background, means3D, colors, opacity, scales, rotations, scale_modifier,
+                        cov3D_precomp, viewmatrix, projmatrix, tan_fovx, tan_fovy, image_height,
+                        image_width, sh, degree, campos, prefiltered, antialiasing, debug):
+    """RasterizeGaussiansCUDA (rasterize_points.cu:36-124).  Returns
+    (num_rendered, color[32,H,W], radii[P] int32, geomBuffer, binningBuffer, imgBuffer, invdepth[1,H,W])."""
+    if means3D.ndimension() != 2 or means3D.size(1) != 3:
+        raise RuntimeError("means3D must have dimensions (num_points, 3)")
+    P = int(means3D.size(0))
+    H = int(image_height)
+    W = int(image_width)
+    dev = means3D.device
+    fopts = dict(dtype=torch.float32, device=dev)
+    # the render pass writes every pixel when P > 0 (empty tiles get the background), so only the
+    # P == 0 case needs the reference's zero fill (rasterize_points.cu:69-73)
+    alloc = torch.zeros if P == 0 else torch.empty
+    out_color = alloc((NUM_CHANNELS, H, W), **fopts)
+    out_invdepth = alloc((1, H, W), **fopts)
+    radii = torch.zeros((P,), dtype=torch.int32, device=dev)
+    geom, binning, img = _Resizer(dev), _Resizer(dev), _Resizer(dev)
+    rendered = 0
+    if P != 0:
+        if dev.type != "cuda":
+            raise RuntimeError("rasterize_gaussians needs tensors on a HIP (cuda) device; "
+                               "there is no CPU implementation")
+        L = _lib.load()
+        M = int(sh.size(1)) if (sh is not None and sh.numel() != 0 and sh.size(0) != 0) else 0
+        means3D = _dev_f32(means3D, dev, "means3D")
+        colors = _dev_f32(colors, dev, "colors_precomp")
+        if colors is not None and colors.numel() and colors.data_ptr() % 16:
+            colors = colors.clone()
+        opacity = _dev_f32(opacity, dev, "opacities")
+        scales = _dev_f32(scales, dev, "scales")
+        rotations = _dev_f32(rotations, dev, "rotations")
+        cov3D_precomp = _dev_f32(cov3D_precomp, dev, "cov3D_precomp")
+        background = _dev_f32(background, dev, "bg")
+        viewmatrix = _dev_f32(viewmatrix, dev, "viewmatrix")
+        projmatrix = _dev_f32(projmatrix, dev, "projmatrix")
+        with torch.cuda.device(dev):
+            rc = L.gsr_forward(
+                geom.cb, binning.cb, img.cb, None, P, int(degree), M, _ptr(background), W, H,
+                _ptr(means3D), _ptr(sh), _ptr(colors), _ptr(opacity), _ptr(scales),
+                float(scale_modifier), _ptr(rotations), _ptr(cov3D_precomp), _ptr(viewmatrix),
+                _ptr(projmatrix), _ptr(campos), float(tan_fovx), float(tan_fovy),
+                int(bool(prefiltered)), out_color.data_ptr(), out_invdepth.data_ptr(),
+                int(bool(antialiasing)), radii.data_ptr(), int(bool(debug)), _stream(dev))
+        rendered = _lib.check(rc, "rasterize_gaussians")
+    return rendered, out_color, radii, geom.t, binning.t, img.t, out_invdepth
+
+
+def rasterize_gaussians_backward(background, means3D, radii, colors, opacities, scales, rotations,
+                                 scale_modifier, cov3D_precomp, viewmatrix, projmatrix, tan_fovx,
+                                 tan_fovy, dL_dout_color, dL_dout_invdepth, sh, degree, campos,
+                                 geomBuffer, R, binningBuffer, imageBuffer, antialiasing, debug):
+    """RasterizeGaussiansBackwardCUDA (rasterize_points.cu:127-223).  Returns
+    (dL_dmeans2D, dL_dcolors, dL_dopacity, dL_dmeans3D, dL_dcov3D, dL_dsh, dL_dscales, dL_drotations)."""
+    P = int(means3D.size(0))
+    H = int(dL_dout_color.size(1))
+    W = int(dL_dout_color.size(2))
+    M = int(sh.size(1)) if (sh is not None and sh.numel() != 0 and sh.size(0) != 0) else 0
+    dev = means3D.device
+    o = dict(dtype=torch.float32, device=dev)
+    dL_dmeans3D = torch.zeros((P, 3), **o)
+    dL_dmeans2D = torch.zeros((P, 3), **o)
+    dL_dcolors = torch.zeros((P, NUM_CHANNELS), **o)
+    dL_dconic = torch.zeros((P, 2, 2), **o)
+    dL_dopacity = torch.zeros((P, 1), **o)
+    dL_dcov3D = torch.zeros((P, 6), **o)
+    dL_dsh = torch.zeros((P, M, 3), **o)
+    dL_dscales = torch.zeros((P, 3), **o)
+    dL_drotations = torch.zeros((P, 4), **o)
+    dL_dinvdepths = torch.zeros((0, 1), **o)
+    inv_pix = None
+    if dL_dout_invdepth is not None and dL_dout_invdepth.numel() != 0 and dL_dout_invdepth.size(0) != 0:
+        dL_dinvdepths = torch.zeros((P, 1), **o)
+        inv_pix = _dev_f32(dL_dout_invdepth, dev, "dL_dout_invdepth")
+    if P != 0:
+        L = _lib.load()
+        dL_dout_color = _dev_f32(dL_dout_color, dev, "dL_dout_color")
+        colors = _dev_f32(colors, dev, "colors_precomp")
+        if colors is not None and colors.numel() and colors.data_ptr() % 16:
+            colors = colors.clone()
+        means3D = _dev_f32(means3D, dev, "means3D")
+        opacities = _dev_f32(opacities, dev, "opacities")
+        scales = _dev_f32(scales, dev, "scales")
+        rotations = _dev_f32(rotations, dev, "rotations")
+        cov3D_precomp = _dev_f32(cov3D_precomp, dev, "cov3D_precomp")
+        background = _dev_f32(background, dev, "bg")
+        viewmatrix = _dev_f32(viewmatrix, dev, "viewmatrix")
+        projmatrix = _dev_f32(projmatrix, dev, "projmatrix")
+        with torch.cuda.device(dev):
+            rc = L.gsr_backward(
+                P, int(degree), M, int(R), _ptr(background), W, H, _ptr(means3D), _ptr(sh),
+                _ptr(colors), _ptr(opacities), _ptr(scales), float(scale_modifier), _ptr(rotations),
+                _ptr(cov3D_precomp), _ptr(viewmatrix), _ptr(projmatrix), _ptr(campos),
+                float(tan_fovx), float(tan_fovy), _ptr(radii), _ptr(geomBuffer), _ptr(binningBuffer),
+                _ptr(imageBuffer), dL_dout_color.data_ptr(), _ptr(inv_pix), dL_dmeans2D.data_ptr(),
+                dL_dconic.data_ptr(), dL_dopacity.data_ptr(), dL_dcolors.data_ptr(),
+                _ptr(dL_dinvdepths), dL_dmeans3D.data_ptr(), dL_dcov3D.data_ptr(), _ptr(dL_dsh),
+                dL_dscales.data_ptr(), dL_drotations.data_ptr(), int(bool(antialiasing)),
+                int(bool(debug)), _stream(dev))
+        _lib.check(rc, "rasterize_gaussians_backward")
+    return (dL_dmeans2D, dL_dcolors, dL_dopacity, dL_dmeans3D, dL_dcov3D, dL_dsh, dL_dscales,
+            dL_drotations)
+
+
+def mark_visible(means3D, viewmatrix, projmatrix):
+    """markVisible (rasterize_points.cu:225-244): bool[P], view-space z > 0.2."""
+    P = int(means3D.size(0))
+    dev = means3D.device
+    present = torch.zeros((P,), dtype=torch.bool, device=dev)
+    if P != 0:
+        L = _lib.load()
+        means3D = _dev_f32(means3D, dev, "means3D")
+        viewmatrix = _dev_f32(viewmatrix, dev, "viewmatrix")
+        projmatrix = _dev_f32(projmatrix, dev, "projmatrix")
+        with torch.cuda.device(dev):
+            rc = L.gsr_mark_visible(P, means3D.data_ptr(), viewmatrix.data_ptr(),
+                                    projmatrix.data_ptr(), present.data_ptr(), _stream(dev))
+        _lib.check(rc, "mark_visible")
+    return present

@@ -1,0 +1,137 @@
+/*
+ * gsr.h -- C ABI of the MI355X (gfx950) 32-channel Gaussian-splat rasterizer.
+ *
+ * Drop-in boundary for GUAVA's diff-gaussian-rasterization-32.  Each entry point replaces one
+ * function of the reference's native layer
+ * (/root/reference/submodules/diff-gaussian-rasterization-32/):
+ *
+ *   gsr_forward      <- CudaRasterizer::Rasterizer::forward     cuda_rasterizer/rasterizer.h:31-61
+ *                       (driver: cuda_rasterizer/rasterizer_impl.cu:198-341)
+ *   gsr_backward     <- CudaRasterizer::Rasterizer::backward    cuda_rasterizer/rasterizer.h:63-91
+ *                       (driver: cuda_rasterizer/rasterizer_impl.cu:345-450)
+ *   gsr_mark_visible <- CudaRasterizer::Rasterizer::markVisible cuda_rasterizer/rasterizer.h:24-29
+ *                       (kernel: rasterizer_impl.cu:54-66)
+ *   gsr_forward_batch / gsr_backward_batch: B frames in one launch set with a preallocated
+ *                       workspace and no host synchronisation (replaces the per-frame Python loop
+ *                       of models/UbodyAvatar/gaussian_render.py:37-67).
+ *
+ * Conventions: every pointer is a device pointer (HBM) unless stated; float32 everywhere; the
+ * layouts are the reference's (means3D [P,3], rotations [P,4] wxyz, colors [P,32], viewmatrix /
+ * projmatrix 4x4 column-major as produced by utils/graphics_utils.py:44-50, out_color [32,H,W]).
+ * `stream` is a hipStream_t (NULL = default stream).  Return codes: >= 0 success (forward:
+ * num_rendered), < 0 = -gsr_status; gsr_last_error() returns a message for the last failure.
+ */
+#ifndef GSR_H
+#define GSR_H
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define GSR_NUM_CHANNELS 32
+#define GSR_BLOCK_X 16
+#define GSR_BLOCK_Y 16
+
+typedef enum {
+    GSR_OK = 0,
+    GSR_ERR_ARG = 1,          /* invalid argument / shape */
+    GSR_ERR_HIP = 2,          /* HIP runtime error (message in gsr_last_error) */
+    GSR_ERR_PREFILTERED = 3,  /* prefiltered=true and a point was culled (reference: __trap) */
+    GSR_ERR_NO_COLORS = 4,    /* colors_precomp missing with 32 channels (rasterizer_impl.cu:244-247) */
+    GSR_ERR_CAPACITY = 5,     /* batch: instances exceed the workspace's R capacity */
+    GSR_ERR_ALLOC = 6         /* allocator callback returned NULL */
+} gsr_status;
+
+/* Mirrors the reference's std::function<char*(size_t)> buffer resizers (rasterize_points.cu:27-33):
+ * must return a device buffer of at least `bytes` bytes that stays alive until backward. */
+typedef char* (*gsr_alloc_fn)(void* ctx, size_t bytes);
+
+const char* gsr_version(void);
+const char* gsr_last_error(void);
+
+/* Blend exponent: 1 = deterministic polynomial exp, bit-identical to the CPU oracle (default);
+ * 0 = hardware v_exp_f32.  Returns the previous setting. */
+int gsr_set_exact_exp(int on);
+
+/* Scratch sizes used by gsr_forward (the three resizer requests). */
+size_t gsr_geometry_bytes(int P);
+size_t gsr_image_bytes(int width, int height);
+size_t gsr_binning_bytes(int64_t R);
+
+int gsr_mark_visible(int P, const float* means3D, const float* viewmatrix, const float* projmatrix,
+                     uint8_t* present, void* stream);
+
+/* Rasterizer::forward.  D, M, shs, cam_pos are accepted for signature parity (32 channels need
+ * colors_precomp, as in the reference).  out_color [32,H,W], depth = inverse-depth image [H,W]
+ * (may be NULL), radii [P] (may be NULL).  Returns num_rendered or -status. */
+int gsr_forward(gsr_alloc_fn geometryBuffer, gsr_alloc_fn binningBuffer, gsr_alloc_fn imageBuffer,
+                void* alloc_ctx, int P, int D, int M, const float* background, int width, int height,
+                const float* means3D, const float* shs, const float* colors_precomp,
+                const float* opacities, const float* scales, float scale_modifier,
+                const float* rotations, const float* cov3D_precomp, const float* viewmatrix,
+                const float* projmatrix, const float* cam_pos, float tan_fovx, float tan_fovy,
+                int prefiltered, float* out_color, float* depth, int antialiasing, int* radii,
+                int debug, void* stream);
+
+/* Rasterizer::backward.  Gradient buffers are accumulated into and must be zeroed by the caller
+ * (the reference's torch::zeros, rasterize_points.cu:163-179): dL_dmean2D [P,3], dL_dconic [P,4],
+ * dL_dopacity [P], dL_dcolor [P,32], dL_dinvdepth [P] (NULL when dL_invdepths is NULL),
+ * dL_dmean3D [P,3], dL_dcov3D [P,6], dL_dscale [P,3], dL_drot [P,4]; dL_dsh is unused (no SH
+ * path with 32 channels). */
+int gsr_backward(int P, int D, int M, int R, const float* background, int width, int height,
+                 const float* means3D, const float* shs, const float* colors_precomp,
+                 const float* opacities, const float* scales, float scale_modifier,
+                 const float* rotations, const float* cov3D_precomp, const float* viewmatrix,
+                 const float* projmatrix, const float* campos, float tan_fovx, float tan_fovy,
+                 const int* radii, char* geom_buffer, char* binning_buffer, char* image_buffer,
+                 const float* dL_dpix, const float* dL_invdepths, float* dL_dmean2D,
+                 float* dL_dconic, float* dL_dopacity, float* dL_dcolor, float* dL_dinvdepth,
+                 float* dL_dmean3D, float* dL_dcov3D, float* dL_dsh, float* dL_dscale,
+                 float* dL_drot, int antialiasing, int debug, void* stream);
+
+/* ---- batched multi-frame path (B frames, one launch per stage, capture-safe) ----
+ * Per-frame inputs use an element stride between frames (0 = shared by every frame).
+ * viewmatrices/projmatrices: [B,16]; tanfov: [B,2] (x,y); backgrounds: [B,32] with bg_stride.
+ * workspace: gsr_batch_workspace_bytes(B,P,W,H,R_capacity) bytes of device memory, reused by
+ * gsr_backward_batch.  Outputs: out_color [B,32,H,W], out_invdepth [B,H,W] (or NULL),
+ * radii [B,P] (or NULL).  No host synchronisation: call gsr_batch_status() to learn R and
+ * whether the capacity overflowed (then nothing was rendered). */
+size_t gsr_batch_workspace_bytes(int B, int P, int width, int height, int64_t R_capacity);
+int gsr_forward_batch(int B, int P, int width, int height, const float* means3D,
+                      int64_t means_stride, const float* colors, int64_t colors_stride,
+                      const float* opacities, int64_t opac_stride, const float* scales,
+                      int64_t scales_stride, const float* rotations, int64_t rot_stride,
+                      float scale_modifier, const float* viewmatrices, const float* projmatrices,
+                      const float* tanfov, const float* backgrounds, int64_t bg_stride,
+                      char* workspace, int64_t R_capacity, float* out_color, float* out_invdepth,
+                      int* radii, int antialiasing, void* stream);
+int gsr_backward_batch(int B, int P, int width, int height, const float* means3D,
+                       int64_t means_stride, const float* colors, int64_t colors_stride,
+                       const float* opacities, int64_t opac_stride, const float* scales,
+                       int64_t scales_stride, const float* rotations, int64_t rot_stride,
+                       float scale_modifier, const float* viewmatrices, const float* projmatrices,
+                       const float* tanfov, const float* backgrounds, int64_t bg_stride,
+                       char* workspace, int64_t R_capacity, const float* dL_dpix,
+                       const float* dL_dinvdepth, float* dL_dmean2D, float* dL_dconic,
+                       float* dL_dopacity, float* dL_dcolor, float* dL_dinvdepth_g,
+                       float* dL_dmean3D, float* dL_dcov3D, float* dL_dscale, float* dL_drot,
+                       int antialiasing, void* stream);
+/* Stage timing with HIP events recorded on the launch stream around each stage whose bit is set in
+ * `stage_mask` (bit i = stage i: 0 preprocess, 1 block scan, 2 bin count, 3 tile scan,
+ * 4 key scatter, 5 tile sort, 6 render fwd, 7 render bwd, 8 preprocess bwd); 0 disables.
+ * gsr_profile_read synchronises the recorded events, writes the summed milliseconds and launch
+ * counts of the first `n` stages and resets the accumulators. */
+#define GSR_NUM_STAGES 9
+int gsr_profile_enable(uint32_t stage_mask);
+int gsr_profile_read(double* ms, int* counts, int n);
+
+/* Synchronises `stream`; writes the batch's instance count and overflow flag. */
+int gsr_batch_status(const char* workspace, int B, int P, int64_t* R_total, int* overflow,
+                     void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif
