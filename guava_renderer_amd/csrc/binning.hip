@@ -137,11 +137,17 @@ void launch_bin_count(const Dims& d, const GeomArena& g, const ImageArena& im, c
 }
 
 // ---------------------------------------------------------------- 3. tile ranges
+// Also emits the render worklist: every tile of the batch ordered by descending log2 list length
+// (counting sort over 34 buckets; empty tiles last), so persistent render workgroups take the
+// longest tiles first (LPT scheduling) and no XCD is left with only empty tiles.
 __global__ __launch_bounds__(1024) void k_tile_scan(int n, const uint32_t* __restrict__ cnt,
                                                     uint2* __restrict__ ranges, uint32_t* ctrl,
-                                                    uint32_t* large_list) {
+                                                    uint32_t* large_list, uint32_t* work_list) {
+    constexpr int kBuckets = 34;  // bucket 0: longest (2^32..), bucket 33: empty
     __shared__ uint32_t sh[1024 / 64 + 1];
+    __shared__ uint32_t bcount[kBuckets];
     const bool ovf = ctrl[kCtrlOverflow] != 0;
+    if (threadIdx.x < kBuckets) bcount[threadIdx.x] = 0;
     const int per = (n + 1023) / 1024;
     const int beg = threadIdx.x * per;
     const int end = min(n, beg + per);
@@ -149,19 +155,36 @@ __global__ __launch_bounds__(1024) void k_tile_scan(int n, const uint32_t* __res
     if (!ovf)
         for (int i = beg; i < end; i++) s += cnt[i];
     uint32_t total;
-    uint32_t ex = block_excl_scan<uint32_t, 1024>(s, &total, sh);
+    uint32_t ex = block_excl_scan<uint32_t, 1024>(s, &total, sh);  // (barriers order bcount init)
     for (int i = beg; i < end; i++) {
         const uint32_t c = ovf ? 0u : cnt[i];
         // empty tiles keep the reference's memset value (0,0) (rasterizer_impl.cu:313)
         ranges[i] = c ? make_uint2(ex, ex + c) : make_uint2(0u, 0u);
         if (c > (uint32_t)kSortSmallCap) large_list[atomicAdd(&ctrl[kCtrlNumLarge], 1u)] = (uint32_t)i;
+        const int bk = c ? __clz(c) : kBuckets - 1;
+        atomicAdd(&bcount[bk], 1u);
         ex += c;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint32_t acc = 0;
+        for (int k = 0; k < kBuckets; k++) {
+            const uint32_t v = bcount[k];
+            bcount[k] = acc;
+            acc += v;
+        }
+    }
+    __syncthreads();
+    for (int i = beg; i < end; i++) {
+        const uint32_t c = ovf ? 0u : cnt[i];
+        const int bk = c ? __clz(c) : kBuckets - 1;
+        work_list[atomicAdd(&bcount[bk], 1u)] = (uint32_t)i;
     }
 }
 
 void launch_tile_scan(const Dims& d, const GeomArena& g, const ImageArena& im, hipStream_t s) {
     hipLaunchKernelGGL(k_tile_scan, dim3(1), dim3(1024), 0, s, d.B * d.T, im.tile_count, im.ranges,
-                       g.ctrl, im.large_list);
+                       g.ctrl, im.large_list, im.work_list);
 }
 
 // ---------------------------------------------------------------- 4. scatter keys

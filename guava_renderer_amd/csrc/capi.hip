@@ -16,6 +16,8 @@ namespace {
 
 thread_local std::string g_err;
 int g_exact_exp = 1;
+uint32_t* g_render_stats = nullptr;
+int g_dbg = 0;  // debug hook (gsr_debug_render_stats)
 
 int fail(gsr_status st, const std::string& msg) {
     g_err = msg;
@@ -79,6 +81,17 @@ inline T* take(char* base, size_t& off, size_t count) {
 
 namespace gsr {
 
+int persistent_grid(int per_cu) {
+    static int cus = 0;
+    if (cus == 0) {
+        int dev = 0;
+        if (hipGetDevice(&dev) != hipSuccess ||
+            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
+            cus = 256;
+    }
+    return cus * per_cu;
+}
+
 size_t carve_geom(char* base, const Dims& d, GeomArena* g) {
     const size_t n = (size_t)d.B * d.P;
     size_t off = 0;
@@ -91,7 +104,7 @@ size_t carve_geom(char* base, const Dims& d, GeomArena* g) {
     a.cov3D = take<float>(base, off, 6 * n);
     a.conic = take<float4>(base, off, n);
     a.rect = take<uint2>(base, off, n);
-    a.ext = take<float2>(base, off, n);
+    a.rrec = take<float4>(base, off, 4 * n);
     a.tiles = take<uint32_t>(base, off, n);
     a.offsets = take<uint32_t>(base, off, n);
     a.blocksums = take<uint32_t>(base, off, (size_t)d.B * d.nblk + 1);
@@ -109,6 +122,7 @@ size_t carve_image(char* base, const Dims& d, ImageArena* im) {
     a.ranges = take<uint2>(base, off, nt);
     a.tile_count = take<uint32_t>(base, off, nt);
     a.large_list = take<uint32_t>(base, off, nt);
+    a.work_list = take<uint32_t>(base, off, nt);
     if (im) *im = a;
     return align_up(off) + 256;
 }
@@ -210,7 +224,7 @@ int gsr_forward(gsr_alloc_fn geometryBuffer, gsr_alloc_fn binningBuffer, gsr_all
     in.bg = background; in.s_bg = 0;
     in.scale_mod = scale_modifier;
     in.prefiltered = prefiltered; in.antialiasing = antialiasing;
-    Outputs o{out_color, depth, radii};
+    Outputs o{out_color, depth, radii, g_render_stats};
 
     HIP_TRY(hipMemsetAsync(g.ctrl, 0, kCtrlWords * 4, s));
     HIP_TRY(hipMemsetAsync(im.tile_count, 0, (size_t)d.T * 4, s));
@@ -333,7 +347,8 @@ int gsr_forward_batch(int B, int P, int width, int height, const float* means3D,
     in.bg = backgrounds; in.s_bg = bg_stride;
     in.scale_mod = scale_modifier;
     in.prefiltered = 0; in.antialiasing = antialiasing;
-    Outputs o{out_color, out_invdepth, radii};
+    in.dbg = g_dbg;
+    Outputs o{out_color, out_invdepth, radii, g_render_stats};
     HIP_TRY(hipMemsetAsync(g.ctrl, 0, kCtrlWords * 4, s));
     HIP_TRY(hipMemsetAsync(im.tile_count, 0, (size_t)d.B * d.T * 4, s));
     { StageTimer st_(0, s); launch_preprocess(d, in, g, o, s); }
@@ -388,6 +403,17 @@ int gsr_backward_batch(int B, int P, int width, int height, const float* means3D
     { StageTimer st_(8, s); launch_preprocess_bwd(d, in, g, gr, s); }
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return fail(GSR_ERR_HIP, std::string("backward_batch: ") + hipGetErrorString(e));
+    return 0;
+}
+
+int gsr_debug_flags(int flags) {
+    int p = g_dbg;
+    g_dbg = flags;
+    return p;
+}
+
+int gsr_debug_render_stats(uint32_t* device_buffer) {
+    g_render_stats = device_buffer;
     return 0;
 }
 

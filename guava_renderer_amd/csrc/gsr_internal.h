@@ -25,6 +25,8 @@ enum Ctrl : int {
     kCtrlOverflow = 1,   // R > binning capacity
     kCtrlError = 2,      // bit0: prefiltered point culled
     kCtrlNumLarge = 3,   // tiles whose list exceeds kSortSmallCap
+    kCtrlRenderHead = 4, // render worklist dequeue counter
+    kCtrlBwdHead = 5,    // render-backward worklist dequeue counter
     kCtrlWords = 64
 };
 
@@ -37,7 +39,7 @@ struct GeomArena {
     float* cov3D;
     float4* conic;
     uint2* rect;          // (xmin | ymin<<16, xmax | ymax<<16)
-    float2* ext;          // conservative half-extents of the alpha >= 1/255 footprint (-1: never)
+    float4* rrec;         // render record, 4 x float4 per Gaussian (see render_fwd.hip)
     uint32_t* tiles;
     uint32_t* offsets;    // inclusive scan of tiles over the batch
     uint32_t* blocksums;  // per scan block; scanned in place to exclusive block offsets
@@ -49,6 +51,7 @@ struct ImageArena {
     uint2* ranges;        // per tile [start, end) into the batch's point_list
     uint32_t* tile_count;
     uint32_t* large_list; // worklist of tiles with > kSortSmallCap instances
+    uint32_t* work_list;  // every tile of the batch, longest list first (render scheduling)
 };
 
 struct BinArena {
@@ -90,12 +93,14 @@ struct Inputs {
     const float* bg; int64_t s_bg;
     float scale_mod;
     int prefiltered, antialiasing;
+    int dbg;  // ablation switches for timing experiments (0 in production)
 };
 
 struct Outputs {
     float* out_color;     // [B][C][H][W]
     float* out_invdepth;  // [B][H][W] or null
     int* radii;           // [B][P] or null
+    uint32_t* stats;      // debug: per-workgroup render statistics (null in production)
 };
 
 struct Grads {
@@ -111,6 +116,9 @@ struct Grads {
     float* dL_dscale;            // [B][P][3] or null
     float* dL_drot;              // [B][P][4] or null
 };
+
+// Workgroups for a persistent (work-queue) launch: CUs of the current device x per_cu.
+int persistent_grid(int per_cu);
 
 // ---- launchers (all asynchronous on `stream`) ----
 void launch_preprocess(const Dims& d, const Inputs& in, const GeomArena& g, const Outputs& o,

@@ -26,7 +26,6 @@ __device__ __forceinline__ int f2i(float v) {
 
 // Deterministic exp: same op sequence as gsro_expf (oracle/gsr_oracle.c).
 __device__ __forceinline__ float expf_exact(float x) {
-    if (x != x) return x;
     float xc = fmaxf(x, -87.0f);
     xc = fminf(xc, 88.0f);
     float k = rintf(xc * 1.44269504088896341f);
@@ -42,7 +41,8 @@ __device__ __forceinline__ float expf_exact(float x) {
     p = fmaf(p, r2, r);
     p = p + 1.0f;
     int ki = (int)k;
-    return p * __uint_as_float((uint32_t)(ki + 127) << 23);
+    const float r_ = p * __uint_as_float((uint32_t)(ki + 127) << 23);
+    return (x != x) ? x : r_;  // NaN passes through (select, no branch)
 }
 
 // Hardware exp2 path (v_exp_f32), used in "fast" mode.

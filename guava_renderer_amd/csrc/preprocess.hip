@@ -129,7 +129,14 @@ __global__ __launch_bounds__(kScanBlock) void k_preprocess(Dims d, Inputs in, Ge
                     radius = ir;
                     tiles = nt;
                     rect = make_uint2(rmin[0] | (rmin[1] << 16), rmax[0] | (rmax[1] << 16));
-                    g.ext[gid] = alpha_extent(conic0, conic1, conic2, op * h_conv);
+                    // render record (render_fwd.hip): position, opacity, 1/depth, pre-scaled conic
+                    // (exact power-of-two scalings), conservative alpha >= 1/255 box
+                    const float2 e = alpha_extent(conic0, conic1, conic2, op * h_conv);
+                    float4* rr = g.rrec + 4 * gid;
+                    rr[0] = make_float4(pix0, pix1, op * h_conv, 1.0f / pv[2]);
+                    rr[1] = make_float4(-0.5f * conic0, -conic1, -0.5f * conic2, 0.f);
+                    rr[2] = make_float4(pix0 - e.x, pix0 + e.x, pix1 - e.y, pix1 + e.y);
+                    rr[3] = make_float4(0.f, 0.f, 0.f, 0.f);
                 }
             }
         }

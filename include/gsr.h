@@ -126,6 +126,11 @@ int gsr_backward_batch(int B, int P, int width, int height, const float* means3D
 #define GSR_NUM_STAGES 9
 int gsr_profile_enable(uint32_t stage_mask);
 int gsr_profile_read(double* ms, int* counts, int n);
+/* Debug hook: when non-NULL, render_fwd writes per-(tile, wave) uint32 {cycles, rounds,
+ * surviving Gaussians, list length} (4 words) into this device buffer ([B*T*4][4]). */
+int gsr_debug_render_stats(uint32_t* device_buffer);
+/* Debug hook: ablation switches for timing experiments (results are wrong when non-zero). */
+int gsr_debug_flags(int flags);
 
 /* Synchronises `stream`; writes the batch's instance count and overflow flag. */
 int gsr_batch_status(const char* workspace, int B, int P, int64_t* R_total, int* overflow,
