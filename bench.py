@@ -97,7 +97,7 @@ def main():
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
 
-    from guava_renderer_amd import _lib, scenes
+    from guava_renderer_amd import _lib, parallel, scenes
     from guava_renderer_amd.batch import BatchRasterizer, profile_enable, profile_read
     _lib.set_exact_exp(not a.fast_exp)
 
@@ -106,7 +106,7 @@ def main():
     scene = scenes.avatar_cloud(P, seed=0, gaussians_per_texel=wl["gpt"])
     P = scene["means3D"].shape[0]
     cams_all = scenes.frame_cameras(B * world, W, H, seed=1000)
-    cams = cams_all[rank * B:(rank + 1) * B]
+    cams = parallel.shard_frames(cams_all, rank, world)  # B frames per rank, no data-path collective
 
     t = lambda x: torch.tensor(np.ascontiguousarray(x), device=dev)  # noqa: E731
     means, colors = t(scene["means3D"]), t(scene["colors"])

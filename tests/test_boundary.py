@@ -1,0 +1,121 @@
+"""CPU tests of the drop-in boundary: the C ABI library loads and exports every symbol declared in
+include/gsr.h, the Python mirror keeps the reference's signatures and error behaviour
+(diff_gaussian_rasterization_32/__init__.py:143-207, rasterize_points.cu:58-60), and there is no
+CPU fallback (GPU-less calls with P > 0 raise)."""
+import inspect
+import os
+import re
+
+import numpy as np
+import pytest
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def test_library_exports_every_header_symbol():
+    from guava_renderer_amd import _lib
+    L = _lib.load()
+    hdr = open(os.path.join(ROOT, "include", "gsr.h")).read()
+    declared = set(re.findall(r"^\s*(?:const\s+)?[a-z_0-9]+\*?\s+\**(gsr_[a-z_0-9]+)\s*\(", hdr, re.M))
+    assert declared, "no declarations parsed"
+    assert declared <= set(_lib.EXPORTS), declared - set(_lib.EXPORTS)
+    for sym in declared:
+        assert hasattr(L, sym), sym
+    assert L.gsr_version().startswith(b"gsr-gfx950")
+
+
+def test_scratch_sizes_grow_with_work():
+    from guava_renderer_amd import _lib
+    L = _lib.load()
+    assert L.gsr_geometry_bytes(1000) < L.gsr_geometry_bytes(100000)
+    assert L.gsr_image_bytes(256, 256) < L.gsr_image_bytes(512, 512)
+    assert L.gsr_binning_bytes(10) < L.gsr_binning_bytes(10 ** 6)
+    assert L.gsr_batch_workspace_bytes(4, 1000, 64, 64, 10 ** 4) > L.gsr_batch_workspace_bytes(1, 1000, 64, 64, 10 ** 4)
+
+
+def test_exact_exp_toggle():
+    from guava_renderer_amd import _lib
+    prev = _lib.set_exact_exp(False)
+    assert _lib.set_exact_exp(True) == 0
+    _lib.set_exact_exp(bool(prev) or True)
+
+
+def test_python_surface_matches_reference():
+    import diff_gaussian_rasterization_32 as m
+    from guava_renderer_amd.diff_gaussian_rasterization_32 import _C
+    assert list(m.GaussianRasterizationSettings._fields) == [
+        "image_height", "image_width", "tanfovx", "tanfovy", "bg", "scale_modifier", "viewmatrix",
+        "projmatrix", "sh_degree", "campos", "prefiltered", "debug", "antialiasing"]
+    assert list(inspect.signature(m.GaussianRasterizer_32.forward).parameters) == [
+        "self", "means3D", "means2D", "opacities", "shs", "colors_precomp", "scales", "rotations",
+        "cov3D_precomp"]
+    assert list(inspect.signature(m.rasterize_gaussians).parameters) == [
+        "means3D", "means2D", "sh", "colors_precomp", "opacities", "scales", "rotations",
+        "cov3Ds_precomp", "raster_settings"]
+    assert len(inspect.signature(_C.rasterize_gaussians).parameters) == 20
+    assert len(inspect.signature(_C.rasterize_gaussians_backward).parameters) == 24
+    assert len(inspect.signature(_C.mark_visible).parameters) == 3
+
+
+def _settings():
+    from diff_gaussian_rasterization_32 import GaussianRasterizationSettings
+    return GaussianRasterizationSettings(16, 16, 0.1, 0.1, torch.zeros(32), 1.0, torch.eye(4), torch.eye(4),
+                                         0, torch.zeros(3), False, False, False)
+
+
+def test_argument_validation_messages():
+    from diff_gaussian_rasterization_32 import GaussianRasterizer_32
+    r = GaussianRasterizer_32(_settings())
+    m = torch.zeros((4, 3))
+    with pytest.raises(Exception, match="excatly one of either SHs or precomputed colors"):
+        r(m, m, torch.ones((4, 1)))
+    with pytest.raises(Exception, match="excatly one of either SHs or precomputed colors"):
+        r(m, m, torch.ones((4, 1)), shs=torch.zeros((4, 1, 3)), colors_precomp=torch.zeros((4, 32)))
+    with pytest.raises(Exception, match="exactly one of either scale/rotation pair or precomputed 3D covariance"):
+        r(m, m, torch.ones((4, 1)), colors_precomp=torch.zeros((4, 32)))
+    with pytest.raises(Exception, match="exactly one of either scale/rotation pair or precomputed 3D covariance"):
+        r(m, m, torch.ones((4, 1)), colors_precomp=torch.zeros((4, 32)), scales=m, rotations=torch.zeros((4, 4)),
+          cov3D_precomp=torch.zeros((4, 6)))
+
+
+def test_bad_means_shape_raises_runtime_error():
+    from guava_renderer_amd.diff_gaussian_rasterization_32 import _C
+    with pytest.raises(RuntimeError, match="means3D must have dimensions"):
+        _C.rasterize_gaussians(torch.zeros(32), torch.zeros((5, 2)), torch.zeros((5, 32)), torch.zeros((5, 1)),
+                               torch.zeros((5, 3)), torch.zeros((5, 4)), 1.0, torch.Tensor([]), torch.eye(4),
+                               torch.eye(4), 0.1, 0.1, 8, 8, torch.Tensor([]), 0, torch.zeros(3), False, False, False)
+
+
+def test_empty_scene_returns_zero_image_without_device():
+    # P == 0: the reference returns zero-filled outputs without launching (rasterize_points.cu:88)
+    from guava_renderer_amd.diff_gaussian_rasterization_32 import _C
+    R, color, radii, gb, bb, ib, invd = _C.rasterize_gaussians(
+        torch.ones(32), torch.zeros((0, 3)), torch.zeros((0, 32)), torch.zeros((0, 1)), torch.zeros((0, 3)),
+        torch.zeros((0, 4)), 1.0, torch.Tensor([]), torch.eye(4), torch.eye(4), 0.1, 0.1, 24, 40,
+        torch.Tensor([]), 0, torch.zeros(3), False, False, False)
+    assert R == 0 and color.shape == (32, 24, 40) and float(color.abs().sum()) == 0.0
+    assert radii.shape == (0,) and invd.shape == (1, 24, 40)
+    assert gb.numel() == 0 and bb.numel() == 0 and ib.numel() == 0
+
+
+def test_no_cpu_fallback():
+    from guava_renderer_amd.diff_gaussian_rasterization_32 import _C
+    with pytest.raises(RuntimeError, match="no CPU implementation"):
+        _C.rasterize_gaussians(torch.zeros(32), torch.zeros((3, 3)), torch.zeros((3, 32)), torch.zeros((3, 1)),
+                               torch.zeros((3, 3)), torch.zeros((3, 4)), 1.0, torch.Tensor([]), torch.eye(4),
+                               torch.eye(4), 0.1, 0.1, 8, 8, torch.Tensor([]), 0, torch.zeros(3), False, False,
+                               False)
+
+
+def test_scene_generators_shapes():
+    from guava_renderer_amd import camera, scenes
+    d = scenes.avatar_cloud(5000, seed=0)
+    assert d["means3D"].shape == (5000, 3) and d["colors"].shape == (5000, 32)
+    q = d["rotations"]
+    np.testing.assert_allclose(np.linalg.norm(q, axis=1), 1.0, rtol=1e-5)
+    assert (d["opacities"] > 0.001).all()
+    cam = camera.camera(512, 512)
+    # canonical camera: R = I, t = (0, 0.6, 22) (data_loader.py:377-394), row-vector view matrix
+    np.testing.assert_allclose(cam["viewmatrix"][3, :3], [0, 0.6, 22])
+    assert cam["projmatrix"].dtype == np.float32

@@ -1,0 +1,261 @@
+"""CPU tests that pin the oracle (oracle/gsr_oracle.c).
+
+The reference ships no tests or golden vectors for the rasterizer, and its CUDA
+build cannot run here, so the oracle is pinned by: analytic known-answer cases, an independent
+numpy restatement of the binning/sort contract, and an independent float64 torch restatement with
+autograd (tests/torch_ref.py) for the forward image and every gradient.
+"""
+import numpy as np
+import pytest
+import torch
+
+import oracle
+from helpers import make_scene
+import torch_ref
+
+C = 32
+
+
+def _fwd(d, **kw):
+    return oracle.forward(d["means3D"], d["colors"], d["opacities"], d["scales"], d["rotations"], None,
+                          d["viewmatrix"], d["projmatrix"], d["image_width"], d["image_height"],
+                          d["tanfovx"], d["tanfovy"], d["bg"], **kw)
+
+
+def test_expf_accuracy():
+    x = np.linspace(-87.0, 0.0, 20001).astype(np.float32)
+    got = oracle.expf(x).astype(np.float64)
+    ref = np.exp(x.astype(np.float64))
+    rel = np.abs(got - ref) / ref
+    assert rel.max() < 3e-7, rel.max()
+    assert oracle.expf([0.0])[0] == 1.0
+    assert np.isnan(oracle.expf([np.nan])[0])
+
+
+def _single(o=0.5, W=64, H=64, scale=0.02, off=(0.0, 0.0, 0.0), feat=None):
+    from guava_renderer_amd import camera
+    cam = camera.camera(W, H)
+    d = dict(cam)
+    d["means3D"] = np.array([[off[0], off[1] - 0.6, off[2]]], np.float32)
+    d["scales"] = np.full((1, 3), scale, np.float32)
+    d["rotations"] = np.array([[1, 0, 0, 0]], np.float32)
+    d["opacities"] = np.array([[o]], np.float32)
+    d["colors"] = (np.arange(C, dtype=np.float32)[None] / 7.0 - 1.0) if feat is None else feat
+    d["bg"] = np.zeros(C, np.float32)
+    return d
+
+
+def test_known_answer_single_gaussian():
+    d = _single(o=0.5)
+    col, radii, invd, st = _fwd(d)
+    assert radii[0] > 0
+    mx, my = st["means2D"][0]
+    co = st["conic_opacity"][0].astype(np.float64)
+    H, W = col.shape[1:]
+    ys, xs = np.mgrid[0:H, 0:W]
+    dx, dy = mx - xs, my - ys
+    power = -0.5 * (co[0] * dx * dx + co[2] * dy * dy) - co[1] * dx * dy
+    alpha = np.minimum(0.99, co[3] * np.exp(power))
+    # only pixels of tiles inside the Gaussian's rect see it
+    rect_mask = np.zeros((H, W), bool)
+    gx = (W + 15) // 16
+    for t in range(st["ranges"].shape[0]):
+        if st["ranges"][t, 1] > st["ranges"][t, 0]:
+            tx, ty = t % gx, t // gx
+            rect_mask[ty * 16:(ty + 1) * 16, tx * 16:(tx + 1) * 16] = True
+    a = np.where(rect_mask & (alpha >= 1 / 255), alpha, 0.0)
+    expect = a[None] * d["colors"][0][:, None, None]
+    np.testing.assert_allclose(col, expect, atol=2e-6)
+    np.testing.assert_allclose(st["final_T"].reshape(H, W), 1 - a, atol=1e-6)
+    np.testing.assert_array_equal(st["n_contrib"].reshape(H, W), (a > 0).astype(np.uint32))
+    # inverse depth image: alpha / z
+    np.testing.assert_allclose(invd[0], a / st["depths"][0], rtol=1e-5, atol=1e-9)
+
+
+def test_known_answer_two_gaussians_depth_order():
+    d = _single(o=0.6, scale=0.05)
+    d2 = _single(o=0.7, scale=0.05, off=(0.0, 0.0, 0.1))  # farther from the camera (+z)
+    for k in ("means3D", "scales", "rotations", "opacities"):
+        d[k] = np.concatenate([d2[k], d[k]], 0)  # back one first in index order
+    d["colors"] = np.stack([np.full(C, 2.0, np.float32), np.full(C, 1.0, np.float32)])
+    col, radii, invd, st = _fwd(d)
+    H, W = col.shape[1:]
+    # per tile lists are depth-sorted: the near Gaussian (index 1) comes first
+    for t in range(st["ranges"].shape[0]):
+        s, e = st["ranges"][t]
+        if e - s == 2:
+            assert list(st["point_list"][s:e]) == [1, 0]
+    c = H // 2 * W + W // 2
+    co = st["conic_opacity"].astype(np.float64)
+    m = st["means2D"].astype(np.float64)
+    a = []
+    for g in (1, 0):
+        dx, dy = m[g, 0] - W // 2, m[g, 1] - H // 2
+        p = -0.5 * (co[g, 0] * dx * dx + co[g, 2] * dy * dy) - co[g, 1] * dx * dy
+        a.append(min(0.99, co[g, 3] * np.exp(p)))
+    expect = 1.0 * a[0] + 2.0 * a[1] * (1 - a[0])
+    assert abs(col[0].reshape(-1)[c] - expect) < 1e-5
+    assert abs(st["final_T"][c] - (1 - a[0]) * (1 - a[1])) < 1e-6
+
+
+def test_saturation_stops_before_terminating_gaussian():
+    # 30 opaque Gaussians stacked on the same pixel: T stops above 1e-4 and the Gaussian that would
+    # push T below it is excluded (forward.cu:363-368)
+    n = 30
+    d = _single(o=0.99, scale=0.05)
+    for k in ("means3D", "scales", "rotations", "opacities"):
+        d[k] = np.repeat(d[k], n, 0)
+    d["means3D"][:, 2] = np.linspace(0, 0.2, n).astype(np.float32)
+    d["colors"] = np.ones((n, C), np.float32)
+    col, radii, invd, st = _fwd(d)
+    H, W = col.shape[1:]
+    c = H // 2 * W + W // 2
+    T = st["final_T"][c]
+    k = int(st["n_contrib"][c])
+    assert T >= 1e-4 and 0 < k < n
+    # the next Gaussian in the pixel's list is the one that would push T below 1e-4: excluded
+    t = (H // 2 // 16) * ((W + 15) // 16) + (W // 2 // 16)
+    s, e = st["ranges"][t]
+    g = int(st["point_list"][s + k])
+    co = st["conic_opacity"][g].astype(np.float64)
+    dx, dy = st["means2D"][g, 0] - W // 2, st["means2D"][g, 1] - H // 2
+    a = min(0.99, co[3] * np.exp(-0.5 * (co[0] * dx * dx + co[2] * dy * dy) - co[1] * dx * dy))
+    assert a >= 1 / 255 and T * (1 - a) < 1e-4
+
+
+def test_binning_contract_independent_restatement():
+    d = make_scene("random", 3000, 160, 96, seed=21)
+    _, radii, _, st = _fwd(d)
+    W, H = 160, 96
+    gx, gy = (W + 15) // 16, (H + 15) // 16
+    # independent restatement: instances from rects, ordered by (tile, depth bits, index)
+    inst = []
+    for g in np.nonzero(radii > 0)[0]:
+        mx, my = st["means2D"][g]
+        r = np.float32(radii[g])
+        def cl(v, hi):
+            v = int(np.trunc(v)) if np.isfinite(v) else 0
+            return min(max(v, 0), hi)
+        x0 = cl((mx - r) / np.float32(16), gx); x1 = cl((((mx + r) + np.float32(16)) - np.float32(1)) / np.float32(16), gx)
+        y0 = cl((my - r) / np.float32(16), gy); y1 = cl((((my + r) + np.float32(16)) - np.float32(1)) / np.float32(16), gy)
+        db = np.float32(st["depths"][g]).view(np.uint32)
+        for y in range(y0, y1):
+            for x in range(x0, x1):
+                inst.append((y * gx + x, int(db), int(g)))
+    inst.sort()
+    assert len(inst) == st["R"]
+    np.testing.assert_array_equal(np.array([i[2] for i in inst], np.uint32), st["point_list"])
+    tiles = np.array([i[0] for i in inst])
+    for t in range(gx * gy):
+        idx = np.nonzero(tiles == t)[0]
+        exp = (idx[0], idx[-1] + 1) if len(idx) else (0, 0)
+        assert tuple(st["ranges"][t]) == exp
+
+
+def test_equal_depth_ties_keep_index_order():
+    d = make_scene("random", 500, 64, 64, seed=22)
+    d["means3D"][:, 2] = 0.0  # identical depth for everyone
+    _, radii, _, st = _fwd(d)
+    for t in range(st["ranges"].shape[0]):
+        s, e = st["ranges"][t]
+        lst = st["point_list"][s:e]
+        assert np.all(np.diff(lst.astype(np.int64)) > 0)
+
+
+def _torch_check(d, W, H, dL=None, dLinv=None, tol_img=2e-5, tol_grad=2e-5):
+    col, radii, invd, st = _fwd(d)
+    tile_lists = {t: st["point_list"][s:e] for t, (s, e) in enumerate(st["ranges"]) if e > s}
+    f64 = lambda a: torch.tensor(np.asarray(a, np.float64), requires_grad=True)  # noqa: E731
+    m3, sc, rot, op, colr = (f64(d["means3D"]), f64(d["scales"]), f64(d["rotations"]),
+                              f64(d["opacities"].reshape(-1)), f64(d["colors"]))
+    off = torch.zeros((m3.shape[0], 3), dtype=torch.float64, requires_grad=True)
+    pr = torch_ref.project(m3, sc, rot, torch.tensor(d["viewmatrix"], dtype=torch.float64),
+                           torch.tensor(d["projmatrix"], dtype=torch.float64), W, H, float(d["tanfovx"]),
+                           float(d["tanfovy"]), ndc_offset=off)
+    out, inv, Tf, nc = torch_ref.render(pr, op, colr, torch.tensor(d["bg"], dtype=torch.float64), W, H,
+                                        tile_lists)
+    same = (nc.numpy().reshape(-1) == st["n_contrib"])
+    assert same.mean() > 0.995, same.mean()
+    err = np.abs(out.detach().numpy() - col).reshape(C, -1)[:, same].max()
+    assert err < tol_img, err
+    if dL is None:
+        return
+    loss = (out * torch.tensor(dL, dtype=torch.float64)).sum() + (inv * torch.tensor(dLinv[0], dtype=torch.float64)).sum()
+    loss.backward()
+    g = oracle.backward(st, d["means3D"], d["colors"], d["opacities"], d["scales"], d["rotations"], None,
+                        d["viewmatrix"], d["projmatrix"], W, H, d["tanfovx"], d["tanfovy"], d["bg"], dL, dLinv)
+    g_m2, g_col, g_op, g_m3, g_cov, g_sh, g_sc, g_rot = g
+    for name, ours, ref in (("colors", g_col, colr.grad), ("opacity", g_op.reshape(-1), op.grad),
+                            ("means3D", g_m3, m3.grad), ("scales", g_sc, sc.grad),
+                            ("rotations", g_rot, rot.grad), ("means2D", g_m2[:, :2], off.grad[:, :2])):
+        ref = ref.numpy()
+        e = np.abs(ours - ref).max() / max(np.abs(ref).max(), 1e-30)
+        assert e < tol_grad, (name, e)
+
+
+def test_forward_and_gradients_match_float64_autograd():
+    W, H = 48, 32
+    d = make_scene("random", 40, W, H, seed=23)
+    d["means3D"][:, :2] *= 0.25
+    rng = np.random.default_rng(3)
+    dL = rng.normal(size=(C, H, W)).astype(np.float32)
+    dLinv = rng.normal(size=(1, H, W)).astype(np.float32)
+    _torch_check(d, W, H, dL, dLinv)
+
+
+def test_avatar_forward_matches_float64_restatement():
+    W, H = 64, 48
+    d = make_scene("avatar", 400, W, H, seed=24)
+    _torch_check(d, W, H)
+
+
+@pytest.mark.parametrize("W,H", [(1, 1), (17, 33), (100, 70)])
+def test_odd_image_sizes(W, H):
+    d = make_scene("random", 200, W, H, seed=25)
+    col, radii, invd, st = _fwd(d)
+    assert col.shape == (C, H, W)
+    assert st["final_T"].shape == (H * W,)
+    assert np.isfinite(col).all()
+
+
+def test_all_behind_camera_and_transparent():
+    d = make_scene("random", 50, 32, 32, seed=26)
+    d["means3D"][:, 2] = -30.0  # behind the camera (view z <= 0.2)
+    col, radii, _, st = _fwd(d)
+    assert (radii == 0).all() and st["R"] == 0
+    np.testing.assert_array_equal(col, 0.0)
+    d = make_scene("random", 50, 32, 32, seed=27)
+    d["opacities"][:] = 1e-3  # below 1/255: never blended
+    col, radii, _, st = _fwd(d)
+    assert (radii > 0).any()
+    np.testing.assert_array_equal(col, 0.0)
+    np.testing.assert_array_equal(st["n_contrib"], 0)
+
+
+def test_prefiltered_raises():
+    d = make_scene("random", 20, 32, 32, seed=28)
+    d["means3D"][0, 2] = -30.0
+    with pytest.raises(RuntimeError):
+        _fwd(d, prefiltered=True)
+
+
+def test_huge_gaussian_covers_every_tile():
+    d = make_scene("random", 3, 96, 64, seed=29)
+    d["scales"][0] = 5.0
+    _, radii, _, st = _fwd(d)
+    assert st["tiles_touched"][0] == st["ranges"].shape[0]
+
+
+def test_mark_visible():
+    d = make_scene("random", 100, 32, 32, seed=30)
+    d["means3D"][:10, 2] = -30.0
+    vis = oracle.mark_visible(d["means3D"], d["viewmatrix"], d["projmatrix"])
+    assert not vis[:10].any() and vis[10:].all()
+
+
+def test_antialiasing_scales_opacity():
+    d = make_scene("random", 300, 64, 64, seed=31)
+    _, _, _, st0 = _fwd(d)
+    _, _, _, st1 = _fwd(d, antialiasing=True)
+    vis = st0["radii"] > 0
+    assert np.all(st1["conic_opacity"][vis, 3] <= st0["conic_opacity"][vis, 3])
