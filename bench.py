@@ -26,6 +26,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+F32_MFMA_PEAK_TFLOPS = 157.3  # dense f32-input MFMA peak (MI355X_MICROARCH.md)
 C = 32
 
 
@@ -76,11 +77,16 @@ def cpu_baseline(scene, cams, W, H, budget_s):
                        cam["tanfovx"], cam["tanfovy"], bg)
         frames += 1
         el = time.perf_counter() - t0
-        if el >= budget_s or frames >= 64:
+        if el >= budget_s or frames >= 512:
             break
+    model = "unknown CPU"
+    try:
+        model = next(ln.split(":", 1)[1].strip() for ln in open("/proc/cpuinfo") if ln.startswith("model name"))
+    except (OSError, StopIteration):
+        pass
     return dict(value=frames / el, unit="frames/s", cores=threads, kind="port",
                 sample=f"{frames} frames of the same {W}x{H} workload through the C oracle "
-                       f"(preprocess+bin+sort+render, OpenMP {threads} threads) in {el:.1f}s")
+                       f"(preprocess+bin+sort+render, OpenMP {threads} threads on {model}) in {el:.1f}s")
 
 
 def main():
@@ -98,7 +104,7 @@ def main():
     torch.cuda.set_device(dev)
 
     from guava_renderer_amd import _lib, parallel, scenes
-    from guava_renderer_amd.batch import BatchRasterizer, profile_enable, profile_read
+    from guava_renderer_amd.batch import BatchRasterizer, profile_enable, profile_read, render_counters
     _lib.set_exact_exp(not a.fast_exp)
 
     wl = _workload(a.config)
@@ -149,6 +155,8 @@ def main():
         dist.barrier()
     prof = profile_read()
     profile_enable(())
+    # work counters of one extra (instrumented, untimed) step: which wall the render kernel hits
+    work = render_counters(step, device=dev)
     R_after, ovf = rast.status()
     assert not ovf, "capacity overflow inside the timed region"
     if dist is not None:
@@ -203,6 +211,13 @@ def main():
                           "achieved_GBs": round(_path_alg_bytes(P, W, H) * fps / 1e9, 1),
                           "frac": round(_path_alg_bytes(P, W, H) * fps / 1e9 / HBM_PEAK_GBS, 4)},
     }
+    # per-frame work of the render kernel and its matrix-core utilisation (f32 MFMA, dense peak)
+    ksteps = work["mfma_ksteps"]
+    mfma_flops = ksteps * 2 * (2 * 32 * 32 * 2)  # two v_mfma_f32_32x32x2f32 per wave k-step
+    out["render_work_per_frame"] = {k: round(v / B, 1) for k, v in work.items()}
+    out["render_mfma"] = {"issued_tflops": round(mfma_flops / (render_ms * 1e-3) / 1e12, 2) if render_ms else None,
+                          "peak_tflops": F32_MFMA_PEAK_TFLOPS,
+                          "useful_frac": round(work["pairs_contributing"] / max(64 * work["strip_pairs_blended"], 1), 4)}
     if a.stages:
         out["stage_ms_per_step"] = {k: round(v[0] / max(v[1], 1), 4) for k, v in prof.items()}
     if rank == 0 and world == 1 and not a.no_cpu_baseline:

@@ -110,3 +110,22 @@ def profile_read():
     cnt = (ctypes.c_int * n)()
     _lib.check(_lib.load().gsr_profile_read(ms, cnt, n), "gsr_profile_read")
     return {s: (ms[i], cnt[i]) for i, s in enumerate(STAGES) if cnt[i]}
+
+
+COUNTERS = ("pairs_evaluated", "pairs_contributing", "strip_pairs_blended", "mfma_ksteps",
+            "gaussians_staged", "list_entries", "tiles_rendered")
+
+
+def render_counters(fn, device="cuda"):
+    """Run `fn()` (one or more forwards) with the instrumented render kernel and return the work
+    counters of include/gsr.h:gsr_render_counters as a dict."""
+    L = _lib.load()
+    buf = torch.zeros(8, dtype=torch.int64, device=device)
+    L.gsr_render_counters(buf.data_ptr())
+    try:
+        fn()
+        torch.cuda.synchronize(device)
+    finally:
+        L.gsr_render_counters(None)
+    v = buf.cpu().tolist()
+    return {k: int(v[i]) for i, k in enumerate(COUNTERS)}

@@ -16,8 +16,7 @@ namespace {
 
 thread_local std::string g_err;
 int g_exact_exp = 1;
-uint32_t* g_render_stats = nullptr;
-int g_dbg = 0;  // debug hook (gsr_debug_render_stats)
+uint64_t* g_render_counters = nullptr;  // gsr_render_counters
 
 int fail(gsr_status st, const std::string& msg) {
     g_err = msg;
@@ -224,7 +223,7 @@ int gsr_forward(gsr_alloc_fn geometryBuffer, gsr_alloc_fn binningBuffer, gsr_all
     in.bg = background; in.s_bg = 0;
     in.scale_mod = scale_modifier;
     in.prefiltered = prefiltered; in.antialiasing = antialiasing;
-    Outputs o{out_color, depth, radii, g_render_stats};
+    Outputs o{out_color, depth, radii, g_render_counters};
 
     HIP_TRY(hipMemsetAsync(g.ctrl, 0, kCtrlWords * 4, s));
     HIP_TRY(hipMemsetAsync(im.tile_count, 0, (size_t)d.T * 4, s));
@@ -347,8 +346,7 @@ int gsr_forward_batch(int B, int P, int width, int height, const float* means3D,
     in.bg = backgrounds; in.s_bg = bg_stride;
     in.scale_mod = scale_modifier;
     in.prefiltered = 0; in.antialiasing = antialiasing;
-    in.dbg = g_dbg;
-    Outputs o{out_color, out_invdepth, radii, g_render_stats};
+    Outputs o{out_color, out_invdepth, radii, g_render_counters};
     HIP_TRY(hipMemsetAsync(g.ctrl, 0, kCtrlWords * 4, s));
     HIP_TRY(hipMemsetAsync(im.tile_count, 0, (size_t)d.B * d.T * 4, s));
     { StageTimer st_(0, s); launch_preprocess(d, in, g, o, s); }
@@ -406,14 +404,8 @@ int gsr_backward_batch(int B, int P, int width, int height, const float* means3D
     return 0;
 }
 
-int gsr_debug_flags(int flags) {
-    int p = g_dbg;
-    g_dbg = flags;
-    return p;
-}
-
-int gsr_debug_render_stats(uint32_t* device_buffer) {
-    g_render_stats = device_buffer;
+int gsr_render_counters(uint64_t* device_counters) {
+    g_render_counters = device_counters;
     return 0;
 }
 

@@ -93,14 +93,13 @@ struct Inputs {
     const float* bg; int64_t s_bg;
     float scale_mod;
     int prefiltered, antialiasing;
-    int dbg;  // ablation switches for timing experiments (0 in production)
 };
 
 struct Outputs {
     float* out_color;     // [B][C][H][W]
     float* out_invdepth;  // [B][H][W] or null
     int* radii;           // [B][P] or null
-    uint32_t* stats;      // debug: per-workgroup render statistics (null in production)
+    uint64_t* stats;      // gsr_render_counters words, or null (production kernel)
 };
 
 struct Grads {

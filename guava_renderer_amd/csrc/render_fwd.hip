@@ -59,7 +59,7 @@ __device__ __forceinline__ void glds16(const void* gsrc, void* lds_wave_base) {
                                      (__attribute__((address_space(3))) void*)lds_wave_base, 16, 0, 0);
 }
 
-template <bool EXACT>
+template <bool EXACT, bool STATS>
 __global__ __launch_bounds__(GSR_TILE_PIX) void k_render_fwd(Dims d, Inputs in, GeomArena g,
                                                              ImageArena im, BinArena bn, Outputs o) {
     __shared__ __attribute__((aligned(16))) float4 s_rec[2][kSlots * kRecF4];
@@ -106,6 +106,8 @@ __global__ __launch_bounds__(GSR_TILE_PIX) void k_render_fwd(Dims d, Inputs in, 
         float T = 1.0f, invd = 0.f;
         uint32_t last = 0;
         bool done = !inside;
+        uint64_t n_surv = 0, n_steps = 0, n_contrib_pairs = 0, n_staged = 0;
+        uint32_t stop = 0;
 
         // stage round `base` into buffer `buf` (lanes beyond the list stay idle)
 #define GSR_ISSUE(base_, buf_)                                                                      \
@@ -136,6 +138,7 @@ __global__ __launch_bounds__(GSR_TILE_PIX) void k_render_fwd(Dims d, Inputs in, 
                 GSR_PREFETCH_IDX(base + 2 * kRB)
             }
             const int cnt = min(kRB, n - base);
+            if (STATS) n_staged += cnt;
             const float4* __restrict__ rec = s_rec[buf];
             const float* __restrict__ fb = s_f[buf];
             if (__any(!done)) {
@@ -145,6 +148,7 @@ __global__ __launch_bounds__(GSR_TILE_PIX) void k_render_fwd(Dims d, Inputs in, 
                     keep = bx.y >= sx0 && bx.x <= sx1 && bx.w >= sy0 && bx.z <= sy1;
                 }
                 uint64_t mask = __ballot(keep);
+                if (STATS) n_surv += __popcll(mask);
                 const int hi = lane >> 5;
                 const int ch = lane & 31;
                 while (mask) {
@@ -153,10 +157,19 @@ __global__ __launch_bounds__(GSR_TILE_PIX) void k_render_fwd(Dims d, Inputs in, 
                     const int ib = mask ? (int)__builtin_ctzll(mask) : kNull;
                     mask &= mask - 1;
                     const float fa = fb[(hi ? ib : ia) * GSR_C + ch];
+                    const bool was_done = done;
                     const float wa = blend_one<EXACT>(rec[ia * kRecF4], rec[ia * kRecF4 + 1], pfx, pfy,
                                                       base + ia + 1, T, invd, last, done);
+                    const bool done_a = done;
                     const float wb = blend_one<EXACT>(rec[ib * kRecF4], rec[ib * kRecF4 + 1], pfx, pfy,
                                                       base + ib + 1, T, invd, last, done);
+                    if (STATS) {
+                        // list position at which a pixel terminated inside this step
+                        if (!was_done && done_a) stop = (uint32_t)(base + ia + 1);
+                        else if (!done_a && done) stop = (uint32_t)(base + ib + 1);
+                        n_contrib_pairs += __popcll(__ballot(wa > 0.f)) + __popcll(__ballot(wb > 0.f));
+                        n_steps++;
+                    }
                     const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(wa), __float_as_uint(wb),
                                                                      false, false);
                     acc0 = __builtin_amdgcn_mfma_f32_32x32x2f32(fa, __uint_as_float(sw[0]), acc0, 0, 0, 0);
@@ -175,6 +188,22 @@ __global__ __launch_bounds__(GSR_TILE_PIX) void k_render_fwd(Dims d, Inputs in, 
 
         // ---- epilogue ----
         const int64_t HW = (int64_t)d.H * d.W;
+        if (STATS) {
+            unsigned long long* cnt = (unsigned long long*)o.stats;
+            uint64_t ev = inside ? (done ? stop : (uint32_t)n) : 0;
+            for (int off = 32; off > 0; off >>= 1) ev += __shfl_xor(ev, off);
+            if (lane == 0) {
+                atomicAdd(&cnt[0], (unsigned long long)ev);
+                atomicAdd(&cnt[1], (unsigned long long)n_contrib_pairs);
+                atomicAdd(&cnt[2], (unsigned long long)n_surv);
+                atomicAdd(&cnt[3], (unsigned long long)n_steps);
+                if (wv == 0) {
+                    atomicAdd(&cnt[4], (unsigned long long)n_staged);
+                    atomicAdd(&cnt[5], (unsigned long long)n);
+                    atomicAdd(&cnt[6], 1ull);
+                }
+            }
+        }
         if (inside) {
             const int64_t pix = (int64_t)py * d.W + px;
             im.final_T[b * HW + pix] = T;
@@ -209,10 +238,14 @@ void launch_render_fwd(const Dims& d, const Inputs& in, const GeomArena& g, cons
     const int ntiles = d.B * d.T;
     if (ntiles == 0) return;
     const int grid = min(ntiles, persistent_grid(4));
-    if (exact)
-        hipLaunchKernelGGL(k_render_fwd<true>, dim3(grid), dim3(GSR_TILE_PIX), 0, s, d, in, g, im, b, o);
-    else
-        hipLaunchKernelGGL(k_render_fwd<false>, dim3(grid), dim3(GSR_TILE_PIX), 0, s, d, in, g, im, b, o);
+    const dim3 gr(grid), bl(GSR_TILE_PIX);
+    if (o.stats) {
+        if (exact) hipLaunchKernelGGL((k_render_fwd<true, true>), gr, bl, 0, s, d, in, g, im, b, o);
+        else hipLaunchKernelGGL((k_render_fwd<false, true>), gr, bl, 0, s, d, in, g, im, b, o);
+    } else {
+        if (exact) hipLaunchKernelGGL((k_render_fwd<true, false>), gr, bl, 0, s, d, in, g, im, b, o);
+        else hipLaunchKernelGGL((k_render_fwd<false, false>), gr, bl, 0, s, d, in, g, im, b, o);
+    }
 }
 
 }  // namespace gsr

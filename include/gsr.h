@@ -126,11 +126,15 @@ int gsr_backward_batch(int B, int P, int width, int height, const float* means3D
 #define GSR_NUM_STAGES 9
 int gsr_profile_enable(uint32_t stage_mask);
 int gsr_profile_read(double* ms, int* counts, int n);
-/* Debug hook: when non-NULL, render_fwd writes per-(tile, wave) uint32 {cycles, rounds,
- * surviving Gaussians, list length} (4 words) into this device buffer ([B*T*4][4]). */
-int gsr_debug_render_stats(uint32_t* device_buffer);
-/* Debug hook: ablation switches for timing experiments (results are wrong when non-zero). */
-int gsr_debug_flags(int flags);
+/* Work counters for the roofline report.  When `device_counters` is non-NULL, later forward calls run
+ * an instrumented render kernel (same results, slower) that atomically adds into 8 uint64 device
+ * words: [0] (pixel, Gaussian) pairs evaluated by the reference's per-pixel loop (sum over pixels
+ * of the list positions visited before the pixel finished: n_contrib, or the terminating
+ * position, or the whole list), [1] pairs that contributed (alpha >= 1/255, before termination),
+ * [2] (wave strip, Gaussian) pairs blended after the per-wave cull, [3] MFMA k-steps issued per
+ * wave, [4] Gaussians staged (list entries loaded into LDS), [5] list entries of all tiles,
+ * [6] tiles rendered, [7] reserved.  NULL restores the production kernel. */
+int gsr_render_counters(uint64_t* device_counters);
 
 /* Synchronises `stream`; writes the batch's instance count and overflow flag. */
 int gsr_batch_status(const char* workspace, int B, int P, int64_t* R_total, int* overflow,

@@ -389,6 +389,44 @@ void gsro_render(int W, int H, const uint32_t* ranges, const uint32_t* point_lis
     }
 }
 
+/* Work counts of the per-pixel loop above (test infrastructure for gsr_render_counters):
+ * out[0] = (pixel, Gaussian) pairs visited (up to and including a terminating Gaussian),
+ * out[1] = pairs that contributed. */
+void gsro_render_counts(int W, int H, const uint32_t* ranges, const uint32_t* point_list,
+                        const float* means2D, const float* conic_opacity, int exact_exp,
+                        uint64_t* out) {
+    const int gx = (W + BX - 1) / BX, gy = (H + BY - 1) / BY;
+    uint64_t visited = 0, contrib = 0;
+    for (int tile = 0; tile < gx * gy; tile++) {
+        const int tx = tile % gx, ty = tile / gx;
+        const uint32_t start = ranges[2 * tile], end = ranges[2 * tile + 1];
+        for (int ly = 0; ly < BY; ly++)
+            for (int lx = 0; lx < BX; lx++) {
+                const int x = tx * BX + lx, y = ty * BY + ly;
+                if (x >= W || y >= H) continue;
+                float Tr = 1.0f;
+                for (uint32_t j = start; j < end; j++) {
+                    visited++;
+                    const uint32_t g = point_list[j];
+                    const float* co = conic_opacity + 4 * (size_t)g;
+                    const float dx = means2D[2 * (size_t)g] - (float)x;
+                    const float dy = means2D[2 * (size_t)g + 1] - (float)y;
+                    const float A = -0.5f * co[0], Bb = -co[1], Cq = -0.5f * co[2];
+                    const float power = fmaf(dy, fmaf(Cq, dy, Bb * dx), (A * dx) * dx);
+                    if (power > 0.0f) continue;
+                    const float alpha = fminf(0.99f, co[3] * blend_exp(power, exact_exp));
+                    if (alpha < 1.0f / 255.0f) continue;
+                    const float test_T = Tr * (1.0f - alpha);
+                    if (test_T < 0.0001f) break;
+                    Tr = test_T;
+                    contrib++;
+                }
+            }
+    }
+    out[0] = visited;
+    out[1] = contrib;
+}
+
 void gsro_render_backward(int W, int H, const uint32_t* ranges, const uint32_t* point_list,
                           const float* bg, const float* means2D, const float* conic_opacity,
                           const float* colors, const float* depths, const float* final_T,

@@ -77,6 +77,9 @@ void gsro_render(int W, int H, const uint32_t* ranges, const uint32_t* point_lis
 /* renderCUDA bwd (backward.cu:452-638).  Gradient buffers must be zeroed by the caller.
  * dL_dinvdepth_pix / dL_dinvdepth_g may be NULL (the "no invdepth grad" path).
  * dL_dmean2D[3P], dL_dconic[4P], dL_dopacity[P], dL_dcolors[C*P], dL_dinvdepth_g[P]. */
+void gsro_render_counts(int W, int H, const uint32_t* ranges, const uint32_t* point_list,
+                        const float* means2D, const float* conic_opacity, int exact_exp,
+                        uint64_t* out);
 void gsro_render_backward(int W, int H, const uint32_t* ranges, const uint32_t* point_list,
                           const float* bg, const float* means2D, const float* conic_opacity,
                           const float* colors, const float* depths, const float* final_T,

@@ -50,6 +50,8 @@ def lib():
                                _u32, _u64, _u32, ctypes.c_int64]
         L.gsro_render.argtypes = [ctypes.c_int, ctypes.c_int, _u32, _u32, _f, _f, _f, _f, _f,
                                   ctypes.c_int, _f, _f, _f, _u32]
+        L.gsro_render_counts.argtypes = [ctypes.c_int, ctypes.c_int, _u32, _u32, _f, _f, ctypes.c_int,
+                                         _u64]
         L.gsro_render_backward.argtypes = [ctypes.c_int, ctypes.c_int, _u32, _u32, _f, _f, _f, _f,
                                            _f, _f, _u32, _f, _f, ctypes.c_int, _f, _f, _f, _f, _f]
         L.gsro_preprocess_backward.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, _f, _i, _f,
@@ -153,6 +155,16 @@ def render(st, colors, bg, W, H, exact_exp=True):
                       _p(out, _f), _p(invd, _f), _p(fT, _f), _p(nc, _u32))
     st.update(final_T=fT, n_contrib=nc)
     return out, invd
+
+
+def render_counts(st, W, H, exact_exp=True):
+    """(pairs visited, pairs contributing) of the per-pixel blend loop (forward.cu:336-381)."""
+    out = np.zeros(2, np.uint64)
+    pl = st["point_list"] if st["R"] > 0 else np.zeros(1, np.uint32)
+    lib().gsro_render_counts(int(W), int(H), _p(st["ranges"], _u32), _p(pl, _u32),
+                             _p(st["means2D"], _f), _p(st["conic_opacity"], _f), int(bool(exact_exp)),
+                             _p(out, _u64))
+    return int(out[0]), int(out[1])
 
 
 def forward(means3D, colors, opacities, scales, rotations, cov3D_precomp, view, proj, W, H, tanx,
