@@ -11,13 +11,13 @@
 //   2. k_bin_count        per 256 Gaussians: instance offsets + LDS tile histogram; one global
 //                         atomic per (workgroup, tile) hands out each workgroup's slot range
 //   3. k_tile_scan        exclusive scan of per-tile counts -> ranges; worklist of long tiles
-//   4. k_bin_scatter      each instance writes its 64-bit (depth bits, index) key into its tile's
-//                         segment (order inside a segment arbitrary)
+//   4. k_bin_scatter      each instance writes its 64-bit (depth bits, index, strip mask) key into
+//                         its tile's segment (order inside a segment arbitrary)
 //   5. k_tile_sort_*      one workgroup per tile sorts its segment in LDS: linear bucket pass on
 //                         the depth bits + in-bucket ranking on the full key (O(n) for smooth depth
 //                         distributions); bitonic in LDS for degenerate buckets; bitonic in global
 //                         memory for tiles longer than kSortLargeCap.
-// All passes are HBM/L2-bound integer work: 4+4+8+8+4 B per instance.
+// All passes are HBM/L2-bound integer work: 4+4+8+8+5 B per instance.
 #include "gsr_internal.h"
 
 namespace gsr {
@@ -169,6 +169,7 @@ __global__ __launch_bounds__(1024) void k_tile_scan(int n, const uint32_t* __res
     if (threadIdx.x == 0) {
         uint32_t acc = 0;
         for (int k = 0; k < kBuckets; k++) {
+            if (k == kBuckets - 1) ctrl[kCtrlNonEmpty] = acc;
             const uint32_t v = bcount[k];
             bcount[k] = acc;
             acc += v;
@@ -188,6 +189,57 @@ void launch_tile_scan(const Dims& d, const GeomArena& g, const ImageArena& im, h
 }
 
 // ---------------------------------------------------------------- 4. scatter keys
+// Minimum over the pixel-centre rectangle dx in [dxl, dxh], dy in [dyl, dyh] (dx = mean - pixel)
+// of the conic's quadratic form Q = a dx^2 + 2b dx dy + c dy^2 (power = -Q/2 in the blend).  Q is
+// convex (a, c > 0, ac > b^2), so the minimum is 0 if the mean lies inside, else it lies on an edge:
+// each edge is a 1-D quadratic minimised by clamping its vertex.
+__device__ __forceinline__ float rect_qmin(float a, float b, float c, float dxl, float dxh, float dyl,
+                                           float dyh) {
+    if (dxl <= 0.f && dxh >= 0.f && dyl <= 0.f && dyh >= 0.f) return 0.f;
+    float q = 3.0e38f;
+    const float ia = 1.0f / a, ic = 1.0f / c;
+    const float xs[2] = {dxl, dxh}, ys[2] = {dyl, dyh};
+#pragma unroll
+    for (int k = 0; k < 2; k++) {
+        const float X = xs[k];
+        const float y = fminf(fmaxf(-b * X * ic, dyl), dyh);
+        q = fminf(q, a * X * X + 2.f * b * X * y + c * y * y);
+        const float Y = ys[k];
+        const float x = fminf(fmaxf(-b * Y * ia, dxl), dxh);
+        q = fminf(q, a * x * x + 2.f * b * x * Y + c * Y * Y);
+    }
+    return q;
+}
+
+// Strip mask of one (Gaussian, tile) instance: bit s is set unless no pixel centre of the tile's
+// s-th 16x4 strip can give alpha = min(0.99, o*exp(-Q/2)) >= 1/255, i.e. unless Q > 2 ln(255 o)
+// on the whole strip.  A cleared bit only ever removes pairs the blend skips anyway (alpha < 1/255,
+// forward.cu:362-363), so culling with it is decision-preserving; the slack (1e-4 of the form's
+// term magnitudes + 1e-3 relative) covers float rounding of both this test and the blend's power.
+// Non-finite or non-positive-definite conics keep every strip.
+__device__ __forceinline__ uint32_t strip_mask(float4 co, float2 m, int tx, int ty) {
+    const float a = co.x, b = co.y, c = co.z, o = co.w;
+    if (o < 1.0f / 255.0f) return 0u;  // alpha <= o < 1/255 at every pixel
+    if (!(a > 0.f) || !(c > 0.f) || !(a * c - b * b > 0.f) || !(o <= 3.0e38f)) return (1u << kStrips) - 1u;
+    const float K = 2.0f * logf(255.0f * o);
+    const float dxl = m.x - (float)(tx * GSR_BX + GSR_BX - 1), dxh = m.x - (float)(tx * GSR_BX);
+    const float mx = fmaxf(fabsf(dxl), fabsf(dxh));
+    uint32_t bits = 0;
+#pragma unroll
+    for (int s = 0; s < kStrips; s++) {
+        const float y0 = (float)(ty * GSR_BY + s * (GSR_BY / kStrips));
+        const float dyl = m.y - (y0 + (float)(GSR_BY / kStrips - 1)), dyh = m.y - y0;
+        const float my = fmaxf(fabsf(dyl), fabsf(dyh));
+        const float slack = 1e-4f * (a * mx * mx + 2.f * fabsf(b) * mx * my + c * my * my) + 1e-3f * K + 1e-3f;
+        const float q = rect_qmin(a, b, c, dxl, dxh, dyl, dyh);
+        if (!(q > K + slack)) bits |= 1u << s;
+    }
+    return bits;
+}
+
+// Key of an instance: depth bits << 32 | Gaussian index << 4 | strip mask.  Sorting the full key
+// orders a tile by (depth, index) as the reference's stable sort does (the index is unique in a
+// tile, so the mask bits never decide).
 __global__ __launch_bounds__(kScanBlock) void k_bin_scatter(Dims d, GeomArena g, ImageArena im,
                                                             BinArena bn) {
     if (g.ctrl[kCtrlOverflow]) return;
@@ -198,6 +250,8 @@ __global__ __launch_bounds__(kScanBlock) void k_bin_scatter(Dims d, GeomArena g,
     const uint32_t tiles = g.tiles[gid];
     if (!tiles) return;
     const uint2 rect = g.rect[gid];
+    const float4 co = g.conic[gid];
+    const float2 m = g.means2D[gid];
     const uint64_t key_hi = (uint64_t)__float_as_uint(g.depth[gid]) << 32;
     const uint2* rg = im.ranges + (int64_t)b * d.T;
     const uint32_t x0 = rect.x & 0xFFFF, y0 = rect.x >> 16, x1 = rect.y & 0xFFFF, y1 = rect.y >> 16;
@@ -205,7 +259,8 @@ __global__ __launch_bounds__(kScanBlock) void k_bin_scatter(Dims d, GeomArena g,
     for (uint32_t y = y0; y < y1; y++)
         for (uint32_t x = x0; x < x1; x++) {
             const uint32_t t = y * (uint32_t)d.gx + x;
-            bn.keys[rg[t].x + bn.inst_slot[k]] = key_hi | (uint32_t)i;
+            const uint32_t sm = strip_mask(co, m, (int)x, (int)y);
+            bn.keys[rg[t].x + bn.inst_slot[k]] = key_hi | ((uint32_t)i << 4) | sm;
             k++;
         }
 }
@@ -273,9 +328,15 @@ __device__ void bitonic_sort(uint64_t* key, int n) {
 }
 
 // Sort one tile segment of n <= CAP keys in LDS; writes the Gaussian indices to out[0..n).
+// Sorted key -> point_list entry (Gaussian index) and strip mask.
+__device__ __forceinline__ void emit(uint64_t key, uint32_t* out, uint8_t* msk, int i) {
+    out[i] = ((uint32_t)key) >> 4;
+    msk[i] = (uint8_t)(key & 0xF);
+}
+
 template <int NT, int CAP>
-__device__ void sort_segment_lds(const uint64_t* __restrict__ gkeys, uint32_t* __restrict__ out, int n,
-                                 char* smem) {
+__device__ void sort_segment_lds(const uint64_t* __restrict__ gkeys, uint32_t* __restrict__ out,
+                                 uint8_t* __restrict__ msk, int n, char* smem) {
     constexpr int ITEMS = CAP / NT;
     constexpr uint32_t kDegenerate = 48;
     uint64_t* key = (uint64_t*)smem;                        // CAP
@@ -316,7 +377,7 @@ __device__ void sort_segment_lds(const uint64_t* __restrict__ gkeys, uint32_t* _
     const uint32_t maxb = block_reduce_max<uint32_t, NT>(mycnt_max, red);
     if (maxb > kDegenerate) {
         bitonic_sort<NT>(key, n);
-        for (int i = threadIdx.x; i < n; i += NT) out[i] = (uint32_t)key[i];
+        for (int i = threadIdx.x; i < n; i += NT) emit(key[i], out, msk, i);
         return;
     }
     // exclusive scan of bucket counts (chunked per thread), kept as bucket START
@@ -363,7 +424,11 @@ __device__ void sort_segment_lds(const uint64_t* __restrict__ gkeys, uint32_t* _
         if (i < n) cnt[rank[k]] = (uint32_t)key[i];
     }
     __syncthreads();
-    for (int i = threadIdx.x; i < n; i += NT) out[i] = cnt[i];
+    for (int i = threadIdx.x; i < n; i += NT) {
+        const uint32_t v = cnt[i];
+        out[i] = v >> 4;
+        msk[i] = (uint8_t)(v & 0xF);
+    }
 }
 
 constexpr size_t sort_lds_bytes(int NT, int CAP) { return (size_t)14 * CAP + 4 * (NT / 64 + 1) + 16; }
@@ -375,10 +440,10 @@ __global__ __launch_bounds__(256) void k_tile_sort_small(ImageArena im, BinArena
     const int n = (int)(r.y - r.x);
     if (n == 0 || n > kSortSmallCap) return;
     if (n == 1) {
-        if (threadIdx.x == 0) bn.point_list[r.x] = (uint32_t)bn.keys[r.x];
+        if (threadIdx.x == 0) emit(bn.keys[r.x], bn.point_list + r.x, bn.smask + r.x, 0);
         return;
     }
-    sort_segment_lds<256, kSortSmallCap>(bn.keys + r.x, bn.point_list + r.x, n, smem);
+    sort_segment_lds<256, kSortSmallCap>(bn.keys + r.x, bn.point_list + r.x, bn.smask + r.x, n, smem);
 }
 
 __global__ __launch_bounds__(1024) void k_tile_sort_large(ImageArena im, BinArena bn, const uint32_t* ctrl) {
@@ -389,11 +454,11 @@ __global__ __launch_bounds__(1024) void k_tile_sort_large(ImageArena im, BinAren
         const uint2 r = im.ranges[im.large_list[w]];
         const int n = (int)(r.y - r.x);
         if (n <= kSortLargeCap) {
-            sort_segment_lds<1024, kSortLargeCap>(bn.keys + r.x, bn.point_list + r.x, n, smem);
+            sort_segment_lds<1024, kSortLargeCap>(bn.keys + r.x, bn.point_list + r.x, bn.smask + r.x, n, smem);
         } else {
             // pathological tile: bitonic network directly on the global segment
             bitonic_sort<1024>(bn.keys + r.x, n);
-            for (int i = threadIdx.x; i < n; i += 1024) bn.point_list[r.x + i] = (uint32_t)bn.keys[r.x + i];
+            for (int i = threadIdx.x; i < n; i += 1024) emit(bn.keys[r.x + i], bn.point_list + r.x, bn.smask + r.x, i);
         }
         __syncthreads();
     }

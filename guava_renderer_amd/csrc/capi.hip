@@ -3,6 +3,7 @@
 // reference's one host synchronisation (num_rendered sizes the binning buffer,
 // rasterizer_impl.cu:284-288); the batch entry points have none.
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -103,7 +104,7 @@ size_t carve_geom(char* base, const Dims& d, GeomArena* g) {
     a.cov3D = take<float>(base, off, 6 * n);
     a.conic = take<float4>(base, off, n);
     a.rect = take<uint2>(base, off, n);
-    a.rrec = take<float4>(base, off, 4 * n);
+    a.rrec = take<float4>(base, off, 2 * n);
     a.tiles = take<uint32_t>(base, off, n);
     a.offsets = take<uint32_t>(base, off, n);
     a.blocksums = take<uint32_t>(base, off, (size_t)d.B * d.nblk + 1);
@@ -133,6 +134,7 @@ size_t carve_bin(char* base, int64_t R, BinArena* b) {
     a.point_list = take<uint32_t>(base, off, n);
     a.keys = take<uint64_t>(base, off, n);
     a.inst_slot = take<uint32_t>(base, off, n);
+    a.smask = take<uint8_t>(base, off, n);
     if (b) *b = a;
     return align_up(off) + 256;
 }
@@ -195,6 +197,7 @@ int gsr_forward(gsr_alloc_fn geometryBuffer, gsr_alloc_fn binningBuffer, gsr_all
     (void)D; (void)M; (void)shs; (void)cam_pos;
     hipStream_t s = (hipStream_t)stream;
     if (P < 0 || width <= 0 || height <= 0) return fail(GSR_ERR_ARG, "bad P/width/height");
+    if (P >= kMaxGaussians) return fail(GSR_ERR_ARG, "P must be < 2^28");
     if (width > 16 * 65535 || height > 16 * 65535) return fail(GSR_ERR_ARG, "image too large");
     const Dims d = make_dims(1, P, width, height);
     GeomArena g;
@@ -326,6 +329,7 @@ int gsr_forward_batch(int B, int P, int width, int height, const float* means3D,
     hipStream_t s = (hipStream_t)stream;
     if (B <= 0 || P <= 0 || width <= 0 || height <= 0 || !workspace || !tanfov)
         return fail(GSR_ERR_ARG, "bad batch arguments");
+    if (P >= kMaxGaussians) return fail(GSR_ERR_ARG, "P must be < 2^28");
     if (!colors) return fail(GSR_ERR_NO_COLORS, "For non-RGB, provide precomputed Gaussian colors!");
     if (((uintptr_t)colors & 15) != 0 || ((colors_stride * 4) & 15) != 0)
         return fail(GSR_ERR_ARG, "colors must be 16-byte aligned per frame");

@@ -17,7 +17,9 @@ constexpr int kScanBlock = 256;       // Gaussians per preprocess / binning work
 constexpr int kSortSmallCap = 2048;   // instances per tile sorted by the 256-thread LDS sort
 constexpr int kSortLargeCap = 8192;   // instances per tile sorted by the 1024-thread LDS sort
 constexpr int kLdsTileHist = 8192;    // tiles per frame counted in LDS (more -> global atomics)
-constexpr int kRenderBatch = 64;      // Gaussians staged in LDS per render round
+constexpr int kRenderBatch = 64;      // Gaussians staged in LDS per render_bwd round
+constexpr int kStrips = 4;            // 16x4 pixel strips per 16x16 tile (one render wave each)
+constexpr int kMaxGaussians = 1 << 28; // Gaussian index field of the binning key (bits 4..31)
 
 // control words (uint32) at the head of the geometry arena
 enum Ctrl : int {
@@ -27,7 +29,10 @@ enum Ctrl : int {
     kCtrlNumLarge = 3,   // tiles whose list exceeds kSortSmallCap
     kCtrlRenderHead = 4, // render worklist dequeue counter
     kCtrlBwdHead = 5,    // render-backward worklist dequeue counter
-    kCtrlWords = 64
+    kCtrlNonEmpty = 6,   // tiles of the batch with a non-empty list
+    kCtrlXcdQueue = 1024,  // 8 per-XCD render dequeue counters, 4 KiB apart
+    kCtrlXcdStride = 1024,
+    kCtrlWords = 9216
 };
 
 struct GeomArena {
@@ -39,7 +44,8 @@ struct GeomArena {
     float* cov3D;
     float4* conic;
     uint2* rect;          // (xmin | ymin<<16, xmax | ymax<<16)
-    float4* rrec;         // render record, 4 x float4 per Gaussian (see render_fwd.hip)
+    float4* rrec;         // render record, 2 x float4 per Gaussian: (x, y, opacity, 1/depth),
+                          // (-a/2, -b, -c/2, 0) of the conic (see render_fwd.hip)
     uint32_t* tiles;
     uint32_t* offsets;    // inclusive scan of tiles over the batch
     uint32_t* blocksums;  // per scan block; scanned in place to exclusive block offsets
@@ -58,6 +64,8 @@ struct BinArena {
     uint32_t* point_list;  // per tile, depth-sorted Gaussian index (within its frame)
     uint64_t* keys;        // unsorted (depth bits << 32 | index), grouped per tile
     uint32_t* inst_slot;   // per (Gaussian, tile) instance: rank inside its tile's list
+    uint8_t* smask;        // per sorted instance: bit s set <=> the Gaussian can reach alpha >= 1/255
+                           // somewhere in the tile's 16x4 pixel strip s (render_fwd's wave unit)
 };
 
 struct Dims {

@@ -24,23 +24,6 @@ __device__ __forceinline__ void cov3d_fwd(const float s[3], float mod, const flo
     cov[3] = Sig.m[1][1]; cov[4] = Sig.m[1][2]; cov[5] = Sig.m[2][2];
 }
 
-// Conservative half-extents (pixels) of the region where alpha = min(0.99, o*exp(power)) can
-// reach 1/255: the bounding box of d^T Q d <= 2 ln(255 o) (Q = conic), inflated by 5% plus one
-// pixel, so that the render kernels may skip a (pixel block, Gaussian) pair outside the box without
-// changing any blend decision.  (-1,-1): o < 1/255, the Gaussian never contributes.  Very
-// ill-conditioned conics are never culled.
-__device__ __forceinline__ float2 alpha_extent(float a, float b, float c, float o) {
-    if (!(o >= 1.0f / 255.0f)) return make_float2(-1.f, -1.f);
-    const double da = a, db = b, dc = c;
-    const double det = da * dc - db * db;
-    const double tr = da + dc;
-    if (!(det > 0.0) || tr * tr > 1e5 * det) return make_float2(3.0e38f, 3.0e38f);
-    const double q = 2.0 * log(255.0 * (double)o) * 1.05 + 0.05;
-    const double hx = sqrt(q * dc / det) + 1.0;
-    const double hy = sqrt(q * da / det) + 1.0;
-    return make_float2((float)hx * 1.0001f, (float)hy * 1.0001f);
-}
-
 __global__ __launch_bounds__(kScanBlock) void k_preprocess(Dims d, Inputs in, GeomArena g, Outputs o) {
     const int b = blockIdx.y;
     const int i = blockIdx.x * kScanBlock + threadIdx.x;
@@ -131,12 +114,9 @@ __global__ __launch_bounds__(kScanBlock) void k_preprocess(Dims d, Inputs in, Ge
                     rect = make_uint2(rmin[0] | (rmin[1] << 16), rmax[0] | (rmax[1] << 16));
                     // render record (render_fwd.hip): position, opacity, 1/depth, pre-scaled conic
                     // (exact power-of-two scalings), conservative alpha >= 1/255 box
-                    const float2 e = alpha_extent(conic0, conic1, conic2, op * h_conv);
-                    float4* rr = g.rrec + 4 * gid;
+                    float4* rr = g.rrec + 2 * gid;
                     rr[0] = make_float4(pix0, pix1, op * h_conv, 1.0f / pv[2]);
                     rr[1] = make_float4(-0.5f * conic0, -conic1, -0.5f * conic2, 0.f);
-                    rr[2] = make_float4(pix0 - e.x, pix0 + e.x, pix1 - e.y, pix1 + e.y);
-                    rr[3] = make_float4(0.f, 0.f, 0.f, 0.f);
                 }
             }
         }

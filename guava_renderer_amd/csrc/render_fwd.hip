@@ -2,23 +2,25 @@
 // the reference).
 //
 // Structure (gfx950):
-//  * Persistent 256-thread workgroups dequeue 16x16 tiles from k_tile_scan's work list (longest
-//    list first), so every XCD gets work and the long tiles start early.
-//  * Each wave owns a 16x4 pixel strip of the tile (lane = pixel).  The tile's depth-sorted list
-//    is staged in rounds of 64 Gaussians by LDS-DMA (global_load_lds_dwordx4, double-buffered):
-//    a 64-byte render record per Gaussian (position, opacity, 1/depth, pre-scaled conic, cull box;
-//    written by preprocess) and its 128-byte feature row.  Round r+1 is in flight while round r is
-//    blended, and no staging data lives in VGPRs.
-//  * Per round every wave culls the 64 Gaussians against its strip with the conservative
-//    alpha >= 1/255 box (one lane per Gaussian, one ballot): a culled pair cannot change any blend
-//    decision, so the result is identical to visiting every pair.
-//  * Survivors are taken two at a time in list order (one MFMA k-step): each lane runs the
-//    branch-free blend step for its pixel (alpha, the T<1e-4 stop, n_contrib) giving the weight
-//    w = alpha*T (0 where the pixel does not take the Gaussian), and the 32-channel accumulation
-//    C += f*w runs on the matrix cores as D[ch][px] += F^T[ch][k] W[k][px] with
-//    v_mfma_f32_32x32x2_f32 over the strip's two 32-pixel halves.  The f32 MFMA is an exact
-//    k-ordered fma chain, i.e. bit-identical to fmaf(f, w, C) Gaussian by Gaussian (the oracle's
-//    contract); a zero weight leaves the accumulator unchanged.  An odd tail uses a null Gaussian.
+//  * The unit of work is one 16x4 pixel strip of a 16x16 tile, owned by ONE wave (lane = pixel).
+//    Waves dequeue strips independently from k_tile_scan's longest-first tile list (4 strips per
+//    entry), so there is no workgroup barrier anywhere: a wave whose pixels all finished moves on
+//    at once, and every XCD gets work.
+//  * The wave walks the tile's depth-sorted list 64 entries at a time (one coalesced load of indices
+//    and strip masks, prefetched one chunk ahead).  The binning pass already decided, with an exact
+//    conservative ellipse/rectangle test, whether each Gaussian can reach alpha >= 1/255 anywhere
+//    in each strip; one ballot over the strip bit gives the chunk's survivors.  A culled pair cannot
+//    change any blend decision, so the result is identical to visiting every pair.
+//  * Survivors are taken two at a time in list order (one MFMA k-step).  Their 32-byte render
+//    records arrive by scalar loads (the Gaussian index is wave-uniform) and feed the blend as SGPR
+//    operands; each lane runs the branch-free blend step for its pixel (alpha, the T<1e-4 stop,
+//    n_contrib) giving the weight w = alpha*T (0 where the pixel does not take the Gaussian).  The
+//    32-channel accumulation C += f*w runs on the matrix cores as D[ch][px] += F^T[ch][k] W[k][px]
+//    with v_mfma_f32_32x32x2_f32 over the strip's two 32-pixel halves, the feature operand loaded
+//    straight from HBM/L2 (lanes 0-31 one Gaussian's 128-byte row, lanes 32-63 the other's).  The
+//    f32 MFMA is an exact k-ordered fma chain, i.e. bit-identical to fmaf(f, w, C) Gaussian by
+//    Gaussian (the oracle's contract); a zero weight leaves the accumulator unchanged.
+//  * No LDS: occupancy is set by registers alone.
 //
 // Roofline: per frame the kernel must read 156 B per visible Gaussian (features + 2D attributes)
 // and write 140 B per pixel (32 channels, inverse depth, final_T, n_contrib).
@@ -27,11 +29,6 @@
 namespace gsr {
 
 typedef float floatx16 __attribute__((ext_vector_type(16)));
-
-constexpr int kRB = kRenderBatch;      // Gaussians per round (64)
-constexpr int kNull = kRB;             // slot of the null Gaussian in each buffer
-constexpr int kRecF4 = 4;              // float4 per render record
-constexpr int kSlots = kRB + 1;
 
 // One (pixel, Gaussian) step of the front-to-back blend (forward.cu:349-381), branch-free.
 // Returns the blend weight alpha*T (0 when the pixel does not take this Gaussian) and updates the
@@ -54,50 +51,101 @@ __device__ __forceinline__ float blend_one(const float4 ga, const float4 gc, flo
     return w;
 }
 
-__device__ __forceinline__ void glds16(const void* gsrc, void* lds_wave_base) {
-    __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)gsrc,
-                                     (__attribute__((address_space(3))) void*)lds_wave_base, 16, 0, 0);
+// Epilogue of one 16x4 strip: final_T, n_contrib, inverse depth (lane = pixel) and the 32
+// channel-major colour rows C + T*bg from the MFMA accumulators.  acc_n[r] at lane l holds channel
+// (r&3)+8*(r>>2)+4*(l>>5) of strip pixel 32n + (l&31), whose transmittance lives in lane 32n + (l&31).
+template <bool EMPTY>
+__device__ __forceinline__ void store_strip(const Dims& d, const ImageArena& im, const Outputs& o,
+                                            const float* bg, int b, int tx, int sy0, int lane,
+                                            const floatx16& acc0, const floatx16& acc1, float T,
+                                            float invd, uint32_t last) {
+    const int64_t HW = (int64_t)d.H * d.W;
+    const int px = tx * GSR_BX + (lane & 15);
+    const int py = sy0 + (lane >> 4);
+    if (px < d.W && py < d.H) {
+        const int64_t pix = b * HW + (int64_t)py * d.W + px;
+        im.final_T[pix] = T;
+        im.n_contrib[pix] = last;
+        if (o.out_invdepth) o.out_invdepth[pix] = invd;
+    }
+    const float T0 = __shfl(T, lane & 31);
+    const float T1 = __shfl(T, 32 + (lane & 31));
+    // channel rows through a buffer resource: one VGPR byte offset per half-strip row, the channel
+    // offset in an SGPR; pixels outside the image get an offset past the buffer and are dropped
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+        o.out_color + (int64_t)b * GSR_C * HW, 0, (int)((int64_t)GSR_C * HW * 4), 0x00020000);
+    const int j = lane & 31;
+    const int qx = tx * GSR_BX + (j & 15);
+    const int qy0 = sy0 + (j >> 4);
+    const int qy1 = qy0 + 2;
+    const int hoff = (lane >> 5) * 4 * (int)HW;  // channels +4 for the upper half-wave
+    const int v0 = (qx < d.W && qy0 < d.H) ? (hoff + qy0 * d.W + qx) * 4 : 0x7FFFFFF0;
+    const int v1 = (qx < d.W && qy1 < d.H) ? (hoff + qy1 * d.W + qx) * 4 : 0x7FFFFFF0;
+#pragma unroll
+    for (int r = 0; r < 16; r++) {
+        const int c = (r & 3) + 8 * (r >> 2);  // + 4 in the upper half-wave (in hoff)
+        const float bgc = (lane >> 5) ? bg[c + 4] : bg[c];
+        const int so = c * (int)HW * 4;
+        const float x0 = EMPTY ? bgc : fmaf(T0, bgc, acc0[r]);
+        const float x1 = EMPTY ? bgc : fmaf(T1, bgc, acc1[r]);
+        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(x0), rs, v0, so, 0);
+        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(x1), rs, v1, so, 0);
+    }
 }
 
+// Work items, in k_tile_scan's longest-first order: the 4 strips of each non-empty tile
+// (items [0, 4*NE)), then each empty tile whole (items [4*NE, 3*NE + B*T)).  Eight queues, one per
+// XCD, take every eighth item (item = x + 8k); a wave dequeues from its own XCD's queue and, once
+// that is drained, from the others, so no counter sees more than a fraction of the traffic.
 template <bool EXACT, bool STATS>
 __global__ __launch_bounds__(GSR_TILE_PIX) void k_render_fwd(Dims d, Inputs in, GeomArena g,
                                                              ImageArena im, BinArena bn, Outputs o) {
-    __shared__ __attribute__((aligned(16))) float4 s_rec[2][kSlots * kRecF4];
-    __shared__ __attribute__((aligned(16))) float s_f[2][kSlots * GSR_C];
-    __shared__ int s_done[GSR_TILE_PIX / 64];
-    __shared__ int s_item;
     if (g.ctrl[kCtrlOverflow]) return;
-    const int ntiles = d.B * d.T;
+    const uint32_t ne = g.ctrl[kCtrlNonEmpty];
+    const uint32_t nstrip = 4u * ne;
+    const uint32_t nitems = nstrip + (uint32_t)(d.B * d.T) - ne;
     const int lane = threadIdx.x & 63;
-    const int wv = threadIdx.x >> 6;
-    // null Gaussian in both buffers: power 0, opacity 0 -> alpha 0, never taken, zero features
-    if (threadIdx.x < 2 * kRecF4)
-        s_rec[threadIdx.x >> 2][kNull * kRecF4 + (threadIdx.x & 3)] = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (threadIdx.x < 2 * GSR_C) s_f[threadIdx.x >> 5][kNull * GSR_C + (threadIdx.x & 31)] = 0.f;
-    // DMA lane roles: records of Gaussians 16*wv + lane/4 (part lane%4), features of Gaussians
-    // 16*wv + lane/8 and 16*wv + 8 + lane/8 (part lane%8)
-    const int rg = 16 * wv + (lane >> 2), rp = lane & 3;
-    const int fg0 = 16 * wv + (lane >> 3), fg1 = fg0 + 8, fp = lane & 7;
+    const int hi = lane >> 5;
+    const int ch = lane & 31;
+    uint32_t q = __builtin_amdgcn_s_getreg((3 << 11) | 20) & 7u;  // HW_REG_XCC_ID
+    uint32_t q_left = 8;
 
     for (;;) {
-        if (threadIdx.x == 0) s_item = (int)atomicAdd(&g.ctrl[kCtrlRenderHead], 1u);
-        __syncthreads();
-        const int item = s_item;
-        if (item >= ntiles) break;
-        const int tile_g = (int)im.work_list[item];
+        uint32_t item = 0xFFFFFFFFu;
+        while (q_left) {
+            uint32_t k = 0;
+            if (lane == 0) k = atomicAdd(&g.ctrl[kCtrlXcdQueue + kCtrlXcdStride * q], 1u);
+            k = __builtin_amdgcn_readfirstlane(k);
+            item = q + 8u * k;
+            if (item < nitems) break;
+            q = (q + 1) & 7u;
+            q_left--;
+        }
+        if (!q_left) break;
+        if (item >= nstrip) {  // empty tile: background everywhere, T = 1
+            const int tile_g = (int)im.work_list[ne + (item - nstrip)];
+            const int b = tile_g / d.T;
+            const int t = tile_g - b * d.T;
+            const floatx16 unused = {};
+            for (int sp = 0; sp < kStrips; sp++)
+                store_strip<true>(d, im, o, in.bg + in.s_bg * b, b, t % d.gx, (t / d.gx) * GSR_BY + sp * 4,
+                                  lane, unused, unused, 1.0f, 0.f, 0u);
+            continue;
+        }
+        const int tile_g = (int)im.work_list[item >> 2];
+        const int strip = (int)(item & 3u);
         const int b = tile_g / d.T;
         const int t = tile_g - b * d.T;
         const int tx = t % d.gx, ty = t / d.gx;
         const int px = tx * GSR_BX + (lane & 15);
-        const int py = ty * GSR_BY + wv * 4 + (lane >> 4);
+        const int py = ty * GSR_BY + strip * 4 + (lane >> 4);
         const bool inside = px < d.W && py < d.H;
         const float pfx = (float)px, pfy = (float)py;
-        const float sx0 = (float)(tx * GSR_BX), sx1 = sx0 + 15.0f;
-        const float sy0 = (float)(ty * GSR_BY + wv * 4), sy1 = sy0 + 3.0f;
         const uint2 range = im.ranges[tile_g];
         const int n = (int)(range.y - range.x);
         const uint32_t* __restrict__ plist = bn.point_list + range.x;
-        const float4* __restrict__ rrec = g.rrec + (int64_t)b * d.P * kRecF4;
+        const uint8_t* __restrict__ smask = bn.smask + range.x;
+        const float4* __restrict__ rrec = g.rrec + (int64_t)b * d.P * 2;
         const float* __restrict__ colors = in.colors + in.s_colors * b;
 
         floatx16 acc0, acc1;
@@ -109,135 +157,121 @@ __global__ __launch_bounds__(GSR_TILE_PIX) void k_render_fwd(Dims d, Inputs in, 
         uint64_t n_surv = 0, n_steps = 0, n_contrib_pairs = 0, n_staged = 0;
         uint32_t stop = 0;
 
-        // stage round `base` into buffer `buf` (lanes beyond the list stay idle)
-#define GSR_ISSUE(base_, buf_)                                                                      \
+        // Survivor stream: wave-uniform state walking the list 64 entries at a time; the next
+        // chunk's indices and strip masks are always in flight.
+        int base = -64;
+        uint64_t mask = 0;
+        uint32_t cidx = 0;
+        uint32_t nidx = lane < n ? plist[lane] : 0u;
+        uint32_t nmsk = lane < n ? (uint32_t)smask[lane] : 0u;
+        // next survivor -> (g, pos); false at the end of the list
+#define GSR_NEXT(g_, pos_)                                                                          \
+        ({                                                                                          \
+            bool ok_ = true;                                                                        \
+            while (mask == 0) {                                                                     \
+                base += 64;                                                                         \
+                if (base >= n) { ok_ = false; break; }                                              \
+                cidx = nidx;                                                                        \
+                const uint32_t cm_ = nmsk;                                                          \
+                if (base + 64 < n) {                                                                \
+                    const int j_ = base + 64 + lane;                                                \
+                    nidx = j_ < n ? plist[j_] : 0u;                                                 \
+                    nmsk = j_ < n ? (uint32_t)smask[j_] : 0u;                                       \
+                }                                                                                   \
+                mask = __ballot(lane < n - base && ((cm_ >> strip) & 1u));                          \
+                if (STATS) n_staged += min(64, n - base);                                           \
+            }                                                                                       \
+            if (ok_) {                                                                              \
+                const int i_ = (int)__builtin_ctzll(mask);                                          \
+                mask &= mask - 1;                                                                   \
+                g_ = __builtin_amdgcn_readlane(cidx, i_);                                           \
+                pos_ = base + i_ + 1;                                                               \
+            }                                                                                       \
+            ok_;                                                                                    \
+        })
+        // fetch the next k-step (two survivors) into register set S: render records (uniform
+        // vector loads, in-order completion) and this lane's feature operand
+#define GSR_FETCH(S)                                                                                \
         {                                                                                           \
-            if ((base_) + rg < n)                                                                   \
-                glds16(rrec + (int64_t)ir * kRecF4 + rp, &s_rec[(buf_)][(16 * wv) * kRecF4]);       \
-            if ((base_) + fg0 < n)                                                                  \
-                glds16(colors + (int64_t)if0 * GSR_C + fp * 4, &s_f[(buf_)][(16 * wv) * GSR_C]);    \
-            if ((base_) + fg1 < n)                                                                  \
-                glds16(colors + (int64_t)if1 * GSR_C + fp * 4, &s_f[(buf_)][(16 * wv + 8) * GSR_C]);\
+            uint32_t ga_ = 0, gb_ = 0;                                                              \
+            int pa_ = 0, pb_ = 0;                                                                   \
+            S##v = GSR_NEXT(ga_, pa_);                                                              \
+            S##hb = S##v && GSR_NEXT(gb_, pb_);                                                     \
+            if (!S##hb) { gb_ = ga_; pb_ = pa_; }                                                   \
+            S##pa = pa_; S##pb = pb_;                                                               \
+            S##a0 = rrec[2 * ga_]; S##a1 = rrec[2 * ga_ + 1];                                       \
+            S##b0 = rrec[2 * gb_]; S##b1 = rrec[2 * gb_ + 1];                                       \
+            S##f = colors[(int64_t)(hi ? gb_ : ga_) * GSR_C + ch];                                  \
         }
-#define GSR_PREFETCH_IDX(nb_)                                                                       \
+        // blend the k-step held in S and accumulate it on the matrix cores
+#define GSR_BLEND(S)                                                                                \
         {                                                                                           \
-            ir = ((nb_) + rg < n) ? (int)plist[(nb_) + rg] : 0;                                     \
-            if0 = ((nb_) + fg0 < n) ? (int)plist[(nb_) + fg0] : 0;                                  \
-            if1 = ((nb_) + fg1 < n) ? (int)plist[(nb_) + fg1] : 0;                                  \
+            const float4 a0_ = make_float4(S##a0.x, S##a0.y, S##v ? S##a0.z : 0.f, S##a0.w);        \
+            const float4 b0_ = make_float4(S##b0.x, S##b0.y, S##hb ? S##b0.z : 0.f, S##b0.w);       \
+            const float f_ = (S##v && (!hi || S##hb)) ? S##f : 0.f;                                 \
+            const bool was_done_ = done;                                                            \
+            const float wa_ = blend_one<EXACT>(a0_, S##a1, pfx, pfy, S##pa, T, invd, last, done);   \
+            const bool done_a_ = done;                                                              \
+            const float wb_ = blend_one<EXACT>(b0_, S##b1, pfx, pfy, S##pb, T, invd, last, done);   \
+            if (STATS) {                                                                            \
+                if (!was_done_ && done_a_) stop = (uint32_t)S##pa;                                  \
+                else if (!done_a_ && done) stop = (uint32_t)S##pb;                                  \
+                n_contrib_pairs += __popcll(__ballot(wa_ > 0.f)) + __popcll(__ballot(wb_ > 0.f));   \
+                n_steps += S##v ? 1 : 0;                                                            \
+                n_surv += S##v ? (S##hb ? 2 : 1) : 0;                                               \
+            }                                                                                       \
+            const auto sw_ = __builtin_amdgcn_permlane32_swap(__float_as_uint(wa_),                 \
+                                                              __float_as_uint(wb_), false, false);  \
+            acc0 = __builtin_amdgcn_mfma_f32_32x32x2f32(f_, __uint_as_float(sw_[0]), acc0, 0, 0, 0); \
+            acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(f_, __uint_as_float(sw_[1]), acc1, 0, 0, 0); \
         }
-        int ir, if0, if1;
-        GSR_PREFETCH_IDX(0)
-        if (n > 0) GSR_ISSUE(0, 0)
-        GSR_PREFETCH_IDX(kRB)
-        __syncthreads();  // round 0 landed (the barrier drains the DMA); s_item consumed
-
-        int buf = 0;
-        for (int base = 0; base < n; base += kRB) {
-            if (base + kRB < n) {
-                GSR_ISSUE(base + kRB, buf ^ 1)
-                GSR_PREFETCH_IDX(base + 2 * kRB)
-            }
-            const int cnt = min(kRB, n - base);
-            if (STATS) n_staged += cnt;
-            const float4* __restrict__ rec = s_rec[buf];
-            const float* __restrict__ fb = s_f[buf];
-            if (__any(!done)) {
-                bool keep = false;
-                if (lane < cnt) {
-                    const float4 bx = rec[lane * kRecF4 + 2];
-                    keep = bx.y >= sx0 && bx.x <= sx1 && bx.w >= sy0 && bx.z <= sy1;
-                }
-                uint64_t mask = __ballot(keep);
-                if (STATS) n_surv += __popcll(mask);
-                const int hi = lane >> 5;
-                const int ch = lane & 31;
-                while (mask) {
-                    const int ia = (int)__builtin_ctzll(mask);
-                    mask &= mask - 1;
-                    const int ib = mask ? (int)__builtin_ctzll(mask) : kNull;
-                    mask &= mask - 1;
-                    const float fa = fb[(hi ? ib : ia) * GSR_C + ch];
-                    const bool was_done = done;
-                    const float wa = blend_one<EXACT>(rec[ia * kRecF4], rec[ia * kRecF4 + 1], pfx, pfy,
-                                                      base + ia + 1, T, invd, last, done);
-                    const bool done_a = done;
-                    const float wb = blend_one<EXACT>(rec[ib * kRecF4], rec[ib * kRecF4 + 1], pfx, pfy,
-                                                      base + ib + 1, T, invd, last, done);
-                    if (STATS) {
-                        // list position at which a pixel terminated inside this step
-                        if (!was_done && done_a) stop = (uint32_t)(base + ia + 1);
-                        else if (!done_a && done) stop = (uint32_t)(base + ib + 1);
-                        n_contrib_pairs += __popcll(__ballot(wa > 0.f)) + __popcll(__ballot(wb > 0.f));
-                        n_steps++;
-                    }
-                    const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(wa), __float_as_uint(wb),
-                                                                     false, false);
-                    acc0 = __builtin_amdgcn_mfma_f32_32x32x2f32(fa, __uint_as_float(sw[0]), acc0, 0, 0, 0);
-                    acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(fa, __uint_as_float(sw[1]), acc1, 0, 0, 0);
-                }
-            }
-            const bool wave_busy = __any(!done);
-            if (lane == 0) s_done[wv] = wave_busy ? 0 : 1;
-            __syncthreads();  // also retires the next round's DMA for every wave
-            const bool all = s_done[0] && s_done[1] && s_done[2] && s_done[3];
-            buf ^= 1;
-            if (all) break;
+        // two register sets, so step s+1's loads are in flight while step s is blended.  The loop
+        // leaves only at its head and its foot (an invalid set blends as two null Gaussians), which
+        // keeps the MFMA accumulators in one register chain.
+        bool Av, Ahb, Bv, Bhb;
+        int Apa, Apb, Bpa, Bpb;
+        float4 Aa0, Aa1, Ab0, Ab1, Ba0, Ba1, Bb0, Bb1;
+        float Af, Bf;
+        GSR_FETCH(A)
+        GSR_FETCH(B)
+        while (Av) {
+            GSR_BLEND(A)
+            GSR_FETCH(A)
+            GSR_BLEND(B)
+            GSR_FETCH(B)
+            if (!__any(!done)) break;  // every pixel of the strip finished
         }
-#undef GSR_ISSUE
-#undef GSR_PREFETCH_IDX
+#undef GSR_NEXT
+#undef GSR_FETCH
+#undef GSR_BLEND
 
         // ---- epilogue ----
-        const int64_t HW = (int64_t)d.H * d.W;
         if (STATS) {
-            unsigned long long* cnt = (unsigned long long*)o.stats;
+            unsigned long long* cn = (unsigned long long*)o.stats;
             uint64_t ev = inside ? (done ? stop : (uint32_t)n) : 0;
             for (int off = 32; off > 0; off >>= 1) ev += __shfl_xor(ev, off);
             if (lane == 0) {
-                atomicAdd(&cnt[0], (unsigned long long)ev);
-                atomicAdd(&cnt[1], (unsigned long long)n_contrib_pairs);
-                atomicAdd(&cnt[2], (unsigned long long)n_surv);
-                atomicAdd(&cnt[3], (unsigned long long)n_steps);
-                if (wv == 0) {
-                    atomicAdd(&cnt[4], (unsigned long long)n_staged);
-                    atomicAdd(&cnt[5], (unsigned long long)n);
-                    atomicAdd(&cnt[6], 1ull);
+                atomicAdd(&cn[0], (unsigned long long)ev);
+                atomicAdd(&cn[1], (unsigned long long)n_contrib_pairs);
+                atomicAdd(&cn[2], (unsigned long long)n_surv);
+                atomicAdd(&cn[3], (unsigned long long)n_steps);
+                atomicAdd(&cn[4], (unsigned long long)n_staged);
+                if (strip == 0) {
+                    atomicAdd(&cn[5], (unsigned long long)n);
+                    atomicAdd(&cn[6], 1ull);
                 }
             }
         }
-        if (inside) {
-            const int64_t pix = (int64_t)py * d.W + px;
-            im.final_T[b * HW + pix] = T;
-            im.n_contrib[b * HW + pix] = last;
-            if (o.out_invdepth) o.out_invdepth[b * HW + pix] = invd;
-        }
-        // acc_n[r] at lane l = channel (r&3)+8*(r>>2)+4*(l>>5) of strip pixel 32n + (l&31), whose
-        // transmittance lives in lane 32n + (l&31).
-        const float T0 = __shfl(T, lane & 31);
-        const float T1 = __shfl(T, 32 + (lane & 31));
-        const float* bg = in.bg + in.s_bg * b;
-        float* out = o.out_color + (int64_t)b * GSR_C * HW;
-        const int j = lane & 31;
-        const int qx = tx * GSR_BX + (j & 15);
-        const int qy0 = ty * GSR_BY + wv * 4 + (j >> 4);
-        const int qy1 = qy0 + 2;
-        const bool in0 = qx < d.W && qy0 < d.H;
-        const bool in1 = qx < d.W && qy1 < d.H;
-#pragma unroll
-        for (int r = 0; r < 16; r++) {
-            const int ch = (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
-            const float bgc = bg[ch];
-            if (in0) out[ch * HW + (int64_t)qy0 * d.W + qx] = fmaf(T0, bgc, acc0[r]);
-            if (in1) out[ch * HW + (int64_t)qy1 * d.W + qx] = fmaf(T1, bgc, acc1[r]);
-        }
-        __syncthreads();  // LDS buffers and s_item are reused by the next tile
+        store_strip<false>(d, im, o, in.bg + in.s_bg * b, b, tx, ty * GSR_BY + strip * 4, lane, acc0, acc1, T,
+                           invd, last);
     }
 }
 
 void launch_render_fwd(const Dims& d, const Inputs& in, const GeomArena& g, const ImageArena& im,
                        const BinArena& b, const Outputs& o, bool exact, hipStream_t s) {
-    const int ntiles = d.B * d.T;
-    if (ntiles == 0) return;
-    const int grid = min(ntiles, persistent_grid(4));
+    const int nwaves = d.B * d.T * kStrips;  // upper bound of the work items
+    if (nwaves == 0) return;
+    const int grid = min((nwaves + 3) / 4, persistent_grid(8));
     const dim3 gr(grid), bl(GSR_TILE_PIX);
     if (o.stats) {
         if (exact) hipLaunchKernelGGL((k_render_fwd<true, true>), gr, bl, 0, s, d, in, g, im, b, o);

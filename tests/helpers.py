@@ -22,9 +22,9 @@ def _carve(spec):
 
 def geom_layout(P):
     nblk = (P + 255) // 256
-    return _carve([("ctrl", np.uint32, 64), ("depth", np.float32, P), ("invdepth", np.float32, P),
+    return _carve([("ctrl", np.uint32, 9216), ("depth", np.float32, P), ("invdepth", np.float32, P),
                    ("radii", np.int32, P), ("means2D", np.float32, 2 * P), ("cov3D", np.float32, 6 * P),
-                   ("conic", np.float32, 4 * P), ("rect", np.uint32, 2 * P), ("rrec", np.float32, 16 * P), ("tiles", np.uint32, P),
+                   ("conic", np.float32, 4 * P), ("rect", np.uint32, 2 * P), ("rrec", np.float32, 8 * P), ("tiles", np.uint32, P),
                    ("offsets", np.uint32, P), ("blocksums", np.uint32, nblk + 1)])
 
 
@@ -37,7 +37,8 @@ def image_layout(W, H):
 
 def bin_layout(R):
     n = max(R, 1)
-    return _carve([("point_list", np.uint32, n), ("keys", np.uint64, n), ("inst_slot", np.uint32, n)])
+    return _carve([("point_list", np.uint32, n), ("keys", np.uint64, n), ("inst_slot", np.uint32, n),
+                   ("smask", np.uint8, n)])
 
 
 def decode(buf_np, layout):
