@@ -141,7 +141,7 @@ def main():
     assert not ovf
     P_vis = int((rast.radii > 0).sum().item())
     profile_read()  # reset accumulators
-    profile_enable(("preprocess", "scan", "bin_count", "tile_scan", "bin_scatter", "tile_sort",
+    profile_enable(("preprocess", "scan", "depth_sort", "chunk_count", "tile_scan", "ordered_scatter",
                     "render_fwd") if a.stages else ("render_fwd",))
     if dist is not None:
         dist.barrier()

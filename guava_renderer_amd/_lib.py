@@ -51,7 +51,7 @@ def load(path=None):
     L.gsr_last_error.restype = ctypes.c_char_p
     L.gsr_set_exact_exp.argtypes = [_i]
     L.gsr_set_exact_exp.restype = _i
-    L.gsr_geometry_bytes.argtypes = [_i]
+    L.gsr_geometry_bytes.argtypes = [_i, _i, _i]
     L.gsr_geometry_bytes.restype = _sz
     L.gsr_image_bytes.argtypes = [_i, _i]
     L.gsr_image_bytes.restype = _sz

@@ -12,7 +12,7 @@ import torch
 from . import _lib
 
 C = 32
-STAGES = ("preprocess", "scan", "bin_count", "tile_scan", "bin_scatter", "tile_sort", "render_fwd",
+STAGES = ("preprocess", "scan", "depth_sort", "chunk_count", "tile_scan", "ordered_scatter", "render_fwd",
           "render_bwd", "preprocess_bwd")
 
 

@@ -23,6 +23,11 @@ FLAGS = ["-O3", "-std=c++17", "-fPIC", "-ffp-contract=off", f"--offload-arch={AR
          "-Wno-unused-result", "-I" + CSRC, "-I" + os.path.join(os.path.dirname(HERE), "include")]
 
 
+# per-source extras: no SLP packing in the render kernel (packed f32 VALU beside MFMAs costs more
+# issue slots than the scalar pair, MI355X_MICROARCH.md "price of one filler")
+EXTRA = {"render_fwd.hip": ["-fno-slp-vectorize"]}
+
+
 def _newer(src_paths, dst):
     if not os.path.exists(dst):
         return True
@@ -35,7 +40,7 @@ def _compile(src):
     deps = [os.path.join(CSRC, src)] + [os.path.join(CSRC, h) for h in os.listdir(CSRC) if h.endswith(".h")]
     deps.append(os.path.join(os.path.dirname(HERE), "include", "gsr.h"))
     if _newer(deps, obj):
-        cmd = [HIPCC] + FLAGS + ["-c", os.path.join(CSRC, src), "-o", obj]
+        cmd = [HIPCC] + FLAGS + EXTRA.get(src, []) + ["-c", os.path.join(CSRC, src), "-o", obj]
         r = subprocess.run(cmd, capture_output=True, text=True)
         if r.returncode != 0:
             raise RuntimeError(f"hipcc failed for {src}:\n{r.stdout}\n{r.stderr}")

@@ -1,4 +1,4 @@
-// binning.hip -- tile binning and per-tile depth sort (replaces rasterizer_impl.cu:280-320 of the
+// binning.hip -- tile binning with depth-ordered lists (replaces rasterizer_impl.cu:280-320 of the
 // reference: cub InclusiveSum, duplicateWithKeys, cub DeviceRadixSort over 32+msb(T) key bits,
 // identifyTileRanges).
 //
@@ -6,18 +6,21 @@
 // tile rect covers t, ordered by (depth float bits, Gaussian index) -- exactly the order a stable
 // LSD sort of (tile<<32 | depth bits) over Gaussian-major emission produces.
 //
-// MI355X structure (no global radix sort):
-//   1. k_scan_blocksums   exclusive scan of the per-256-Gaussian tile counts (1 workgroup)
-//   2. k_bin_count        per 256 Gaussians: instance offsets + LDS tile histogram; one global
-//                         atomic per (workgroup, tile) hands out each workgroup's slot range
-//   3. k_tile_scan        exclusive scan of per-tile counts -> ranges; worklist of long tiles
-//   4. k_bin_scatter      each instance writes its 64-bit (depth bits, index, strip mask) key into
-//                         its tile's segment (order inside a segment arbitrary)
-//   5. k_tile_sort_*      one workgroup per tile sorts its segment in LDS: linear bucket pass on
-//                         the depth bits + in-bucket ranking on the full key (O(n) for smooth depth
-//                         distributions); bitonic in LDS for degenerate buckets; bitonic in global
-//                         memory for tiles longer than kSortLargeCap.
-// All passes are HBM/L2-bound integer work: 4+4+8+8+5 B per instance.
+// MI355X structure: the instances (Gaussian x tile, ~6 per Gaussian) are never sorted.  The
+// Gaussians are sorted once per frame by (depth bits, index); emitting instances in that order
+// with stable per-tile ranks yields every tile's list already ordered.
+//   1. k_scan_blocksums    exclusive scan of the per-256-Gaussian tile counts -> R (1 workgroup)
+//   2. depth sort          per frame: bucket count on the depth bits (range from preprocess),
+//                          bucket scan, scatter of (depth bits, index) keys, in-place ranking of
+//                          small buckets, LDS segment sort of the few large ones -> order[]
+//   3. k_chunk_count       per 256 depth-ordered Gaussians: tile histogram in LDS from 4 corner
+//                          updates per rect (2-D difference array) -> count table row;
+//      k_column_scan       per tile: exclusive scan down the table -> chunk bases, tile counts
+//   4. k_tile_scan         tile counts -> ranges, longest-first render work list
+//   5. k_ordered_scatter   per chunk: load-balanced expansion of the instances over the workgroup,
+//                          stable rank = tile base + chunk base + earlier slots covering the tile
+//                          (popcount of row/column ballots), plus the exact 16x4 strip mask
+// Traffic per instance: 4 B point_list + 1 B strip mask written once; per Gaussian a few words.
 #include "gsr_internal.h"
 
 namespace gsr {
@@ -52,8 +55,11 @@ __device__ __forceinline__ TV block_excl_scan(TV v, TV* total, TV* sh /* NT/64 +
 }
 
 // ---------------------------------------------------------------- 1. block-sum scan
+// Also reduces the blocks' depth-key ranges to per-frame ranges for the bucket sort.
 __global__ __launch_bounds__(1024) void k_scan_blocksums(uint32_t* __restrict__ bs, int n,
-                                                         uint32_t* ctrl, int64_t R_cap) {
+                                                         uint32_t* ctrl, int64_t R_cap,
+                                                         const uint32_t* __restrict__ bkey, uint32_t* fstat,
+                                                         int nblk) {
     __shared__ uint64_t sh[1024 / 64 + 1];
     const int per = (n + 1023) / 1024;
     const int beg = threadIdx.x * per;
@@ -62,11 +68,21 @@ __global__ __launch_bounds__(1024) void k_scan_blocksums(uint32_t* __restrict__ 
     for (int i = beg; i < end; i++) s += bs[i];
     uint64_t total;
     uint64_t ex = block_excl_scan<uint64_t, 1024>(s, &total, sh);
+    uint32_t km = 0, nkm = 0;
+    int f = beg / nblk;
     for (int i = beg; i < end; i++) {
         const uint32_t v = bs[i];
         bs[i] = (uint32_t)ex;
         ex += v;
+        if (i / nblk != f) {  // frame boundary inside this thread's range
+            if (km) { atomicMax(&fstat[kFsWords * f + kFsKeyMax], km); atomicMax(&fstat[kFsWords * f + kFsNotKeyMax], nkm); }
+            km = nkm = 0;
+            f = i / nblk;
+        }
+        km = max(km, bkey[2 * i]);
+        nkm = max(nkm, bkey[2 * i + 1]);
     }
+    if (km) { atomicMax(&fstat[kFsWords * f + kFsKeyMax], km); atomicMax(&fstat[kFsWords * f + kFsNotKeyMax], nkm); }
     if (threadIdx.x == 0) {
         ctrl[kCtrlRLo] = (uint32_t)min(total, (uint64_t)0xFFFFFFFFu);
         ctrl[kCtrlOverflow] = (total > (uint64_t)R_cap || total >= 0xFFFFFFF0ull) ? 1u : 0u;
@@ -75,203 +91,10 @@ __global__ __launch_bounds__(1024) void k_scan_blocksums(uint32_t* __restrict__ 
 
 void launch_scan_blocksums(const Dims& d, const GeomArena& g, int64_t R_cap, hipStream_t s) {
     hipLaunchKernelGGL(k_scan_blocksums, dim3(1), dim3(1024), 0, s, g.blocksums, d.B * d.nblk, g.ctrl,
-                       R_cap);
+                       R_cap, g.blockkey, g.fstat, d.nblk);
 }
 
-// ---------------------------------------------------------------- 2. offsets + tile counts
-__global__ __launch_bounds__(kScanBlock) void k_bin_count(Dims d, GeomArena g, ImageArena im,
-                                                          BinArena bn) {
-    extern __shared__ uint32_t hist[];  // d.T entries when d.T <= kLdsTileHist
-    __shared__ uint32_t sh[kScanBlock / 64 + 1];
-    if (g.ctrl[kCtrlOverflow]) return;
-    const int b = blockIdx.y;
-    const int i = blockIdx.x * kScanBlock + threadIdx.x;
-    const int64_t gid = (int64_t)b * d.P + i;
-    const bool valid = i < d.P;
-    const uint32_t tiles = valid ? g.tiles[gid] : 0u;
-    uint32_t total;
-    const uint32_t excl = block_excl_scan<uint32_t, kScanBlock>(tiles, &total, sh) +
-                          g.blocksums[(int64_t)b * d.nblk + blockIdx.x];
-    if (valid) g.offsets[gid] = excl + tiles;
-    const bool use_lds = d.T <= kLdsTileHist;
-    if (use_lds) {
-        for (int t = threadIdx.x; t < d.T; t += kScanBlock) hist[t] = 0;
-        __syncthreads();
-    }
-    uint32_t* gcount = im.tile_count + (int64_t)b * d.T;
-    uint2 rect = make_uint2(0, 0);
-    if (tiles) {
-        rect = g.rect[gid];
-        const uint32_t x0 = rect.x & 0xFFFF, y0 = rect.x >> 16, x1 = rect.y & 0xFFFF, y1 = rect.y >> 16;
-        uint32_t k = excl;
-        for (uint32_t y = y0; y < y1; y++)
-            for (uint32_t x = x0; x < x1; x++) {
-                const uint32_t t = y * (uint32_t)d.gx + x;
-                bn.inst_slot[k++] = use_lds ? atomicAdd(&hist[t], 1u) : atomicAdd(&gcount[t], 1u);
-            }
-    }
-    if (!use_lds) return;
-    __syncthreads();
-    for (int t = threadIdx.x; t < d.T; t += kScanBlock) {
-        const uint32_t c = hist[t];
-        if (c) hist[t] = atomicAdd(&gcount[t], c);
-    }
-    __syncthreads();
-    if (tiles) {
-        const uint32_t x0 = rect.x & 0xFFFF, y0 = rect.x >> 16, x1 = rect.y & 0xFFFF, y1 = rect.y >> 16;
-        uint32_t k = excl;
-        for (uint32_t y = y0; y < y1; y++)
-            for (uint32_t x = x0; x < x1; x++) {
-                const uint32_t t = y * (uint32_t)d.gx + x;
-                bn.inst_slot[k] += hist[t];
-                k++;
-            }
-    }
-}
-
-void launch_bin_count(const Dims& d, const GeomArena& g, const ImageArena& im, const BinArena& b,
-                      hipStream_t s) {
-    if (d.P == 0 || d.B == 0) return;
-    const size_t lds = d.T <= kLdsTileHist ? (size_t)d.T * 4 : 0;
-    hipLaunchKernelGGL(k_bin_count, dim3(d.nblk, d.B), dim3(kScanBlock), lds, s, d, g, im, b);
-}
-
-// ---------------------------------------------------------------- 3. tile ranges
-// Also emits the render worklist: every tile of the batch ordered by descending log2 list length
-// (counting sort over 34 buckets; empty tiles last), so persistent render workgroups take the
-// longest tiles first (LPT scheduling) and no XCD is left with only empty tiles.
-__global__ __launch_bounds__(1024) void k_tile_scan(int n, const uint32_t* __restrict__ cnt,
-                                                    uint2* __restrict__ ranges, uint32_t* ctrl,
-                                                    uint32_t* large_list, uint32_t* work_list) {
-    constexpr int kBuckets = 34;  // bucket 0: longest (2^32..), bucket 33: empty
-    __shared__ uint32_t sh[1024 / 64 + 1];
-    __shared__ uint32_t bcount[kBuckets];
-    const bool ovf = ctrl[kCtrlOverflow] != 0;
-    if (threadIdx.x < kBuckets) bcount[threadIdx.x] = 0;
-    const int per = (n + 1023) / 1024;
-    const int beg = threadIdx.x * per;
-    const int end = min(n, beg + per);
-    uint32_t s = 0;
-    if (!ovf)
-        for (int i = beg; i < end; i++) s += cnt[i];
-    uint32_t total;
-    uint32_t ex = block_excl_scan<uint32_t, 1024>(s, &total, sh);  // (barriers order bcount init)
-    for (int i = beg; i < end; i++) {
-        const uint32_t c = ovf ? 0u : cnt[i];
-        // empty tiles keep the reference's memset value (0,0) (rasterizer_impl.cu:313)
-        ranges[i] = c ? make_uint2(ex, ex + c) : make_uint2(0u, 0u);
-        if (c > (uint32_t)kSortSmallCap) large_list[atomicAdd(&ctrl[kCtrlNumLarge], 1u)] = (uint32_t)i;
-        const int bk = c ? __clz(c) : kBuckets - 1;
-        atomicAdd(&bcount[bk], 1u);
-        ex += c;
-    }
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        uint32_t acc = 0;
-        for (int k = 0; k < kBuckets; k++) {
-            if (k == kBuckets - 1) ctrl[kCtrlNonEmpty] = acc;
-            const uint32_t v = bcount[k];
-            bcount[k] = acc;
-            acc += v;
-        }
-    }
-    __syncthreads();
-    for (int i = beg; i < end; i++) {
-        const uint32_t c = ovf ? 0u : cnt[i];
-        const int bk = c ? __clz(c) : kBuckets - 1;
-        work_list[atomicAdd(&bcount[bk], 1u)] = (uint32_t)i;
-    }
-}
-
-void launch_tile_scan(const Dims& d, const GeomArena& g, const ImageArena& im, hipStream_t s) {
-    hipLaunchKernelGGL(k_tile_scan, dim3(1), dim3(1024), 0, s, d.B * d.T, im.tile_count, im.ranges,
-                       g.ctrl, im.large_list, im.work_list);
-}
-
-// ---------------------------------------------------------------- 4. scatter keys
-// Minimum over the pixel-centre rectangle dx in [dxl, dxh], dy in [dyl, dyh] (dx = mean - pixel)
-// of the conic's quadratic form Q = a dx^2 + 2b dx dy + c dy^2 (power = -Q/2 in the blend).  Q is
-// convex (a, c > 0, ac > b^2), so the minimum is 0 if the mean lies inside, else it lies on an edge:
-// each edge is a 1-D quadratic minimised by clamping its vertex.
-__device__ __forceinline__ float rect_qmin(float a, float b, float c, float dxl, float dxh, float dyl,
-                                           float dyh) {
-    if (dxl <= 0.f && dxh >= 0.f && dyl <= 0.f && dyh >= 0.f) return 0.f;
-    float q = 3.0e38f;
-    const float ia = 1.0f / a, ic = 1.0f / c;
-    const float xs[2] = {dxl, dxh}, ys[2] = {dyl, dyh};
-#pragma unroll
-    for (int k = 0; k < 2; k++) {
-        const float X = xs[k];
-        const float y = fminf(fmaxf(-b * X * ic, dyl), dyh);
-        q = fminf(q, a * X * X + 2.f * b * X * y + c * y * y);
-        const float Y = ys[k];
-        const float x = fminf(fmaxf(-b * Y * ia, dxl), dxh);
-        q = fminf(q, a * x * x + 2.f * b * x * Y + c * Y * Y);
-    }
-    return q;
-}
-
-// Strip mask of one (Gaussian, tile) instance: bit s is set unless no pixel centre of the tile's
-// s-th 16x4 strip can give alpha = min(0.99, o*exp(-Q/2)) >= 1/255, i.e. unless Q > 2 ln(255 o)
-// on the whole strip.  A cleared bit only ever removes pairs the blend skips anyway (alpha < 1/255,
-// forward.cu:362-363), so culling with it is decision-preserving; the slack (1e-4 of the form's
-// term magnitudes + 1e-3 relative) covers float rounding of both this test and the blend's power.
-// Non-finite or non-positive-definite conics keep every strip.
-__device__ __forceinline__ uint32_t strip_mask(float4 co, float2 m, int tx, int ty) {
-    const float a = co.x, b = co.y, c = co.z, o = co.w;
-    if (o < 1.0f / 255.0f) return 0u;  // alpha <= o < 1/255 at every pixel
-    if (!(a > 0.f) || !(c > 0.f) || !(a * c - b * b > 0.f) || !(o <= 3.0e38f)) return (1u << kStrips) - 1u;
-    const float K = 2.0f * logf(255.0f * o);
-    const float dxl = m.x - (float)(tx * GSR_BX + GSR_BX - 1), dxh = m.x - (float)(tx * GSR_BX);
-    const float mx = fmaxf(fabsf(dxl), fabsf(dxh));
-    uint32_t bits = 0;
-#pragma unroll
-    for (int s = 0; s < kStrips; s++) {
-        const float y0 = (float)(ty * GSR_BY + s * (GSR_BY / kStrips));
-        const float dyl = m.y - (y0 + (float)(GSR_BY / kStrips - 1)), dyh = m.y - y0;
-        const float my = fmaxf(fabsf(dyl), fabsf(dyh));
-        const float slack = 1e-4f * (a * mx * mx + 2.f * fabsf(b) * mx * my + c * my * my) + 1e-3f * K + 1e-3f;
-        const float q = rect_qmin(a, b, c, dxl, dxh, dyl, dyh);
-        if (!(q > K + slack)) bits |= 1u << s;
-    }
-    return bits;
-}
-
-// Key of an instance: depth bits << 32 | Gaussian index << 4 | strip mask.  Sorting the full key
-// orders a tile by (depth, index) as the reference's stable sort does (the index is unique in a
-// tile, so the mask bits never decide).
-__global__ __launch_bounds__(kScanBlock) void k_bin_scatter(Dims d, GeomArena g, ImageArena im,
-                                                            BinArena bn) {
-    if (g.ctrl[kCtrlOverflow]) return;
-    const int b = blockIdx.y;
-    const int i = blockIdx.x * kScanBlock + threadIdx.x;
-    if (i >= d.P) return;
-    const int64_t gid = (int64_t)b * d.P + i;
-    const uint32_t tiles = g.tiles[gid];
-    if (!tiles) return;
-    const uint2 rect = g.rect[gid];
-    const float4 co = g.conic[gid];
-    const float2 m = g.means2D[gid];
-    const uint64_t key_hi = (uint64_t)__float_as_uint(g.depth[gid]) << 32;
-    const uint2* rg = im.ranges + (int64_t)b * d.T;
-    const uint32_t x0 = rect.x & 0xFFFF, y0 = rect.x >> 16, x1 = rect.y & 0xFFFF, y1 = rect.y >> 16;
-    uint32_t k = g.offsets[gid] - tiles;
-    for (uint32_t y = y0; y < y1; y++)
-        for (uint32_t x = x0; x < x1; x++) {
-            const uint32_t t = y * (uint32_t)d.gx + x;
-            const uint32_t sm = strip_mask(co, m, (int)x, (int)y);
-            bn.keys[rg[t].x + bn.inst_slot[k]] = key_hi | ((uint32_t)i << 4) | sm;
-            k++;
-        }
-}
-
-void launch_bin_scatter(const Dims& d, const GeomArena& g, const ImageArena& im,
-                        const BinArena& b, hipStream_t s) {
-    if (d.P == 0 || d.B == 0) return;
-    hipLaunchKernelGGL(k_bin_scatter, dim3(d.nblk, d.B), dim3(kScanBlock), 0, s, d, g, im, b);
-}
-
-// ---------------------------------------------------------------- 5. per-tile sort
+// ---------------------------------------------------------------- segment sort (LDS)
 template <typename TV, int NT>
 __device__ __forceinline__ TV block_reduce_max(TV v, TV* sh) {
 #pragma unroll
@@ -328,15 +151,9 @@ __device__ void bitonic_sort(uint64_t* key, int n) {
 }
 
 // Sort one tile segment of n <= CAP keys in LDS; writes the Gaussian indices to out[0..n).
-// Sorted key -> point_list entry (Gaussian index) and strip mask.
-__device__ __forceinline__ void emit(uint64_t key, uint32_t* out, uint8_t* msk, int i) {
-    out[i] = ((uint32_t)key) >> 4;
-    msk[i] = (uint8_t)(key & 0xF);
-}
-
 template <int NT, int CAP>
-__device__ void sort_segment_lds(const uint64_t* __restrict__ gkeys, uint32_t* __restrict__ out,
-                                 uint8_t* __restrict__ msk, int n, char* smem) {
+__device__ void sort_segment_lds(const uint64_t* __restrict__ gkeys, uint32_t* __restrict__ out, int n,
+                                 char* smem) {
     constexpr int ITEMS = CAP / NT;
     constexpr uint32_t kDegenerate = 48;
     uint64_t* key = (uint64_t*)smem;                        // CAP
@@ -377,7 +194,7 @@ __device__ void sort_segment_lds(const uint64_t* __restrict__ gkeys, uint32_t* _
     const uint32_t maxb = block_reduce_max<uint32_t, NT>(mycnt_max, red);
     if (maxb > kDegenerate) {
         bitonic_sort<NT>(key, n);
-        for (int i = threadIdx.x; i < n; i += NT) emit(key[i], out, msk, i);
+        for (int i = threadIdx.x; i < n; i += NT) out[i] = (uint32_t)key[i];
         return;
     }
     // exclusive scan of bucket counts (chunked per thread), kept as bucket START
@@ -424,61 +241,398 @@ __device__ void sort_segment_lds(const uint64_t* __restrict__ gkeys, uint32_t* _
         if (i < n) cnt[rank[k]] = (uint32_t)key[i];
     }
     __syncthreads();
-    for (int i = threadIdx.x; i < n; i += NT) {
-        const uint32_t v = cnt[i];
-        out[i] = v >> 4;
-        msk[i] = (uint8_t)(v & 0xF);
+    for (int i = threadIdx.x; i < n; i += NT) out[i] = cnt[i];
+}
+
+// ---------------------------------------------------------------- 2. per-frame depth sort
+// Bucket of a depth key: linear in the key bits over the frame's [kmin, kmax]; monotone
+// non-decreasing in the key, so bucket order is key order and equal keys share a bucket.
+__device__ __forceinline__ uint32_t bucket_of(uint32_t key, uint32_t kmin, float scale, int NB) {
+    const uint32_t bk = (uint32_t)((float)(key - kmin) * scale);
+    return min(bk, (uint32_t)(NB - 1));
+}
+__device__ __forceinline__ float bucket_scale(uint32_t kmin, uint32_t kmax, int NB) {
+    return (float)NB / ((float)(kmax - kmin) + 1.0f);
+}
+
+__global__ __launch_bounds__(kScanBlock) void k_bucket_count(Dims d, GeomArena g) {
+    if (g.ctrl[kCtrlOverflow]) return;
+    const int b = blockIdx.y;
+    const int i = blockIdx.x * kScanBlock + threadIdx.x;
+    if (i >= d.P) return;
+    const int64_t gid = (int64_t)b * d.P + i;
+    if (!g.tiles[gid]) return;
+    const uint32_t kmin = ~g.fstat[kFsWords * b + kFsNotKeyMax], kmax = g.fstat[kFsWords * b + kFsKeyMax];
+    const uint32_t bk = bucket_of(__float_as_uint(g.depth[gid]), kmin, bucket_scale(kmin, kmax, d.NB), d.NB);
+    g.bslot[gid] = atomicAdd(&g.bstart[(int64_t)b * (d.NB + 1) + bk], 1u);
+}
+
+// One workgroup per frame: bucket counts -> bucket starts (entry NB = visible count); buckets
+// longer than kTinyBucket go to the segment-sort worklist.
+__global__ __launch_bounds__(1024) void k_bucket_scan(Dims d, GeomArena g) {
+    __shared__ uint32_t sh[1024 / 64 + 1];
+    if (g.ctrl[kCtrlOverflow]) return;
+    const int b = blockIdx.x;
+    uint32_t* bs = g.bstart + (int64_t)b * (d.NB + 1);
+    const int n = d.NB + 1;
+    const int per = (n + 1023) / 1024;
+    const int beg = threadIdx.x * per;
+    const int end = min(n, beg + per);
+    uint32_t s = 0;
+    for (int k = beg; k < end; k++) s += bs[k];
+    uint32_t total;
+    uint32_t ex = block_excl_scan<uint32_t, 1024>(s, &total, sh);
+    for (int k = beg; k < end; k++) {
+        const uint32_t c = bs[k];
+        bs[k] = ex;
+        if (c > (uint32_t)kTinyBucket) g.big[atomicAdd(&g.ctrl[kCtrlNumBig], 1u)] = (uint32_t)(b * d.NB + k);
+        ex += c;
     }
+    if (threadIdx.x == 0) g.fstat[kFsWords * b + kFsVisible] = total;
+}
+
+__global__ __launch_bounds__(kScanBlock) void k_bucket_scatter(Dims d, GeomArena g) {
+    if (g.ctrl[kCtrlOverflow]) return;
+    const int b = blockIdx.y;
+    const int i = blockIdx.x * kScanBlock + threadIdx.x;
+    if (i >= d.P) return;
+    const int64_t gid = (int64_t)b * d.P + i;
+    if (!g.tiles[gid]) return;
+    const uint32_t kmin = ~g.fstat[kFsWords * b + kFsNotKeyMax], kmax = g.fstat[kFsWords * b + kFsKeyMax];
+    const uint32_t key = __float_as_uint(g.depth[gid]);
+    const uint32_t bk = bucket_of(key, kmin, bucket_scale(kmin, kmax, d.NB), d.NB);
+    const uint32_t pos = g.bstart[(int64_t)b * (d.NB + 1) + bk] + g.bslot[gid];
+    g.skey[(int64_t)b * d.P + pos] = ((uint64_t)key << 32) | (uint32_t)i;
+}
+
+// Small buckets: each key's final position is its bucket start plus the number of smaller keys in
+// the bucket (keys are unique: the index is in the low word).
+__global__ __launch_bounds__(kScanBlock) void k_bucket_rank(Dims d, GeomArena g) {
+    if (g.ctrl[kCtrlOverflow]) return;
+    const int b = blockIdx.y;
+    const int j = blockIdx.x * kScanBlock + threadIdx.x;
+    if (j >= (int)g.fstat[kFsWords * b + kFsVisible]) return;
+    const uint32_t kmin = ~g.fstat[kFsWords * b + kFsNotKeyMax], kmax = g.fstat[kFsWords * b + kFsKeyMax];
+    const uint64_t* sk = g.skey + (int64_t)b * d.P;
+    const uint64_t key = sk[j];
+    const uint32_t bk = bucket_of((uint32_t)(key >> 32), kmin, bucket_scale(kmin, kmax, d.NB), d.NB);
+    const uint32_t* bs = g.bstart + (int64_t)b * (d.NB + 1);
+    const uint32_t s0 = bs[bk], e0 = bs[bk + 1];
+    if (e0 - s0 > (uint32_t)kTinyBucket) return;
+    uint32_t r = s0;
+    for (uint32_t m = s0; m < e0; m++) r += sk[m] < key ? 1u : 0u;
+    g.order[(int64_t)b * d.P + r] = (uint32_t)key;
 }
 
 constexpr size_t sort_lds_bytes(int NT, int CAP) { return (size_t)14 * CAP + 4 * (NT / 64 + 1) + 16; }
 
-__global__ __launch_bounds__(256) void k_tile_sort_small(ImageArena im, BinArena bn, const uint32_t* ctrl) {
+// Large buckets (worklist from k_bucket_scan): LDS sort, 256 threads up to kSortSmallCap keys,
+// 1024 threads up to kSortLargeCap, a bitonic network in global memory beyond.
+template <int NT, int CAP>
+__global__ __launch_bounds__(NT) void k_bucket_sort(Dims d, GeomArena g) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
-    if (ctrl[kCtrlOverflow]) return;
-    const uint2 r = im.ranges[blockIdx.x];
-    const int n = (int)(r.y - r.x);
-    if (n == 0 || n > kSortSmallCap) return;
-    if (n == 1) {
-        if (threadIdx.x == 0) emit(bn.keys[r.x], bn.point_list + r.x, bn.smask + r.x, 0);
-        return;
-    }
-    sort_segment_lds<256, kSortSmallCap>(bn.keys + r.x, bn.point_list + r.x, bn.smask + r.x, n, smem);
-}
-
-__global__ __launch_bounds__(1024) void k_tile_sort_large(ImageArena im, BinArena bn, const uint32_t* ctrl) {
-    extern __shared__ __attribute__((aligned(16))) char smem[];
-    if (ctrl[kCtrlOverflow]) return;
-    const uint32_t nl = ctrl[kCtrlNumLarge];
-    for (uint32_t w = blockIdx.x; w < nl; w += gridDim.x) {
-        const uint2 r = im.ranges[im.large_list[w]];
-        const int n = (int)(r.y - r.x);
-        if (n <= kSortLargeCap) {
-            sort_segment_lds<1024, kSortLargeCap>(bn.keys + r.x, bn.point_list + r.x, bn.smask + r.x, n, smem);
+    if (g.ctrl[kCtrlOverflow]) return;
+    const uint32_t nbig = g.ctrl[kCtrlNumBig];
+    for (uint32_t w = blockIdx.x; w < nbig; w += gridDim.x) {
+        const uint32_t fb = g.big[w];
+        const int b = (int)(fb / (uint32_t)d.NB), bk = (int)(fb % (uint32_t)d.NB);
+        const uint32_t* bs = g.bstart + (int64_t)b * (d.NB + 1);
+        const uint32_t s0 = bs[bk];
+        const int n = (int)(bs[bk + 1] - s0);
+        const bool mine = (CAP == kSortSmallCap) ? n <= kSortSmallCap : n > kSortSmallCap;
+        if (!mine) continue;
+        uint64_t* keys = g.skey + (int64_t)b * d.P + s0;
+        uint32_t* out = g.order + (int64_t)b * d.P + s0;
+        if (n <= CAP) {
+            sort_segment_lds<NT, CAP>(keys, out, n, smem);
         } else {
-            // pathological tile: bitonic network directly on the global segment
-            bitonic_sort<1024>(bn.keys + r.x, n);
-            for (int i = threadIdx.x; i < n; i += 1024) emit(bn.keys[r.x + i], bn.point_list + r.x, bn.smask + r.x, i);
+            bitonic_sort<NT>(keys, n);
+            for (int i = threadIdx.x; i < n; i += NT) out[i] = (uint32_t)keys[i];
         }
         __syncthreads();
     }
 }
 
-void launch_tile_sort(const Dims& d, const GeomArena& g, const ImageArena& im, const BinArena& b,
-                      hipStream_t s) {
-    const int ntiles = d.B * d.T;
-    if (ntiles == 0) return;
-    hipLaunchKernelGGL(k_tile_sort_small, dim3(ntiles), dim3(256), sort_lds_bytes(256, kSortSmallCap), s,
-                       im, b, (const uint32_t*)g.ctrl);
+void launch_depth_sort(const Dims& d, const GeomArena& g, hipStream_t s) {
+    if (d.P == 0 || d.B == 0) return;
+    hipLaunchKernelGGL(k_bucket_count, dim3(d.nblk, d.B), dim3(kScanBlock), 0, s, d, g);
+    hipLaunchKernelGGL(k_bucket_scan, dim3(d.B), dim3(1024), 0, s, d, g);
+    hipLaunchKernelGGL(k_bucket_scatter, dim3(d.nblk, d.B), dim3(kScanBlock), 0, s, d, g);
+    hipLaunchKernelGGL(k_bucket_rank, dim3(d.nblk, d.B), dim3(kScanBlock), 0, s, d, g);
     static bool attr = false;
     if (!attr) {
         attr = true;
-        hipFuncSetAttribute((const void*)k_tile_sort_large, hipFuncAttributeMaxDynamicSharedMemorySize,
-                            (int)sort_lds_bytes(1024, kSortLargeCap));
+        hipFuncSetAttribute((const void*)k_bucket_sort<1024, kSortLargeCap>,
+                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)sort_lds_bytes(1024, kSortLargeCap));
     }
-    const int grid = ntiles < 256 ? ntiles : 256;
-    hipLaunchKernelGGL(k_tile_sort_large, dim3(grid), dim3(1024), sort_lds_bytes(1024, kSortLargeCap), s,
-                       im, b, (const uint32_t*)g.ctrl);
+    hipLaunchKernelGGL((k_bucket_sort<256, kSortSmallCap>), dim3(persistent_grid(2)), dim3(256),
+                       sort_lds_bytes(256, kSortSmallCap), s, d, g);
+    hipLaunchKernelGGL((k_bucket_sort<1024, kSortLargeCap>), dim3(persistent_grid(1) / 4), dim3(1024),
+                       sort_lds_bytes(1024, kSortLargeCap), s, d, g);
+}
+
+// ---------------------------------------------------------------- 3. instance count table
+// Tile histogram of one chunk of kChunk depth-ordered Gaussians: each rect adds +1/-1 at its four
+// corners of a (gx+1) x (gy+1) difference array in LDS; a 2-D prefix sum gives the per-tile counts.
+__global__ __launch_bounds__(kScanBlock) void k_chunk_count(Dims d, GeomArena g) {
+    extern __shared__ int diff[];  // (gx+1)*(gy+1)
+    if (g.ctrl[kCtrlOverflow]) return;
+    const int b = blockIdx.y, c = blockIdx.x;
+    const uint32_t V = g.fstat[kFsWords * b + kFsVisible];
+    if ((uint32_t)c * kChunk >= V) return;
+    const int W1 = d.gx + 1, H1 = d.gy + 1;
+    for (int k = threadIdx.x; k < W1 * H1; k += kScanBlock) diff[k] = 0;
+    __syncthreads();
+    const uint32_t j = (uint32_t)c * kChunk + threadIdx.x;
+    if (j < V) {
+        const uint32_t gi = g.order[(int64_t)b * d.P + j];
+        const uint2 r = g.rect[(int64_t)b * d.P + gi];
+        const int x0 = r.x & 0xFFFF, y0 = r.x >> 16, x1 = r.y & 0xFFFF, y1 = r.y >> 16;
+        atomicAdd(&diff[y0 * W1 + x0], 1);
+        atomicAdd(&diff[y0 * W1 + x1], -1);
+        atomicAdd(&diff[y1 * W1 + x0], -1);
+        atomicAdd(&diff[y1 * W1 + x1], 1);
+    }
+    __syncthreads();
+    for (int y = threadIdx.x; y < d.gy; y += kScanBlock) {  // prefix along x
+        int acc = 0;
+        for (int x = 0; x < d.gx; x++) { acc += diff[y * W1 + x]; diff[y * W1 + x] = acc; }
+    }
+    __syncthreads();
+    uint32_t* row = g.table + ((int64_t)b * d.nchunk + c) * d.T;
+    for (int x = threadIdx.x; x < d.gx; x += kScanBlock) {  // prefix along y, write the row
+        int acc = 0;
+        for (int y = 0; y < d.gy; y++) { acc += diff[y * W1 + x]; row[y * d.gx + x] = (uint32_t)acc; }
+    }
+}
+
+// Per (frame, tile): exclusive scan of the counts down the frame's chunks, total -> tile_count.
+__global__ __launch_bounds__(kScanBlock) void k_column_scan(Dims d, GeomArena g, ImageArena im) {
+    const int b = blockIdx.y;
+    const int t = blockIdx.x * kScanBlock + threadIdx.x;
+    if (t >= d.T) return;
+    uint32_t acc = 0;
+    if (!g.ctrl[kCtrlOverflow]) {
+        const int nc = (int)((g.fstat[kFsWords * b + kFsVisible] + kChunk - 1) / kChunk);
+        uint32_t* col = g.table + (int64_t)b * d.nchunk * d.T + t;
+        int c = 0;
+        for (; c + 4 <= nc; c += 4) {
+            const uint32_t v0 = col[(int64_t)c * d.T], v1 = col[(int64_t)(c + 1) * d.T];
+            const uint32_t v2 = col[(int64_t)(c + 2) * d.T], v3 = col[(int64_t)(c + 3) * d.T];
+            col[(int64_t)c * d.T] = acc;
+            col[(int64_t)(c + 1) * d.T] = acc + v0;
+            col[(int64_t)(c + 2) * d.T] = acc + v0 + v1;
+            col[(int64_t)(c + 3) * d.T] = acc + v0 + v1 + v2;
+            acc += v0 + v1 + v2 + v3;
+        }
+        for (; c < nc; c++) {
+            const uint32_t v = col[(int64_t)c * d.T];
+            col[(int64_t)c * d.T] = acc;
+            acc += v;
+        }
+    }
+    im.tile_count[(int64_t)b * d.T + t] = acc;
+}
+
+void launch_chunk_count(const Dims& d, const GeomArena& g, const ImageArena& im, hipStream_t s) {
+    if (d.P == 0 || d.B == 0) return;
+    const size_t lds = (size_t)(d.gx + 1) * (d.gy + 1) * 4;
+    static size_t attr = 0;
+    if (lds > 65536 && attr < lds) {
+        attr = lds;
+        hipFuncSetAttribute((const void*)k_chunk_count, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    }
+    hipLaunchKernelGGL(k_chunk_count, dim3(d.nchunk, d.B), dim3(kScanBlock), lds, s, d, g);
+    hipLaunchKernelGGL(k_column_scan, dim3((d.T + kScanBlock - 1) / kScanBlock, d.B), dim3(kScanBlock), 0, s,
+                       d, g, im);
+}
+
+// ---------------------------------------------------------------- 4. tile ranges
+// Also emits the render worklist: every tile of the batch ordered by descending log2 list length
+// (counting sort over 34 buckets; empty tiles last), so persistent render workgroups take the
+// longest tiles first (LPT scheduling) and no XCD is left with only empty tiles.
+__global__ __launch_bounds__(1024) void k_tile_scan(int n, const uint32_t* __restrict__ cnt,
+                                                    uint2* __restrict__ ranges, uint32_t* ctrl,
+                                                    uint32_t* work_list) {
+    constexpr int kBuckets = 34;  // bucket 0: longest (2^32..), bucket 33: empty
+    __shared__ uint32_t sh[1024 / 64 + 1];
+    __shared__ uint32_t bcount[kBuckets];
+    const bool ovf = ctrl[kCtrlOverflow] != 0;
+    if (threadIdx.x < kBuckets) bcount[threadIdx.x] = 0;
+    const int per = (n + 1023) / 1024;
+    const int beg = threadIdx.x * per;
+    const int end = min(n, beg + per);
+    uint32_t s = 0;
+    if (!ovf)
+        for (int i = beg; i < end; i++) s += cnt[i];
+    uint32_t total;
+    uint32_t ex = block_excl_scan<uint32_t, 1024>(s, &total, sh);  // (barriers order bcount init)
+    for (int i = beg; i < end; i++) {
+        const uint32_t c = ovf ? 0u : cnt[i];
+        // empty tiles keep the reference's memset value (0,0) (rasterizer_impl.cu:313)
+        ranges[i] = c ? make_uint2(ex, ex + c) : make_uint2(0u, 0u);
+        const int bk = c ? __clz(c) : kBuckets - 1;
+        atomicAdd(&bcount[bk], 1u);
+        ex += c;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint32_t acc = 0;
+        for (int k = 0; k < kBuckets; k++) {
+            if (k == kBuckets - 1) ctrl[kCtrlNonEmpty] = acc;
+            const uint32_t v = bcount[k];
+            bcount[k] = acc;
+            acc += v;
+        }
+    }
+    __syncthreads();
+    for (int i = beg; i < end; i++) {
+        const uint32_t c = ovf ? 0u : cnt[i];
+        const int bk = c ? __clz(c) : kBuckets - 1;
+        work_list[atomicAdd(&bcount[bk], 1u)] = (uint32_t)i;
+    }
+}
+
+void launch_tile_scan(const Dims& d, const GeomArena& g, const ImageArena& im, hipStream_t s) {
+    hipLaunchKernelGGL(k_tile_scan, dim3(1), dim3(1024), 0, s, d.B * d.T, im.tile_count, im.ranges,
+                       g.ctrl, im.work_list);
+}
+
+// ---------------------------------------------------------------- strip masks
+// Minimum over the pixel-centre rectangle dx in [dxl, dxh], dy in [dyl, dyh] (dx = mean - pixel)
+// of the conic's quadratic form Q = a dx^2 + 2b dx dy + c dy^2 (power = -Q/2 in the blend).  Q is
+// convex (a, c > 0, ac > b^2), so the minimum is 0 if the mean lies inside, else it lies on an edge:
+// each edge is a 1-D quadratic minimised by clamping its vertex.
+__device__ __forceinline__ float rect_qmin(float a, float b, float c, float dxl, float dxh, float dyl,
+                                           float dyh) {
+    if (dxl <= 0.f && dxh >= 0.f && dyl <= 0.f && dyh >= 0.f) return 0.f;
+    float q = 3.0e38f;
+    const float ia = 1.0f / a, ic = 1.0f / c;
+    const float xs[2] = {dxl, dxh}, ys[2] = {dyl, dyh};
+#pragma unroll
+    for (int k = 0; k < 2; k++) {
+        const float X = xs[k];
+        const float y = fminf(fmaxf(-b * X * ic, dyl), dyh);
+        q = fminf(q, a * X * X + 2.f * b * X * y + c * y * y);
+        const float Y = ys[k];
+        const float x = fminf(fmaxf(-b * Y * ia, dxl), dxh);
+        q = fminf(q, a * x * x + 2.f * b * x * Y + c * Y * Y);
+    }
+    return q;
+}
+
+// Strip mask of one (Gaussian, tile) instance: bit s is set unless no pixel centre of the tile's
+// s-th 16x4 strip can give alpha = min(0.99, o*exp(-Q/2)) >= 1/255, i.e. unless Q > 2 ln(255 o)
+// on the whole strip.  A cleared bit only ever removes pairs the blend skips anyway (alpha < 1/255,
+// forward.cu:362-363), so culling with it is decision-preserving; the slack (1e-4 of the form's
+// term magnitudes + 1e-3 relative) covers float rounding of both this test and the blend's power.
+// Non-finite or non-positive-definite conics keep every strip.
+__device__ __forceinline__ uint32_t strip_mask(float4 co, float2 m, int tx, int ty) {
+    const float a = co.x, b = co.y, c = co.z, o = co.w;
+    if (o < 1.0f / 255.0f) return 0u;  // alpha <= o < 1/255 at every pixel
+    if (!(a > 0.f) || !(c > 0.f) || !(a * c - b * b > 0.f) || !(o <= 3.0e38f)) return (1u << kStrips) - 1u;
+    const float K = 2.0f * logf(255.0f * o);
+    const float dxl = m.x - (float)(tx * GSR_BX + GSR_BX - 1), dxh = m.x - (float)(tx * GSR_BX);
+    const float mx = fmaxf(fabsf(dxl), fabsf(dxh));
+    uint32_t bits = 0;
+#pragma unroll
+    for (int s = 0; s < kStrips; s++) {
+        const float y0 = (float)(ty * GSR_BY + s * (GSR_BY / kStrips));
+        const float dyl = m.y - (y0 + (float)(GSR_BY / kStrips - 1)), dyh = m.y - y0;
+        const float my = fmaxf(fabsf(dyl), fabsf(dyh));
+        const float slack = 1e-4f * (a * mx * mx + 2.f * fabsf(b) * mx * my + c * my * my) + 1e-3f * K + 1e-3f;
+        const float q = rect_qmin(a, b, c, dxl, dxh, dyl, dyh);
+        if (!(q > K + slack)) bits |= 1u << s;
+    }
+    return bits;
+}
+
+// ---------------------------------------------------------------- 5. ordered scatter
+// One workgroup per chunk of kChunk depth-ordered Gaussians (one per thread, "slot").  The chunk's
+// instances are spread evenly over the threads (binary search in the slots' inclusive tile-count
+// scan), so one huge splat does not serialise a wave.  An instance (slot o, tile t) lands at
+//     ranges[t].x + table[chunk][t] + #(slots o' < o whose rect covers t)
+// and the last term is a popcount of per-wave ballots of "rect covers tile column tx" and "... row
+// ty" (4 x 64-bit masks per column and per row, in LDS).
+__global__ __launch_bounds__(kChunk) void k_ordered_scatter(Dims d, GeomArena g, ImageArena im, BinArena bn) {
+    extern __shared__ uint64_t masks[];  // colm[gx][4], rowm[gy][4], then uint32 tile bases[T]
+    __shared__ uint32_t s_pref[kChunk];
+    __shared__ uint32_t s_sh[kChunk / 64 + 1];
+    __shared__ uint2 s_rect[kChunk];
+    __shared__ uint32_t s_gi[kChunk];
+    __shared__ float4 s_co[kChunk];
+    __shared__ float2 s_m[kChunk];
+    if (g.ctrl[kCtrlOverflow]) return;
+    const int b = blockIdx.y, c = blockIdx.x;
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const uint32_t V = g.fstat[kFsWords * b + kFsVisible];
+    if ((uint32_t)c * kChunk >= V) return;
+    uint64_t* colm = masks;
+    uint64_t* rowm = masks + 4 * d.gx;
+    uint32_t* base = (uint32_t*)(masks + 4 * (d.gx + d.gy));
+    // list position of this chunk's first instance in every tile of the frame
+    const uint32_t* tbl = g.table + ((int64_t)b * d.nchunk + c) * d.T;
+    const uint2* rg = im.ranges + (int64_t)b * d.T;
+    for (int t = tid; t < d.T; t += kChunk) base[t] = rg[t].x + tbl[t];
+    const uint32_t j = (uint32_t)c * kChunk + tid;
+    uint32_t gi = 0, nt = 0;
+    uint2 r = make_uint2(0u, 0u);
+    if (j < V) {
+        gi = g.order[(int64_t)b * d.P + j];
+        const int64_t gid = (int64_t)b * d.P + gi;
+        r = g.rect[gid];
+        nt = ((r.y & 0xFFFF) - (r.x & 0xFFFF)) * ((r.y >> 16) - (r.x >> 16));
+        s_co[tid] = g.conic[gid];
+        s_m[tid] = g.means2D[gid];
+    }
+    uint32_t total;
+    s_pref[tid] = block_excl_scan<uint32_t, kChunk>(nt, &total, s_sh) + nt;
+    s_rect[tid] = r;
+    s_gi[tid] = gi;
+    const int x0 = r.x & 0xFFFF, y0 = r.x >> 16, x1 = r.y & 0xFFFF, y1 = r.y >> 16;
+    for (int x = 0; x < d.gx; x++) {
+        const uint64_t m = __ballot(nt && x >= x0 && x < x1);
+        if (lane == 0) colm[4 * x + wv] = m;
+    }
+    for (int y = 0; y < d.gy; y++) {
+        const uint64_t m = __ballot(nt && y >= y0 && y < y1);
+        if (lane == 0) rowm[4 * y + wv] = m;
+    }
+    __syncthreads();
+    for (uint32_t q = tid; q < total; q += kChunk) {
+        int lo = 0, hi = kChunk - 1;  // first slot whose inclusive count exceeds q
+#pragma unroll
+        for (int step = 0; step < 8; step++) {
+            const int mid = (lo + hi) >> 1;
+            if (s_pref[mid] > q) hi = mid; else lo = mid + 1;
+        }
+        const int o = lo;
+        const uint32_t k = q - (o ? s_pref[o - 1] : 0u);
+        const uint2 ro = s_rect[o];
+        const int ox0 = ro.x & 0xFFFF, oy0 = ro.x >> 16, ow = (ro.y & 0xFFFF) - ox0;
+        // k / ow in float: exact, the quotient's fraction is >= 0.5/ow from an integer
+        const int dy = (int)(((float)k + 0.5f) * __builtin_amdgcn_rcpf((float)ow));
+        const int ty = oy0 + dy, tx = ox0 + (int)k - dy * ow;
+        const int t = ty * d.gx + tx;
+        const int w_o = o >> 6, l_o = o & 63;
+        uint32_t lr = 0;
+        for (int w = 0; w < w_o; w++) lr += (uint32_t)__popcll(colm[4 * tx + w] & rowm[4 * ty + w]);
+        const uint64_t below = l_o ? (~0ull >> (64 - l_o)) : 0ull;
+        lr += (uint32_t)__popcll(colm[4 * tx + w_o] & rowm[4 * ty + w_o] & below);
+        bn.point_list[base[t] + lr] = s_gi[o] | (strip_mask(s_co[o], s_m[o], tx, ty) << 28);
+    }
+}
+
+void launch_ordered_scatter(const Dims& d, const GeomArena& g, const ImageArena& im,
+                            const BinArena& b, hipStream_t s) {
+    if (d.P == 0 || d.B == 0) return;
+    const size_t lds = (size_t)(d.gx + d.gy) * 4 * 8 + (size_t)d.T * 4;
+    static size_t attr = 0;
+    if (lds > 65536 && attr < lds) {
+        attr = lds;
+        hipFuncSetAttribute((const void*)k_ordered_scatter, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    }
+    hipLaunchKernelGGL(k_ordered_scatter, dim3(d.nchunk, d.B), dim3(kChunk), lds, s, d, g, im, b);
 }
 
 }  // namespace gsr

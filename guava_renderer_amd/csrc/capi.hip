@@ -68,6 +68,7 @@ struct StageTimer {
 };
 
 inline size_t align_up(size_t x) { return (x + 255) & ~(size_t)255; }
+inline size_t ctrl_words(const Dims& d) { return (size_t)kCtrlWords + (size_t)kFsWords * d.B; }
 
 template <typename T>
 inline T* take(char* base, size_t& off, size_t count) {
@@ -96,7 +97,8 @@ size_t carve_geom(char* base, const Dims& d, GeomArena* g) {
     const size_t n = (size_t)d.B * d.P;
     size_t off = 0;
     GeomArena a;
-    a.ctrl = take<uint32_t>(base, off, kCtrlWords);
+    a.ctrl = take<uint32_t>(base, off, ctrl_words(d));
+    a.fstat = a.ctrl ? a.ctrl + kCtrlWords : nullptr;
     a.depth = take<float>(base, off, n);
     a.invdepth = take<float>(base, off, n);
     a.radii = take<int>(base, off, n);
@@ -106,8 +108,14 @@ size_t carve_geom(char* base, const Dims& d, GeomArena* g) {
     a.rect = take<uint2>(base, off, n);
     a.rrec = take<float4>(base, off, 2 * n);
     a.tiles = take<uint32_t>(base, off, n);
-    a.offsets = take<uint32_t>(base, off, n);
     a.blocksums = take<uint32_t>(base, off, (size_t)d.B * d.nblk + 1);
+    a.blockkey = take<uint32_t>(base, off, (size_t)d.B * d.nblk * 2);
+    a.bslot = take<uint32_t>(base, off, n);
+    a.bstart = take<uint32_t>(base, off, (size_t)d.B * (d.NB + 1));
+    a.skey = take<uint64_t>(base, off, n);
+    a.big = take<uint32_t>(base, off, (size_t)d.B * d.NB);
+    a.order = take<uint32_t>(base, off, n);
+    a.table = take<uint32_t>(base, off, (size_t)d.B * d.nchunk * d.T);
     if (g) *g = a;
     return align_up(off) + 256;
 }
@@ -121,7 +129,6 @@ size_t carve_image(char* base, const Dims& d, ImageArena* im) {
     a.n_contrib = take<uint32_t>(base, off, npx);
     a.ranges = take<uint2>(base, off, nt);
     a.tile_count = take<uint32_t>(base, off, nt);
-    a.large_list = take<uint32_t>(base, off, nt);
     a.work_list = take<uint32_t>(base, off, nt);
     if (im) *im = a;
     return align_up(off) + 256;
@@ -132,9 +139,6 @@ size_t carve_bin(char* base, int64_t R, BinArena* b) {
     size_t off = 0;
     BinArena a;
     a.point_list = take<uint32_t>(base, off, n);
-    a.keys = take<uint64_t>(base, off, n);
-    a.inst_slot = take<uint32_t>(base, off, n);
-    a.smask = take<uint8_t>(base, off, n);
     if (b) *b = a;
     return align_up(off) + 256;
 }
@@ -146,14 +150,14 @@ namespace {
 // Shared forward sequence once R is known and the binning arena exists.
 int run_binning_and_render(const Dims& d, const Inputs& in, const GeomArena& g, const ImageArena& im,
                            const BinArena& bn, const Outputs& o, int debug, hipStream_t s) {
-    { StageTimer st_(2, s); launch_bin_count(d, g, im, bn, s); }
-    STAGE(debug, s, "bin_count");
-    { StageTimer st_(3, s); launch_tile_scan(d, g, im, s); }
+    { StageTimer st_(2, s); launch_depth_sort(d, g, s); }
+    STAGE(debug, s, "depth_sort");
+    { StageTimer st_(3, s); launch_chunk_count(d, g, im, s); }
+    STAGE(debug, s, "chunk_count");
+    { StageTimer st_(4, s); launch_tile_scan(d, g, im, s); }
     STAGE(debug, s, "tile_scan");
-    { StageTimer st_(4, s); launch_bin_scatter(d, g, im, bn, s); }
-    STAGE(debug, s, "bin_scatter");
-    { StageTimer st_(5, s); launch_tile_sort(d, g, im, bn, s); }
-    STAGE(debug, s, "tile_sort");
+    { StageTimer st_(5, s); launch_ordered_scatter(d, g, im, bn, s); }
+    STAGE(debug, s, "ordered_scatter");
     { StageTimer st_(6, s); launch_render_fwd(d, in, g, im, bn, o, g_exact_exp != 0, s); }
     STAGE(debug, s, "render_fwd");
     return 0;
@@ -171,7 +175,9 @@ int gsr_set_exact_exp(int on) {
     return prev;
 }
 
-size_t gsr_geometry_bytes(int P) { return carve_geom(nullptr, make_dims(1, P, 16, 16), nullptr); }
+size_t gsr_geometry_bytes(int P, int width, int height) {
+    return carve_geom(nullptr, make_dims(1, P, width, height), nullptr);
+}
 size_t gsr_image_bytes(int width, int height) {
     return carve_image(nullptr, make_dims(1, 1, width, height), nullptr);
 }
@@ -198,7 +204,7 @@ int gsr_forward(gsr_alloc_fn geometryBuffer, gsr_alloc_fn binningBuffer, gsr_all
     hipStream_t s = (hipStream_t)stream;
     if (P < 0 || width <= 0 || height <= 0) return fail(GSR_ERR_ARG, "bad P/width/height");
     if (P >= kMaxGaussians) return fail(GSR_ERR_ARG, "P must be < 2^28");
-    if (width > 16 * 65535 || height > 16 * 65535) return fail(GSR_ERR_ARG, "image too large");
+    if ((int64_t)((width + 15) / 16) * ((height + 15) / 16) > kMaxTiles) return fail(GSR_ERR_ARG, "image too large");
     const Dims d = make_dims(1, P, width, height);
     GeomArena g;
     ImageArena im;
@@ -228,8 +234,8 @@ int gsr_forward(gsr_alloc_fn geometryBuffer, gsr_alloc_fn binningBuffer, gsr_all
     in.prefiltered = prefiltered; in.antialiasing = antialiasing;
     Outputs o{out_color, depth, radii, g_render_counters};
 
-    HIP_TRY(hipMemsetAsync(g.ctrl, 0, kCtrlWords * 4, s));
-    HIP_TRY(hipMemsetAsync(im.tile_count, 0, (size_t)d.T * 4, s));
+    HIP_TRY(hipMemsetAsync(g.ctrl, 0, ctrl_words(d) * 4, s));
+    HIP_TRY(hipMemsetAsync(g.bstart, 0, (size_t)d.B * (d.NB + 1) * 4, s));
     { StageTimer st_(0, s); launch_preprocess(d, in, g, o, s); }
     STAGE(debug, s, "preprocess");
     { StageTimer st_(1, s); launch_scan_blocksums(d, g, (int64_t)0xFFFFFFF0u, s); }
@@ -329,6 +335,7 @@ int gsr_forward_batch(int B, int P, int width, int height, const float* means3D,
     hipStream_t s = (hipStream_t)stream;
     if (B <= 0 || P <= 0 || width <= 0 || height <= 0 || !workspace || !tanfov)
         return fail(GSR_ERR_ARG, "bad batch arguments");
+    if ((int64_t)((width + 15) / 16) * ((height + 15) / 16) > kMaxTiles) return fail(GSR_ERR_ARG, "image too large");
     if (P >= kMaxGaussians) return fail(GSR_ERR_ARG, "P must be < 2^28");
     if (!colors) return fail(GSR_ERR_NO_COLORS, "For non-RGB, provide precomputed Gaussian colors!");
     if (((uintptr_t)colors & 15) != 0 || ((colors_stride * 4) & 15) != 0)
@@ -351,8 +358,8 @@ int gsr_forward_batch(int B, int P, int width, int height, const float* means3D,
     in.scale_mod = scale_modifier;
     in.prefiltered = 0; in.antialiasing = antialiasing;
     Outputs o{out_color, out_invdepth, radii, g_render_counters};
-    HIP_TRY(hipMemsetAsync(g.ctrl, 0, kCtrlWords * 4, s));
-    HIP_TRY(hipMemsetAsync(im.tile_count, 0, (size_t)d.B * d.T * 4, s));
+    HIP_TRY(hipMemsetAsync(g.ctrl, 0, ctrl_words(d) * 4, s));
+    HIP_TRY(hipMemsetAsync(g.bstart, 0, (size_t)d.B * (d.NB + 1) * 4, s));
     { StageTimer st_(0, s); launch_preprocess(d, in, g, o, s); }
     { StageTimer st_(1, s); launch_scan_blocksums(d, g, R_capacity, s); }
     int rc = run_binning_and_render(d, in, g, im, bn, o, 0, s);

@@ -14,19 +14,19 @@
 namespace gsr {
 
 constexpr int kScanBlock = 256;       // Gaussians per preprocess / binning workgroup
-constexpr int kSortSmallCap = 2048;   // instances per tile sorted by the 256-thread LDS sort
-constexpr int kSortLargeCap = 8192;   // instances per tile sorted by the 1024-thread LDS sort
-constexpr int kLdsTileHist = 8192;    // tiles per frame counted in LDS (more -> global atomics)
+constexpr int kSortSmallCap = 2048;   // keys per segment sorted by the 256-thread LDS sort
+constexpr int kSortLargeCap = 8192;   // keys per segment sorted by the 1024-thread LDS sort
+constexpr int kTinyBucket = 64;       // depth buckets up to this size are ranked in place
+constexpr int kChunk = 256;           // depth-ordered Gaussians per instance-count table row
 constexpr int kRenderBatch = 64;      // Gaussians staged in LDS per render_bwd round
 constexpr int kStrips = 4;            // 16x4 pixel strips per 16x16 tile (one render wave each)
-constexpr int kMaxGaussians = 1 << 28; // Gaussian index field of the binning key (bits 4..31)
 
 // control words (uint32) at the head of the geometry arena
 enum Ctrl : int {
     kCtrlRLo = 0,        // total instances of the batch
     kCtrlOverflow = 1,   // R > binning capacity
     kCtrlError = 2,      // bit0: prefiltered point culled
-    kCtrlNumLarge = 3,   // tiles whose list exceeds kSortSmallCap
+    kCtrlNumBig = 3,     // depth buckets longer than kTinyBucket (segment-sort worklist)
     kCtrlRenderHead = 4, // render worklist dequeue counter
     kCtrlBwdHead = 5,    // render-backward worklist dequeue counter
     kCtrlNonEmpty = 6,   // tiles of the batch with a non-empty list
@@ -34,9 +34,17 @@ enum Ctrl : int {
     kCtrlXcdStride = 1024,
     kCtrlWords = 9216
 };
+// per-frame words following the control words (zeroed with them)
+enum FrameStat : int {
+    kFsNotKeyMax = 0,  // max of ~depth_bits over the frame's visible Gaussians (= ~min key)
+    kFsKeyMax = 1,     // max of depth_bits
+    kFsVisible = 2,    // visible Gaussians (bucket-scan total)
+    kFsWords = 4
+};
 
 struct GeomArena {
-    uint32_t* ctrl;
+    uint32_t* ctrl;       // kCtrlWords control words, then kFsWords per frame
+    uint32_t* fstat;      // = ctrl + kCtrlWords
     float* depth;
     float* invdepth;
     int* radii;
@@ -47,8 +55,15 @@ struct GeomArena {
     float4* rrec;         // render record, 2 x float4 per Gaussian: (x, y, opacity, 1/depth),
                           // (-a/2, -b, -c/2, 0) of the conic (see render_fwd.hip)
     uint32_t* tiles;
-    uint32_t* offsets;    // inclusive scan of tiles over the batch
     uint32_t* blocksums;  // per scan block; scanned in place to exclusive block offsets
+    uint32_t* blockkey;   // per scan block: max depth key, max ~depth key of its visible Gaussians
+    // per-frame depth sort of the visible Gaussians (bucket sort on the depth float bits)
+    uint32_t* bslot;      // per Gaussian: arrival slot inside its depth bucket
+    uint32_t* bstart;     // per frame NB+1 bucket counts, scanned in place to bucket starts
+    uint64_t* skey;       // per frame, (depth bits << 32 | index) grouped by bucket
+    uint32_t* big;        // worklist of buckets longer than kTinyBucket: frame * NB + bucket
+    uint32_t* order;      // per frame, visible Gaussians in (depth, index) order
+    uint32_t* table;      // [B][nchunk][T] instance counts per (depth chunk, tile), scanned per tile
 };
 
 struct ImageArena {
@@ -56,20 +71,19 @@ struct ImageArena {
     uint32_t* n_contrib;
     uint2* ranges;        // per tile [start, end) into the batch's point_list
     uint32_t* tile_count;
-    uint32_t* large_list; // worklist of tiles with > kSortSmallCap instances
     uint32_t* work_list;  // every tile of the batch, longest list first (render scheduling)
 };
 
 struct BinArena {
-    uint32_t* point_list;  // per tile, depth-sorted Gaussian index (within its frame)
-    uint64_t* keys;        // unsorted (depth bits << 32 | index), grouped per tile
-    uint32_t* inst_slot;   // per (Gaussian, tile) instance: rank inside its tile's list
-    uint8_t* smask;        // per sorted instance: bit s set <=> the Gaussian can reach alpha >= 1/255
+    uint32_t* point_list;  // per tile, depth-sorted: Gaussian index (within its frame, bits 0..27) |
+                           // strip mask << 28, bit s set <=> the Gaussian can reach alpha >= 1/255
                            // somewhere in the tile's 16x4 pixel strip s (render_fwd's wave unit)
 };
 
 struct Dims {
     int B, P, W, H, gx, gy, T, nblk;  // nblk: scan blocks per frame
+    int NB;                           // depth buckets per frame (power of two)
+    int nchunk;                       // kChunk-Gaussian rows of the count table per frame
 };
 
 inline Dims make_dims(int B, int P, int W, int H) {
@@ -79,6 +93,10 @@ inline Dims make_dims(int B, int P, int W, int H) {
     d.gy = (H + GSR_BY - 1) / GSR_BY;
     d.T = d.gx * d.gy;
     d.nblk = (P + kScanBlock - 1) / kScanBlock;
+    int nb = 64;
+    while (nb < P / 8 && nb < (1 << 20)) nb <<= 1;
+    d.NB = nb;
+    d.nchunk = (P + kChunk - 1) / kChunk;
     return d;
 }
 
@@ -86,6 +104,11 @@ inline Dims make_dims(int B, int P, int W, int H) {
 size_t carve_geom(char* base, const Dims& d, GeomArena* g);
 size_t carve_image(char* base, const Dims& d, ImageArena* im);
 size_t carve_bin(char* base, int64_t R, BinArena* b);
+// Upper bound on P (the binning key keeps the Gaussian index in 32 bits with room to spare).
+constexpr int kMaxGaussians = 1 << 28;
+constexpr uint32_t kIndexMask = (1u << 28) - 1u;  // point_list entry -> Gaussian index
+// Upper bound on tiles per frame (the ordered scatter keeps a per-tile counter array in LDS).
+constexpr int kMaxTiles = 16384;
 
 struct Inputs {
     const float* means3D; int64_t s_means;     // element stride between frames (0 = shared)
@@ -131,13 +154,14 @@ int persistent_grid(int per_cu);
 void launch_preprocess(const Dims& d, const Inputs& in, const GeomArena& g, const Outputs& o,
                        hipStream_t s);
 void launch_scan_blocksums(const Dims& d, const GeomArena& g, int64_t R_cap, hipStream_t s);
-void launch_bin_count(const Dims& d, const GeomArena& g, const ImageArena& im, const BinArena& b,
-                      hipStream_t s);
+// per-frame depth sort of the visible Gaussians -> g.order
+void launch_depth_sort(const Dims& d, const GeomArena& g, hipStream_t s);
+// instance counts per (depth chunk, tile), scanned per tile -> g.table, im.tile_count
+void launch_chunk_count(const Dims& d, const GeomArena& g, const ImageArena& im, hipStream_t s);
 void launch_tile_scan(const Dims& d, const GeomArena& g, const ImageArena& im, hipStream_t s);
-void launch_bin_scatter(const Dims& d, const GeomArena& g, const ImageArena& im,
-                        const BinArena& b, hipStream_t s);
-void launch_tile_sort(const Dims& d, const GeomArena& g, const ImageArena& im, const BinArena& b,
-                      hipStream_t s);
+// depth-ordered instance emission -> point_list (index | strip mask << 28)
+void launch_ordered_scatter(const Dims& d, const GeomArena& g, const ImageArena& im,
+                            const BinArena& b, hipStream_t s);
 void launch_render_fwd(const Dims& d, const Inputs& in, const GeomArena& g, const ImageArena& im,
                        const BinArena& b, const Outputs& o, bool exact, hipStream_t s);
 void launch_render_bwd(const Dims& d, const Inputs& in, const GeomArena& g, const ImageArena& im,

@@ -125,18 +125,35 @@ __global__ __launch_bounds__(kScanBlock) void k_preprocess(Dims d, Inputs in, Ge
         g.rect[gid] = rect;
         if (o.radii) o.radii[gid] = radius;
     }
-    // block sum of tiles for the batch-wide scan
-    __shared__ uint32_t red[kScanBlock / 64];
+    // block sum of tiles for the batch-wide scan; depth-key range of the frame for the bucket sort
+    __shared__ uint32_t red[3][kScanBlock / 64];
     uint32_t v = tiles;
+    const uint32_t key = tiles ? __float_as_uint(g.depth[gid]) : 0u;  // depth > 0.2: monotone bits
+    uint32_t kmax = key, nkmax = tiles ? ~key : 0u;
 #pragma unroll
-    for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
-    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
+    for (int off = 32; off > 0; off >>= 1) {
+        v += __shfl_xor(v, off);
+        kmax = max(kmax, (uint32_t)__shfl_xor(kmax, off));
+        nkmax = max(nkmax, (uint32_t)__shfl_xor(nkmax, off));
+    }
+    if ((threadIdx.x & 63) == 0) {
+        red[0][threadIdx.x >> 6] = v;
+        red[1][threadIdx.x >> 6] = kmax;
+        red[2][threadIdx.x >> 6] = nkmax;
+    }
     __syncthreads();
     if (threadIdx.x == 0) {
-        uint32_t s = 0;
+        uint32_t s = 0, km = 0, nkm = 0;
 #pragma unroll
-        for (int w = 0; w < kScanBlock / 64; w++) s += red[w];
-        g.blocksums[(int64_t)b * d.nblk + blockIdx.x] = s;
+        for (int w = 0; w < kScanBlock / 64; w++) {
+            s += red[0][w];
+            km = max(km, red[1][w]);
+            nkm = max(nkm, red[2][w]);
+        }
+        const int64_t blk = (int64_t)b * d.nblk + blockIdx.x;
+        g.blocksums[blk] = s;
+        g.blockkey[2 * blk] = km;
+        g.blockkey[2 * blk + 1] = nkm;
     }
 }
 

@@ -107,7 +107,7 @@ __global__ __launch_bounds__(GSR_TILE_PIX) void k_render_bwd(Dims d, Inputs in, 
         const int cnt = min(kRenderBatch, (int)n - done_cnt);
         __syncthreads();
         if (lj < cnt) {
-            const uint32_t idx = bn.point_list[range.x + n - 1 - done_cnt - lj];
+            const uint32_t idx = bn.point_list[range.x + n - 1 - done_cnt - lj] & kIndexMask;
             const float4* fs = reinterpret_cast<const float4*>(colors + (int64_t)idx * GSR_C) + lq * 2;
             s_f[lj * 8 + lq * 2] = fs[0];
             s_f[lj * 8 + lq * 2 + 1] = fs[1];

@@ -24,6 +24,8 @@
 //
 // Roofline: per frame the kernel must read 156 B per visible Gaussian (features + 2D attributes)
 // and write 140 B per pixel (32 channels, inverse depth, final_T, n_contrib).
+#include <cstdlib>
+
 #include "gsr_internal.h"
 
 namespace gsr {
@@ -97,7 +99,7 @@ __device__ __forceinline__ void store_strip(const Dims& d, const ImageArena& im,
 // (items [0, 4*NE)), then each empty tile whole (items [4*NE, 3*NE + B*T)).  Eight queues, one per
 // XCD, take every eighth item (item = x + 8k); a wave dequeues from its own XCD's queue and, once
 // that is drained, from the others, so no counter sees more than a fraction of the traffic.
-template <bool EXACT, bool STATS>
+template <bool EXACT, bool STATS, int ABL>
 __global__ __launch_bounds__(GSR_TILE_PIX) void k_render_fwd(Dims d, Inputs in, GeomArena g,
                                                              ImageArena im, BinArena bn, Outputs o) {
     if (g.ctrl[kCtrlOverflow]) return;
@@ -144,7 +146,6 @@ __global__ __launch_bounds__(GSR_TILE_PIX) void k_render_fwd(Dims d, Inputs in, 
         const uint2 range = im.ranges[tile_g];
         const int n = (int)(range.y - range.x);
         const uint32_t* __restrict__ plist = bn.point_list + range.x;
-        const uint8_t* __restrict__ smask = bn.smask + range.x;
         const float4* __restrict__ rrec = g.rrec + (int64_t)b * d.P * 2;
         const float* __restrict__ colors = in.colors + in.s_colors * b;
 
@@ -163,7 +164,6 @@ __global__ __launch_bounds__(GSR_TILE_PIX) void k_render_fwd(Dims d, Inputs in, 
         uint64_t mask = 0;
         uint32_t cidx = 0;
         uint32_t nidx = lane < n ? plist[lane] : 0u;
-        uint32_t nmsk = lane < n ? (uint32_t)smask[lane] : 0u;
         // next survivor -> (g, pos); false at the end of the list
 #define GSR_NEXT(g_, pos_)                                                                          \
         ({                                                                                          \
@@ -172,19 +172,17 @@ __global__ __launch_bounds__(GSR_TILE_PIX) void k_render_fwd(Dims d, Inputs in, 
                 base += 64;                                                                         \
                 if (base >= n) { ok_ = false; break; }                                              \
                 cidx = nidx;                                                                        \
-                const uint32_t cm_ = nmsk;                                                          \
                 if (base + 64 < n) {                                                                \
                     const int j_ = base + 64 + lane;                                                \
                     nidx = j_ < n ? plist[j_] : 0u;                                                 \
-                    nmsk = j_ < n ? (uint32_t)smask[j_] : 0u;                                       \
                 }                                                                                   \
-                mask = __ballot(lane < n - base && ((cm_ >> strip) & 1u));                          \
+                mask = __ballot(lane < n - base && ((cidx >> (28 + strip)) & 1u));                 \
                 if (STATS) n_staged += min(64, n - base);                                           \
             }                                                                                       \
             if (ok_) {                                                                              \
                 const int i_ = (int)__builtin_ctzll(mask);                                          \
                 mask &= mask - 1;                                                                   \
-                g_ = __builtin_amdgcn_readlane(cidx, i_);                                           \
+                g_ = __builtin_amdgcn_readlane(cidx, i_) & kIndexMask;                              \
                 pos_ = base + i_ + 1;                                                               \
             }                                                                                       \
             ok_;                                                                                    \
@@ -201,7 +199,7 @@ __global__ __launch_bounds__(GSR_TILE_PIX) void k_render_fwd(Dims d, Inputs in, 
             S##pa = pa_; S##pb = pb_;                                                               \
             S##a0 = rrec[2 * ga_]; S##a1 = rrec[2 * ga_ + 1];                                       \
             S##b0 = rrec[2 * gb_]; S##b1 = rrec[2 * gb_ + 1];                                       \
-            S##f = colors[(int64_t)(hi ? gb_ : ga_) * GSR_C + ch];                                  \
+            S##f = (ABL & 2) ? 1.0f : colors[(int64_t)(hi ? gb_ : ga_) * GSR_C + ch];               \
         }
         // blend the k-step held in S and accumulate it on the matrix cores
 #define GSR_BLEND(S)                                                                                \
@@ -222,8 +220,13 @@ __global__ __launch_bounds__(GSR_TILE_PIX) void k_render_fwd(Dims d, Inputs in, 
             }                                                                                       \
             const auto sw_ = __builtin_amdgcn_permlane32_swap(__float_as_uint(wa_),                 \
                                                               __float_as_uint(wb_), false, false);  \
+            if (ABL & 1) {                                                                          \
+                acc0[0] = fmaf(f_, __uint_as_float(sw_[0]), acc0[0]);                               \
+                acc1[0] = fmaf(f_, __uint_as_float(sw_[1]), acc1[0]);                               \
+            } else {                                                                                \
             acc0 = __builtin_amdgcn_mfma_f32_32x32x2f32(f_, __uint_as_float(sw_[0]), acc0, 0, 0, 0); \
             acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(f_, __uint_as_float(sw_[1]), acc1, 0, 0, 0); \
+            }                                                                                       \
         }
         // two register sets, so step s+1's loads are in flight while step s is blended.  The loop
         // leaves only at its head and its foot (an invalid set blends as two null Gaussians), which
@@ -232,14 +235,23 @@ __global__ __launch_bounds__(GSR_TILE_PIX) void k_render_fwd(Dims d, Inputs in, 
         int Apa, Apb, Bpa, Bpb;
         float4 Aa0, Aa1, Ab0, Ab1, Ba0, Ba1, Bb0, Bb1;
         float Af, Bf;
-        GSR_FETCH(A)
-        GSR_FETCH(B)
-        while (Av) {
-            GSR_BLEND(A)
+        if (true) {
             GSR_FETCH(A)
-            GSR_BLEND(B)
             GSR_FETCH(B)
-            if (!__any(!done)) break;  // every pixel of the strip finished
+            while (Av) {
+                GSR_BLEND(A)
+                GSR_FETCH(A)
+                GSR_BLEND(B)
+                GSR_FETCH(B)
+                if (!__any(!done)) break;  // every pixel of the strip finished
+            }
+        } else {
+            for (;;) {
+                GSR_FETCH(A)
+                if (!Av) break;
+                GSR_BLEND(A)
+                if (!__any(!done)) break;
+            }
         }
 #undef GSR_NEXT
 #undef GSR_FETCH
@@ -267,18 +279,32 @@ __global__ __launch_bounds__(GSR_TILE_PIX) void k_render_fwd(Dims d, Inputs in, 
     }
 }
 
+template <bool EXACT>
+static void launch_variant(int v, dim3 gr, dim3 bl, hipStream_t s, const Dims& d, const Inputs& in,
+                           const GeomArena& g, const ImageArena& im, const BinArena& b, const Outputs& o) {
+    switch (v) {
+        case 1: hipLaunchKernelGGL((k_render_fwd<EXACT, false, 1>), gr, bl, 0, s, d, in, g, im, b, o); break;
+        case 2: hipLaunchKernelGGL((k_render_fwd<EXACT, false, 2>), gr, bl, 0, s, d, in, g, im, b, o); break;
+        case 3: hipLaunchKernelGGL((k_render_fwd<EXACT, false, 3>), gr, bl, 0, s, d, in, g, im, b, o); break;
+        default: hipLaunchKernelGGL((k_render_fwd<EXACT, false, 0>), gr, bl, 0, s, d, in, g, im, b, o); break;
+    }
+}
+
 void launch_render_fwd(const Dims& d, const Inputs& in, const GeomArena& g, const ImageArena& im,
                        const BinArena& b, const Outputs& o, bool exact, hipStream_t s) {
     const int nwaves = d.B * d.T * kStrips;  // upper bound of the work items
     if (nwaves == 0) return;
     const int grid = min((nwaves + 3) / 4, persistent_grid(8));
     const dim3 gr(grid), bl(GSR_TILE_PIX);
+    static int variant = -1;
+    if (variant < 0) { const char* e = getenv("GSR_RENDER_VARIANT"); variant = e ? atoi(e) : 0; }
     if (o.stats) {
-        if (exact) hipLaunchKernelGGL((k_render_fwd<true, true>), gr, bl, 0, s, d, in, g, im, b, o);
-        else hipLaunchKernelGGL((k_render_fwd<false, true>), gr, bl, 0, s, d, in, g, im, b, o);
+        if (exact) hipLaunchKernelGGL((k_render_fwd<true, true, 0>), gr, bl, 0, s, d, in, g, im, b, o);
+        else hipLaunchKernelGGL((k_render_fwd<false, true, 0>), gr, bl, 0, s, d, in, g, im, b, o);
+    } else if (exact) {
+        launch_variant<true>(variant, gr, bl, s, d, in, g, im, b, o);
     } else {
-        if (exact) hipLaunchKernelGGL((k_render_fwd<true, false>), gr, bl, 0, s, d, in, g, im, b, o);
-        else hipLaunchKernelGGL((k_render_fwd<false, false>), gr, bl, 0, s, d, in, g, im, b, o);
+        launch_variant<false>(variant, gr, bl, s, d, in, g, im, b, o);
     }
 }
 

@@ -55,8 +55,11 @@ const char* gsr_last_error(void);
  * 0 = hardware v_exp_f32.  Returns the previous setting. */
 int gsr_set_exact_exp(int on);
 
-/* Scratch sizes used by gsr_forward (the three resizer requests). */
-size_t gsr_geometry_bytes(int P);
+/* Scratch sizes used by gsr_forward (the three resizer requests).  Unlike the reference's
+ * GeometryState, the geometry arena also holds the per-frame depth sort and the (depth chunk x tile)
+ * instance-count table, so it depends on the image size too.  Images are limited to 16384 tiles
+ * (2048 x 2048 pixels). */
+size_t gsr_geometry_bytes(int P, int width, int height);
 size_t gsr_image_bytes(int width, int height);
 size_t gsr_binning_bytes(int64_t R);
 
@@ -119,8 +122,8 @@ int gsr_backward_batch(int B, int P, int width, int height, const float* means3D
                        float* dL_dmean3D, float* dL_dcov3D, float* dL_dscale, float* dL_drot,
                        int antialiasing, void* stream);
 /* Stage timing with HIP events recorded on the launch stream around each stage whose bit is set in
- * `stage_mask` (bit i = stage i: 0 preprocess, 1 block scan, 2 bin count, 3 tile scan,
- * 4 key scatter, 5 tile sort, 6 render fwd, 7 render bwd, 8 preprocess bwd); 0 disables.
+ * `stage_mask` (bit i = stage i: 0 preprocess, 1 block scan, 2 depth sort, 3 chunk count,
+ * 4 tile scan, 5 ordered scatter, 6 render fwd, 7 render bwd, 8 preprocess bwd); 0 disables.
  * gsr_profile_read synchronises the recorded events, writes the summed milliseconds and launch
  * counts of the first `n` stages and resets the accumulators. */
 #define GSR_NUM_STAGES 9

@@ -20,25 +20,35 @@ def _carve(spec):
     return out
 
 
-def geom_layout(P):
+def _nb(P):
+    nb = 64
+    while nb < P // 8 and nb < (1 << 20):
+        nb <<= 1
+    return nb
+
+
+def geom_layout(P, W, H):
     nblk = (P + 255) // 256
-    return _carve([("ctrl", np.uint32, 9216), ("depth", np.float32, P), ("invdepth", np.float32, P),
+    T = ((W + 15) // 16) * ((H + 15) // 16)
+    NB = _nb(P)
+    nchunk = (P + 255) // 256
+    return _carve([("ctrl", np.uint32, 9216 + 4), ("depth", np.float32, P), ("invdepth", np.float32, P),
                    ("radii", np.int32, P), ("means2D", np.float32, 2 * P), ("cov3D", np.float32, 6 * P),
-                   ("conic", np.float32, 4 * P), ("rect", np.uint32, 2 * P), ("rrec", np.float32, 8 * P), ("tiles", np.uint32, P),
-                   ("offsets", np.uint32, P), ("blocksums", np.uint32, nblk + 1)])
+                   ("conic", np.float32, 4 * P), ("rect", np.uint32, 2 * P), ("rrec", np.float32, 8 * P),
+                   ("tiles", np.uint32, P), ("blocksums", np.uint32, nblk + 1), ("blockkey", np.uint32, 2 * nblk), ("bslot", np.uint32, P),
+                   ("bstart", np.uint32, NB + 1), ("skey", np.uint64, P), ("big", np.uint32, NB),
+                   ("order", np.uint32, P), ("table", np.uint32, nchunk * T)])
 
 
 def image_layout(W, H):
     T = ((W + 15) // 16) * ((H + 15) // 16)
     return _carve([("final_T", np.float32, W * H), ("n_contrib", np.uint32, W * H),
-                   ("ranges", np.uint32, 2 * T), ("tile_count", np.uint32, T), ("large_list", np.uint32, T),
-                   ("work_list", np.uint32, T)])
+                   ("ranges", np.uint32, 2 * T), ("tile_count", np.uint32, T), ("work_list", np.uint32, T)])
 
 
 def bin_layout(R):
     n = max(R, 1)
-    return _carve([("point_list", np.uint32, n), ("keys", np.uint64, n), ("inst_slot", np.uint32, n),
-                   ("smask", np.uint8, n)])
+    return _carve([("point_list", np.uint32, n)])
 
 
 def decode(buf_np, layout):
@@ -105,8 +115,10 @@ def gpu_forward(d, antialiasing=False, use_cov=None, debug=False):
     P = d["means3D"].shape[0]
     W, H = d["image_width"], d["image_height"]
     st = {}
-    st.update(decode(gb.cpu().numpy(), geom_layout(P)))
+    st.update(decode(gb.cpu().numpy(), geom_layout(P, W, H)))
     st.update(decode(ib.cpu().numpy(), image_layout(W, H)))
     st.update(decode(bb.cpu().numpy(), bin_layout(R)))
+    st["smask"] = st["point_list"] >> 28           # entries: index | strip mask << 28
+    st["point_list"] = st["point_list"] & 0x0FFFFFFF
     st["R"] = R
     return color.cpu().numpy(), radii.cpu().numpy(), invd.cpu().numpy(), st

@@ -28,7 +28,8 @@ def test_library_exports_every_header_symbol():
 def test_scratch_sizes_grow_with_work():
     from guava_renderer_amd import _lib
     L = _lib.load()
-    assert L.gsr_geometry_bytes(1000) < L.gsr_geometry_bytes(100000)
+    assert L.gsr_geometry_bytes(1000, 64, 64) < L.gsr_geometry_bytes(100000, 64, 64)
+    assert L.gsr_geometry_bytes(1000, 64, 64) < L.gsr_geometry_bytes(1000, 512, 512)
     assert L.gsr_image_bytes(256, 256) < L.gsr_image_bytes(512, 512)
     assert L.gsr_binning_bytes(10) < L.gsr_binning_bytes(10 ** 6)
     assert L.gsr_batch_workspace_bytes(4, 1000, 64, 64, 10 ** 4) > L.gsr_batch_workspace_bytes(1, 1000, 64, 64, 10 ** 4)
