@@ -95,16 +95,25 @@ __device__ __forceinline__ void store_strip(const Dims& d, const ImageArena& im,
     }
 }
 
-// Work items, in k_tile_scan's longest-first order: the 4 strips of each non-empty tile
-// (items [0, 4*NE)), then each empty tile whole (items [4*NE, 3*NE + B*T)).  Eight queues, one per
-// XCD, take every eighth item (item = x + 8k); a wave dequeues from its own XCD's queue and, once
-// that is drained, from the others, so no counter sees more than a fraction of the traffic.
-template <bool EXACT, bool STATS, int ABL>
-__global__ __launch_bounds__(GSR_TILE_PIX) void k_render_fwd(Dims d, Inputs in, GeomArena g,
+// Work items, in k_tile_scan's longest-first order: the 4/NS strip groups (NS strips of 16x4 pixels,
+// one wave) of each non-empty tile (items [0, (4/NS)*NE)), then each empty tile whole.  Eight
+// queues, one per XCD, take every eighth item (item = x + 8k); a wave dequeues from its own XCD's
+// queue and, once that is drained, from the others, so no counter sees more than a fraction of the
+// traffic.
+//
+// NS = 2: each lane owns one pixel in each of the wave's two strips (rows r and r+4 of an 16x8
+// block): the two transmittance chains are independent, which doubles the instruction-level
+// parallelism of the blend, and the per-Gaussian stream, record and feature work is shared by 128
+// pixels.  A Gaussian is blended for both strips whenever it survives the cull of either (for the
+// other strip its alpha is < 1/255 at every pixel, so that blend takes nothing).
+template <bool EXACT, bool STATS, int NS>
+__global__ __launch_bounds__(GSR_TILE_PIX, NS == 2 ? 3 : 1) void k_render_fwd(Dims d, Inputs in, GeomArena g,
                                                              ImageArena im, BinArena bn, Outputs o) {
+    constexpr int kGroups = kStrips / NS;     // strip groups per tile
+    constexpr uint32_t kGroupShift = NS == 2 ? 1 : 2;
     if (g.ctrl[kCtrlOverflow]) return;
     const uint32_t ne = g.ctrl[kCtrlNonEmpty];
-    const uint32_t nstrip = 4u * ne;
+    const uint32_t nstrip = (uint32_t)kGroups * ne;
     const uint32_t nitems = nstrip + (uint32_t)(d.B * d.T) - ne;
     const int lane = threadIdx.x & 63;
     const int hi = lane >> 5;
@@ -134,32 +143,43 @@ __global__ __launch_bounds__(GSR_TILE_PIX) void k_render_fwd(Dims d, Inputs in, 
                                   lane, unused, unused, 1.0f, 0.f, 0u);
             continue;
         }
-        const int tile_g = (int)im.work_list[item >> 2];
-        const int strip = (int)(item & 3u);
+        const int tile_g = (int)im.work_list[item >> kGroupShift];
+        const int s0 = (int)(item & (uint32_t)(kGroups - 1)) * NS;  // first strip of the group
         const int b = tile_g / d.T;
         const int t = tile_g - b * d.T;
         const int tx = t % d.gx, ty = t / d.gx;
         const int px = tx * GSR_BX + (lane & 15);
-        const int py = ty * GSR_BY + strip * 4 + (lane >> 4);
-        const bool inside = px < d.W && py < d.H;
-        const float pfx = (float)px, pfy = (float)py;
+        const float pfx = (float)px;
+        float pfy[NS];
+        bool done[NS];
+        float T[NS], invd[NS];
+        uint32_t last[NS], stop[NS];
+#pragma unroll
+        for (int k = 0; k < NS; k++) {
+            const int py = ty * GSR_BY + (s0 + k) * 4 + (lane >> 4);
+            pfy[k] = (float)py;
+            done[k] = !(px < d.W && py < d.H);
+            T[k] = 1.0f;
+            invd[k] = 0.f;
+            last[k] = 0;
+            stop[k] = 0;
+        }
+        const uint32_t gmask = ((1u << NS) - 1u) << (28 + s0);  // this group's strip bits
         const uint2 range = im.ranges[tile_g];
         const int n = (int)(range.y - range.x);
         const uint32_t* __restrict__ plist = bn.point_list + range.x;
         const float4* __restrict__ rrec = g.rrec + (int64_t)b * d.P * 2;
         const float* __restrict__ colors = in.colors + in.s_colors * b;
 
-        floatx16 acc0, acc1;
+        floatx16 acc[NS][2];
 #pragma unroll
-        for (int r = 0; r < 16; r++) { acc0[r] = 0.f; acc1[r] = 0.f; }
-        float T = 1.0f, invd = 0.f;
-        uint32_t last = 0;
-        bool done = !inside;
+        for (int k = 0; k < NS; k++)
+#pragma unroll
+            for (int r = 0; r < 16; r++) { acc[k][0][r] = 0.f; acc[k][1][r] = 0.f; }
         uint64_t n_surv = 0, n_steps = 0, n_contrib_pairs = 0, n_staged = 0;
-        uint32_t stop = 0;
 
         // Survivor stream: wave-uniform state walking the list 64 entries at a time; the next
-        // chunk's indices and strip masks are always in flight.
+        // chunk's entries (index | strip mask << 28) are always in flight.
         int base = -64;
         uint64_t mask = 0;
         uint32_t cidx = 0;
@@ -176,7 +196,7 @@ __global__ __launch_bounds__(GSR_TILE_PIX) void k_render_fwd(Dims d, Inputs in, 
                     const int j_ = base + 64 + lane;                                                \
                     nidx = j_ < n ? plist[j_] : 0u;                                                 \
                 }                                                                                   \
-                mask = __ballot(lane < n - base && ((cidx >> (28 + strip)) & 1u));                 \
+                mask = __ballot(lane < n - base && (cidx & gmask) != 0u);                           \
                 if (STATS) n_staged += min(64, n - base);                                           \
             }                                                                                       \
             if (ok_) {                                                                              \
@@ -199,33 +219,35 @@ __global__ __launch_bounds__(GSR_TILE_PIX) void k_render_fwd(Dims d, Inputs in, 
             S##pa = pa_; S##pb = pb_;                                                               \
             S##a0 = rrec[2 * ga_]; S##a1 = rrec[2 * ga_ + 1];                                       \
             S##b0 = rrec[2 * gb_]; S##b1 = rrec[2 * gb_ + 1];                                       \
-            S##f = (ABL & 2) ? 1.0f : colors[(int64_t)(hi ? gb_ : ga_) * GSR_C + ch];               \
+            S##f = colors[(int64_t)(hi ? gb_ : ga_) * GSR_C + ch];                                  \
         }
-        // blend the k-step held in S and accumulate it on the matrix cores
+        // blend the k-step held in S for every strip of the group and accumulate on the matrix cores
 #define GSR_BLEND(S)                                                                                \
         {                                                                                           \
             const float4 a0_ = make_float4(S##a0.x, S##a0.y, S##v ? S##a0.z : 0.f, S##a0.w);        \
             const float4 b0_ = make_float4(S##b0.x, S##b0.y, S##hb ? S##b0.z : 0.f, S##b0.w);       \
             const float f_ = (S##v && (!hi || S##hb)) ? S##f : 0.f;                                 \
-            const bool was_done_ = done;                                                            \
-            const float wa_ = blend_one<EXACT>(a0_, S##a1, pfx, pfy, S##pa, T, invd, last, done);   \
-            const bool done_a_ = done;                                                              \
-            const float wb_ = blend_one<EXACT>(b0_, S##b1, pfx, pfy, S##pb, T, invd, last, done);   \
+            _Pragma("unroll")                                                                       \
+            for (int k = 0; k < NS; k++) {                                                          \
+                const bool was_done_ = done[k];                                                     \
+                const float wa_ = blend_one<EXACT>(a0_, S##a1, pfx, pfy[k], S##pa, T[k], invd[k],   \
+                                                   last[k], done[k]);                               \
+                const bool done_a_ = done[k];                                                       \
+                const float wb_ = blend_one<EXACT>(b0_, S##b1, pfx, pfy[k], S##pb, T[k], invd[k],   \
+                                                   last[k], done[k]);                               \
+                if (STATS) {                                                                        \
+                    if (!was_done_ && done_a_) stop[k] = (uint32_t)S##pa;                           \
+                    else if (!done_a_ && done[k]) stop[k] = (uint32_t)S##pb;                        \
+                    n_contrib_pairs += __popcll(__ballot(wa_ > 0.f)) + __popcll(__ballot(wb_ > 0.f)); \
+                }                                                                                   \
+                const auto sw_ = __builtin_amdgcn_permlane32_swap(__float_as_uint(wa_),             \
+                                                                  __float_as_uint(wb_), false, false); \
+                acc[k][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(f_, __uint_as_float(sw_[0]), acc[k][0], 0, 0, 0); \
+                acc[k][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(f_, __uint_as_float(sw_[1]), acc[k][1], 0, 0, 0); \
+            }                                                                                       \
             if (STATS) {                                                                            \
-                if (!was_done_ && done_a_) stop = (uint32_t)S##pa;                                  \
-                else if (!done_a_ && done) stop = (uint32_t)S##pb;                                  \
-                n_contrib_pairs += __popcll(__ballot(wa_ > 0.f)) + __popcll(__ballot(wb_ > 0.f));   \
                 n_steps += S##v ? 1 : 0;                                                            \
                 n_surv += S##v ? (S##hb ? 2 : 1) : 0;                                               \
-            }                                                                                       \
-            const auto sw_ = __builtin_amdgcn_permlane32_swap(__float_as_uint(wa_),                 \
-                                                              __float_as_uint(wb_), false, false);  \
-            if (ABL & 1) {                                                                          \
-                acc0[0] = fmaf(f_, __uint_as_float(sw_[0]), acc0[0]);                               \
-                acc1[0] = fmaf(f_, __uint_as_float(sw_[1]), acc1[0]);                               \
-            } else {                                                                                \
-            acc0 = __builtin_amdgcn_mfma_f32_32x32x2f32(f_, __uint_as_float(sw_[0]), acc0, 0, 0, 0); \
-            acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(f_, __uint_as_float(sw_[1]), acc1, 0, 0, 0); \
             }                                                                                       \
         }
         // two register sets, so step s+1's loads are in flight while step s is blended.  The loop
@@ -235,23 +257,16 @@ __global__ __launch_bounds__(GSR_TILE_PIX) void k_render_fwd(Dims d, Inputs in, 
         int Apa, Apb, Bpa, Bpb;
         float4 Aa0, Aa1, Ab0, Ab1, Ba0, Ba1, Bb0, Bb1;
         float Af, Bf;
-        if (true) {
+        GSR_FETCH(A)
+        GSR_FETCH(B)
+        while (Av) {
+            GSR_BLEND(A)
             GSR_FETCH(A)
+            GSR_BLEND(B)
             GSR_FETCH(B)
-            while (Av) {
-                GSR_BLEND(A)
-                GSR_FETCH(A)
-                GSR_BLEND(B)
-                GSR_FETCH(B)
-                if (!__any(!done)) break;  // every pixel of the strip finished
-            }
-        } else {
-            for (;;) {
-                GSR_FETCH(A)
-                if (!Av) break;
-                GSR_BLEND(A)
-                if (!__any(!done)) break;
-            }
+            // every pixel of the group finished (written without a loop: a bool reduction loop here
+            // costs the register allocator ~40 VGPRs)
+            if (!__any(!done[0] || !done[NS - 1])) break;
         }
 #undef GSR_NEXT
 #undef GSR_FETCH
@@ -260,7 +275,12 @@ __global__ __launch_bounds__(GSR_TILE_PIX) void k_render_fwd(Dims d, Inputs in, 
         // ---- epilogue ----
         if (STATS) {
             unsigned long long* cn = (unsigned long long*)o.stats;
-            uint64_t ev = inside ? (done ? stop : (uint32_t)n) : 0;
+            uint64_t ev = 0;
+#pragma unroll
+            for (int k = 0; k < NS; k++) {
+                const int py = ty * GSR_BY + (s0 + k) * 4 + (lane >> 4);
+                if (px < d.W && py < d.H) ev += done[k] ? stop[k] : (uint32_t)n;
+            }
             for (int off = 32; off > 0; off >>= 1) ev += __shfl_xor(ev, off);
             if (lane == 0) {
                 atomicAdd(&cn[0], (unsigned long long)ev);
@@ -268,25 +288,16 @@ __global__ __launch_bounds__(GSR_TILE_PIX) void k_render_fwd(Dims d, Inputs in, 
                 atomicAdd(&cn[2], (unsigned long long)n_surv);
                 atomicAdd(&cn[3], (unsigned long long)n_steps);
                 atomicAdd(&cn[4], (unsigned long long)n_staged);
-                if (strip == 0) {
+                if (s0 == 0) {
                     atomicAdd(&cn[5], (unsigned long long)n);
                     atomicAdd(&cn[6], 1ull);
                 }
             }
         }
-        store_strip<false>(d, im, o, in.bg + in.s_bg * b, b, tx, ty * GSR_BY + strip * 4, lane, acc0, acc1, T,
-                           invd, last);
-    }
-}
-
-template <bool EXACT>
-static void launch_variant(int v, dim3 gr, dim3 bl, hipStream_t s, const Dims& d, const Inputs& in,
-                           const GeomArena& g, const ImageArena& im, const BinArena& b, const Outputs& o) {
-    switch (v) {
-        case 1: hipLaunchKernelGGL((k_render_fwd<EXACT, false, 1>), gr, bl, 0, s, d, in, g, im, b, o); break;
-        case 2: hipLaunchKernelGGL((k_render_fwd<EXACT, false, 2>), gr, bl, 0, s, d, in, g, im, b, o); break;
-        case 3: hipLaunchKernelGGL((k_render_fwd<EXACT, false, 3>), gr, bl, 0, s, d, in, g, im, b, o); break;
-        default: hipLaunchKernelGGL((k_render_fwd<EXACT, false, 0>), gr, bl, 0, s, d, in, g, im, b, o); break;
+#pragma unroll
+        for (int k = 0; k < NS; k++)
+            store_strip<false>(d, im, o, in.bg + in.s_bg * b, b, tx, ty * GSR_BY + (s0 + k) * 4, lane, acc[k][0],
+                               acc[k][1], T[k], invd[k], last[k]);
     }
 }
 
@@ -296,16 +307,17 @@ void launch_render_fwd(const Dims& d, const Inputs& in, const GeomArena& g, cons
     if (nwaves == 0) return;
     const int grid = min((nwaves + 3) / 4, persistent_grid(8));
     const dim3 gr(grid), bl(GSR_TILE_PIX);
-    static int variant = -1;
-    if (variant < 0) { const char* e = getenv("GSR_RENDER_VARIANT"); variant = e ? atoi(e) : 0; }
-    if (o.stats) {
-        if (exact) hipLaunchKernelGGL((k_render_fwd<true, true, 0>), gr, bl, 0, s, d, in, g, im, b, o);
-        else hipLaunchKernelGGL((k_render_fwd<false, true, 0>), gr, bl, 0, s, d, in, g, im, b, o);
-    } else if (exact) {
-        launch_variant<true>(variant, gr, bl, s, d, in, g, im, b, o);
+    static int ns = -1;
+    if (ns < 0) { const char* e = getenv("GSR_RENDER_NS"); ns = e ? atoi(e) : 1; }
+#define GSR_LAUNCH(E, S, N) hipLaunchKernelGGL((k_render_fwd<E, S, N>), gr, bl, 0, s, d, in, g, im, b, o)
+    if (ns == 1) {
+        if (o.stats) { if (exact) GSR_LAUNCH(true, true, 1); else GSR_LAUNCH(false, true, 1); }
+        else { if (exact) GSR_LAUNCH(true, false, 1); else GSR_LAUNCH(false, false, 1); }
     } else {
-        launch_variant<false>(variant, gr, bl, s, d, in, g, im, b, o);
+        if (o.stats) { if (exact) GSR_LAUNCH(true, true, 2); else GSR_LAUNCH(false, true, 2); }
+        else { if (exact) GSR_LAUNCH(true, false, 2); else GSR_LAUNCH(false, false, 2); }
     }
+#undef GSR_LAUNCH
 }
 
 }  // namespace gsr
