@@ -13,7 +13,7 @@ EXPORTS = ("gsr_version", "gsr_last_error", "gsr_set_exact_exp", "gsr_geometry_b
            "gsr_image_bytes", "gsr_binning_bytes", "gsr_mark_visible", "gsr_forward",
            "gsr_backward", "gsr_batch_workspace_bytes", "gsr_forward_batch",
            "gsr_backward_batch", "gsr_batch_status", "gsr_profile_enable", "gsr_profile_read",
-           "gsr_render_counters")
+           "gsr_render_counters", "gsr_render_timeline")
 
 ALLOC_FN = ctypes.CFUNCTYPE(ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t)
 
@@ -85,6 +85,8 @@ def load(path=None):
     L.gsr_profile_read.restype = _i
     L.gsr_render_counters.argtypes = [_vp]
     L.gsr_render_counters.restype = _i
+    L.gsr_render_timeline.argtypes = [_vp, ctypes.c_uint32]
+    L.gsr_render_timeline.restype = _i
     _lib = L
     return L
 

@@ -18,6 +18,8 @@ namespace {
 thread_local std::string g_err;
 int g_exact_exp = 1;
 uint64_t* g_render_counters = nullptr;  // gsr_render_counters
+uint32_t* g_timeline = nullptr;         // gsr_render_timeline
+uint32_t g_timeline_cap = 0;
 
 int fail(gsr_status st, const std::string& msg) {
     g_err = msg;
@@ -232,7 +234,7 @@ int gsr_forward(gsr_alloc_fn geometryBuffer, gsr_alloc_fn binningBuffer, gsr_all
     in.bg = background; in.s_bg = 0;
     in.scale_mod = scale_modifier;
     in.prefiltered = prefiltered; in.antialiasing = antialiasing;
-    Outputs o{out_color, depth, radii, g_render_counters};
+    Outputs o{out_color, depth, radii, g_render_counters, g_timeline, g_timeline_cap};
 
     HIP_TRY(hipMemsetAsync(g.ctrl, 0, ctrl_words(d) * 4, s));
     HIP_TRY(hipMemsetAsync(g.bstart, 0, (size_t)d.B * (d.NB + 1) * 4, s));
@@ -357,7 +359,8 @@ int gsr_forward_batch(int B, int P, int width, int height, const float* means3D,
     in.bg = backgrounds; in.s_bg = bg_stride;
     in.scale_mod = scale_modifier;
     in.prefiltered = 0; in.antialiasing = antialiasing;
-    Outputs o{out_color, out_invdepth, radii, g_render_counters};
+    { const char* e = getenv("GSR_PRIO_ITEMS"); in.prio_items = e ? (uint32_t)atoi(e) : 0u; }
+    Outputs o{out_color, out_invdepth, radii, g_render_counters, g_timeline, g_timeline_cap};
     HIP_TRY(hipMemsetAsync(g.ctrl, 0, ctrl_words(d) * 4, s));
     HIP_TRY(hipMemsetAsync(g.bstart, 0, (size_t)d.B * (d.NB + 1) * 4, s));
     { StageTimer st_(0, s); launch_preprocess(d, in, g, o, s); }
@@ -417,6 +420,12 @@ int gsr_backward_batch(int B, int P, int width, int height, const float* means3D
 
 int gsr_render_counters(uint64_t* device_counters) {
     g_render_counters = device_counters;
+    return 0;
+}
+
+int gsr_render_timeline(uint32_t* device_records, uint32_t capacity) {
+    g_timeline = device_records;
+    g_timeline_cap = device_records ? capacity : 0u;
     return 0;
 }
 

@@ -124,6 +124,7 @@ struct Inputs {
     const float* bg; int64_t s_bg;
     float scale_mod;
     int prefiltered, antialiasing;
+    uint32_t prio_items;  // render_fwd: work items (longest first) that run at raised issue priority
 };
 
 struct Outputs {
@@ -131,6 +132,8 @@ struct Outputs {
     float* out_invdepth;  // [B][H][W] or null
     int* radii;           // [B][P] or null
     uint64_t* stats;      // gsr_render_counters words, or null (production kernel)
+    uint32_t* timeline;   // gsr_render_timeline records (instrumented kernel only), or null
+    uint32_t timeline_cap;
 };
 
 struct Grads {

@@ -24,31 +24,36 @@
 //
 // Roofline: per frame the kernel must read 156 B per visible Gaussian (features + 2D attributes)
 // and write 140 B per pixel (32 channels, inverse depth, final_T, n_contrib).
-#include <cstdlib>
-
 #include "gsr_internal.h"
 
 namespace gsr {
 
 typedef float floatx16 __attribute__((ext_vector_type(16)));
 
-// One (pixel, Gaussian) step of the front-to-back blend (forward.cu:349-381), branch-free.
-// Returns the blend weight alpha*T (0 when the pixel does not take this Gaussian) and updates the
-// pixel's transmittance, inverse depth, last contributor (1-based list position) and done flag.
+// The blend step of forward.cu:349-381 split in two (both halves are branch-free):
+//  * alpha_of: the pixel-local alpha of one Gaussian, independent of the pixel's transmittance, with
+//    the `power > 0` skip folded in as alpha = 0 (0 < 1/255 is never taken; a NaN power still gives
+//    alpha = min(0.99, NaN) = 0.99 as in the reference) -- computed one step ahead;
+//  * take_step: the serial part on the pixel's state (the 1/255 skip, the T < 1e-4 stop, the
+//    weight alpha*T, inverse depth, last contributor = 1-based list position, done flag).
 template <bool EXACT>
-__device__ __forceinline__ float blend_one(const float4 ga, const float4 gc, float pfx, float pfy,
-                                           int pos, float& T, float& invd, uint32_t& last, bool& done) {
+__device__ __forceinline__ float alpha_of(const float4 ga, const float4 gc, float pfx, float pfy) {
     const float dx = ga.x - pfx, dy = ga.y - pfy;
     const float power = blend_power(gc.x, gc.y, gc.z, dx, dy);
     const float alpha = fminf(0.99f, ga.z * blend_exp<EXACT>(power));
-    const bool take = !done && !(power > 0.0f) && !(alpha < 1.0f / 255.0f);
+    return (power > 0.0f) ? 0.0f : alpha;
+}
+
+__device__ __forceinline__ float take_step(float alpha, float inv_depth, uint32_t pos, float& T, float& invd,
+                                           uint32_t& last, bool& done) {
+    const bool take = !done && !(alpha < 1.0f / 255.0f);
     const float test_T = T * (1.0f - alpha);
     const bool term = take && (test_T < 0.0001f);
     const bool contrib = take && !term;
     const float w = contrib ? alpha * T : 0.0f;
-    invd = fmaf(ga.w, w, invd);
+    invd = fmaf(inv_depth, w, invd);
     T = contrib ? test_T : T;
-    last = contrib ? (uint32_t)pos : last;
+    last = contrib ? pos : last;
     done = done || term;
     return w;
 }
@@ -95,25 +100,21 @@ __device__ __forceinline__ void store_strip(const Dims& d, const ImageArena& im,
     }
 }
 
-// Work items, in k_tile_scan's longest-first order: the 4/NS strip groups (NS strips of 16x4 pixels,
-// one wave) of each non-empty tile (items [0, (4/NS)*NE)), then each empty tile whole.  Eight
-// queues, one per XCD, take every eighth item (item = x + 8k); a wave dequeues from its own XCD's
-// queue and, once that is drained, from the others, so no counter sees more than a fraction of the
-// traffic.
+// Work items, in k_tile_scan's longest-first order: the 4 strips of each non-empty tile
+// (items [0, 4*NE)), then each empty tile whole (items [4*NE, 3*NE + B*T)).  Eight queues, one per
+// XCD, take every eighth item (item = x + 8k); a wave dequeues from its own XCD's queue and, once
+// that is drained, from the others, so no counter sees more than a fraction of the traffic.
 //
-// NS = 2: each lane owns one pixel in each of the wave's two strips (rows r and r+4 of an 16x8
-// block): the two transmittance chains are independent, which doubles the instruction-level
-// parallelism of the blend, and the per-Gaussian stream, record and feature work is shared by 128
-// pixels.  A Gaussian is blended for both strips whenever it survives the cull of either (for the
-// other strip its alpha is < 1/255 at every pixel, so that blend takes nothing).
-template <bool EXACT, bool STATS, int NS>
-__global__ __launch_bounds__(GSR_TILE_PIX, NS == 2 ? 3 : 1) void k_render_fwd(Dims d, Inputs in, GeomArena g,
+// The survivor stream runs as a three-stage software pipeline over k-steps (two Gaussians each) held
+// in three rotating register slots: the records and feature operand of step s+3 are loaded while
+// step s+1's alphas (the exp-heavy, transmittance-independent part) are computed and step s's
+// serial blend and MFMA accumulation run.
+template <bool EXACT, bool STATS, bool TL>
+__global__ __launch_bounds__(GSR_TILE_PIX) void k_render_fwd(Dims d, Inputs in, GeomArena g,
                                                              ImageArena im, BinArena bn, Outputs o) {
-    constexpr int kGroups = kStrips / NS;     // strip groups per tile
-    constexpr uint32_t kGroupShift = NS == 2 ? 1 : 2;
     if (g.ctrl[kCtrlOverflow]) return;
     const uint32_t ne = g.ctrl[kCtrlNonEmpty];
-    const uint32_t nstrip = (uint32_t)kGroups * ne;
+    const uint32_t nstrip = (uint32_t)kStrips * ne;
     const uint32_t nitems = nstrip + (uint32_t)(d.B * d.T) - ne;
     const int lane = threadIdx.x & 63;
     const int hi = lane >> 5;
@@ -143,39 +144,31 @@ __global__ __launch_bounds__(GSR_TILE_PIX, NS == 2 ? 3 : 1) void k_render_fwd(Di
                                   lane, unused, unused, 1.0f, 0.f, 0u);
             continue;
         }
-        const int tile_g = (int)im.work_list[item >> kGroupShift];
-        const int s0 = (int)(item & (uint32_t)(kGroups - 1)) * NS;  // first strip of the group
+        // the longest strips bound the kernel's latency: give them issue priority on their SIMD
+        if (item < in.prio_items) __builtin_amdgcn_s_setprio(3);
+        else __builtin_amdgcn_s_setprio(0);
+        const uint64_t t_start = TL ? __builtin_amdgcn_s_memrealtime() : 0;
+        const int tile_g = (int)im.work_list[item >> 2];
+        const int strip = (int)(item & 3u);
         const int b = tile_g / d.T;
         const int t = tile_g - b * d.T;
         const int tx = t % d.gx, ty = t / d.gx;
         const int px = tx * GSR_BX + (lane & 15);
-        const float pfx = (float)px;
-        float pfy[NS];
-        bool done[NS];
-        float T[NS], invd[NS];
-        uint32_t last[NS], stop[NS];
-#pragma unroll
-        for (int k = 0; k < NS; k++) {
-            const int py = ty * GSR_BY + (s0 + k) * 4 + (lane >> 4);
-            pfy[k] = (float)py;
-            done[k] = !(px < d.W && py < d.H);
-            T[k] = 1.0f;
-            invd[k] = 0.f;
-            last[k] = 0;
-            stop[k] = 0;
-        }
-        const uint32_t gmask = ((1u << NS) - 1u) << (28 + s0);  // this group's strip bits
+        const int py = ty * GSR_BY + strip * 4 + (lane >> 4);
+        const float pfx = (float)px, pfy = (float)py;
+        bool done = !(px < d.W && py < d.H);
+        float T = 1.0f, invd = 0.f;
+        uint32_t last = 0, stop = 0;
+        const uint32_t smask_bit = 1u << (28 + strip);
         const uint2 range = im.ranges[tile_g];
         const int n = (int)(range.y - range.x);
         const uint32_t* __restrict__ plist = bn.point_list + range.x;
         const float4* __restrict__ rrec = g.rrec + (int64_t)b * d.P * 2;
         const float* __restrict__ colors = in.colors + in.s_colors * b;
 
-        floatx16 acc[NS][2];
+        floatx16 acc0, acc1;
 #pragma unroll
-        for (int k = 0; k < NS; k++)
-#pragma unroll
-            for (int r = 0; r < 16; r++) { acc[k][0][r] = 0.f; acc[k][1][r] = 0.f; }
+        for (int r = 0; r < 16; r++) { acc0[r] = 0.f; acc1[r] = 0.f; }
         uint64_t n_surv = 0, n_steps = 0, n_contrib_pairs = 0, n_staged = 0;
 
         // Survivor stream: wave-uniform state walking the list 64 entries at a time; the next
@@ -196,7 +189,7 @@ __global__ __launch_bounds__(GSR_TILE_PIX, NS == 2 ? 3 : 1) void k_render_fwd(Di
                     const int j_ = base + 64 + lane;                                                \
                     nidx = j_ < n ? plist[j_] : 0u;                                                 \
                 }                                                                                   \
-                mask = __ballot(lane < n - base && (cidx & gmask) != 0u);                           \
+                mask = __ballot(lane < n - base && (cidx & smask_bit) != 0u);                       \
                 if (STATS) n_staged += min(64, n - base);                                           \
             }                                                                                       \
             if (ok_) {                                                                              \
@@ -207,7 +200,7 @@ __global__ __launch_bounds__(GSR_TILE_PIX, NS == 2 ? 3 : 1) void k_render_fwd(Di
             }                                                                                       \
             ok_;                                                                                    \
         })
-        // fetch the next k-step (two survivors) into register set S: render records (uniform
+        // stage 1: fetch the next k-step (two survivors) into slot S: render records (uniform
         // vector loads, in-order completion) and this lane's feature operand
 #define GSR_FETCH(S)                                                                                \
         {                                                                                           \
@@ -221,66 +214,67 @@ __global__ __launch_bounds__(GSR_TILE_PIX, NS == 2 ? 3 : 1) void k_render_fwd(Di
             S##b0 = rrec[2 * gb_]; S##b1 = rrec[2 * gb_ + 1];                                       \
             S##f = colors[(int64_t)(hi ? gb_ : ga_) * GSR_C + ch];                                  \
         }
-        // blend the k-step held in S for every strip of the group and accumulate on the matrix cores
-#define GSR_BLEND(S)                                                                                \
+        // stage 2: the pixel-local alphas of slot S (a missing survivor has alpha 0)
+#define GSR_ALPHA(S)                                                                                \
         {                                                                                           \
-            const float4 a0_ = make_float4(S##a0.x, S##a0.y, S##v ? S##a0.z : 0.f, S##a0.w);        \
-            const float4 b0_ = make_float4(S##b0.x, S##b0.y, S##hb ? S##b0.z : 0.f, S##b0.w);       \
+            S##al = S##v ? alpha_of<EXACT>(S##a0, S##a1, pfx, pfy) : 0.f;                           \
+            S##bl = S##hb ? alpha_of<EXACT>(S##b0, S##b1, pfx, pfy) : 0.f;                          \
+            S##ai = S##a0.w;                                                                        \
+            S##bi = S##b0.w;                                                                        \
+        }
+        // stage 3: the serial blend of slot S and its accumulation on the matrix cores
+#define GSR_TAKE(S)                                                                                 \
+        {                                                                                           \
             const float f_ = (S##v && (!hi || S##hb)) ? S##f : 0.f;                                 \
-            _Pragma("unroll")                                                                       \
-            for (int k = 0; k < NS; k++) {                                                          \
-                const bool was_done_ = done[k];                                                     \
-                const float wa_ = blend_one<EXACT>(a0_, S##a1, pfx, pfy[k], S##pa, T[k], invd[k],   \
-                                                   last[k], done[k]);                               \
-                const bool done_a_ = done[k];                                                       \
-                const float wb_ = blend_one<EXACT>(b0_, S##b1, pfx, pfy[k], S##pb, T[k], invd[k],   \
-                                                   last[k], done[k]);                               \
-                if (STATS) {                                                                        \
-                    if (!was_done_ && done_a_) stop[k] = (uint32_t)S##pa;                           \
-                    else if (!done_a_ && done[k]) stop[k] = (uint32_t)S##pb;                        \
-                    n_contrib_pairs += __popcll(__ballot(wa_ > 0.f)) + __popcll(__ballot(wb_ > 0.f)); \
-                }                                                                                   \
-                const auto sw_ = __builtin_amdgcn_permlane32_swap(__float_as_uint(wa_),             \
-                                                                  __float_as_uint(wb_), false, false); \
-                acc[k][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(f_, __uint_as_float(sw_[0]), acc[k][0], 0, 0, 0); \
-                acc[k][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(f_, __uint_as_float(sw_[1]), acc[k][1], 0, 0, 0); \
-            }                                                                                       \
+            const bool was_done_ = done;                                                            \
+            const float wa_ = take_step(S##al, S##ai, (uint32_t)S##pa, T, invd, last, done);        \
+            const bool done_a_ = done;                                                              \
+            const float wb_ = take_step(S##bl, S##bi, (uint32_t)S##pb, T, invd, last, done);        \
             if (STATS) {                                                                            \
-                n_steps += S##v ? 1 : 0;                                                            \
+                if (!was_done_ && done_a_) stop = (uint32_t)S##pa;                                  \
+                else if (!done_a_ && done) stop = (uint32_t)S##pb;                                  \
+                n_contrib_pairs += __popcll(__ballot(wa_ > 0.f)) + __popcll(__ballot(wb_ > 0.f));   \
                 n_surv += S##v ? (S##hb ? 2 : 1) : 0;                                               \
             }                                                                                       \
+            if (STATS || TL) n_steps += S##v ? 1 : 0;                                               \
+            const auto sw_ = __builtin_amdgcn_permlane32_swap(__float_as_uint(wa_),                 \
+                                                              __float_as_uint(wb_), false, false);  \
+            acc0 = __builtin_amdgcn_mfma_f32_32x32x2f32(f_, __uint_as_float(sw_[0]), acc0, 0, 0, 0); \
+            acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(f_, __uint_as_float(sw_[1]), acc1, 0, 0, 0); \
         }
-        // two register sets, so step s+1's loads are in flight while step s is blended.  The loop
-        // leaves only at its head and its foot (an invalid set blends as two null Gaussians), which
-        // keeps the MFMA accumulators in one register chain.
-        bool Av, Ahb, Bv, Bhb;
-        int Apa, Apb, Bpa, Bpb;
-        float4 Aa0, Aa1, Ab0, Ab1, Ba0, Ba1, Bb0, Bb1;
-        float Af, Bf;
+#define GSR_SLOT(S) bool S##v, S##hb; int S##pa, S##pb; float4 S##a0, S##a1, S##b0, S##b1; \
+        float S##f, S##al, S##bl, S##ai, S##bi;
+        GSR_SLOT(A)
+        GSR_SLOT(B)
+        GSR_SLOT(C)
+        // An invalid slot takes nothing (alpha 0, feature 0); the loop leaves only at its head and
+        // its foot, which keeps the MFMA accumulators in one register chain.
         GSR_FETCH(A)
         GSR_FETCH(B)
+        GSR_FETCH(C)
+        GSR_ALPHA(A)
         while (Av) {
-            GSR_BLEND(A)
+            GSR_ALPHA(B)
+            GSR_TAKE(A)
             GSR_FETCH(A)
-            GSR_BLEND(B)
+            GSR_ALPHA(C)
+            GSR_TAKE(B)
             GSR_FETCH(B)
-            // every pixel of the group finished (written without a loop: a bool reduction loop here
-            // costs the register allocator ~40 VGPRs)
-            if (!__any(!done[0] || !done[NS - 1])) break;
+            GSR_ALPHA(A)
+            GSR_TAKE(C)
+            GSR_FETCH(C)
+            if (!__any(!done)) break;  // every pixel of the strip finished
         }
 #undef GSR_NEXT
 #undef GSR_FETCH
-#undef GSR_BLEND
+#undef GSR_ALPHA
+#undef GSR_TAKE
+#undef GSR_SLOT
 
         // ---- epilogue ----
         if (STATS) {
             unsigned long long* cn = (unsigned long long*)o.stats;
-            uint64_t ev = 0;
-#pragma unroll
-            for (int k = 0; k < NS; k++) {
-                const int py = ty * GSR_BY + (s0 + k) * 4 + (lane >> 4);
-                if (px < d.W && py < d.H) ev += done[k] ? stop[k] : (uint32_t)n;
-            }
+            uint64_t ev = (px < d.W && py < d.H) ? (done ? stop : (uint32_t)n) : 0;
             for (int off = 32; off > 0; off >>= 1) ev += __shfl_xor(ev, off);
             if (lane == 0) {
                 atomicAdd(&cn[0], (unsigned long long)ev);
@@ -288,16 +282,22 @@ __global__ __launch_bounds__(GSR_TILE_PIX, NS == 2 ? 3 : 1) void k_render_fwd(Di
                 atomicAdd(&cn[2], (unsigned long long)n_surv);
                 atomicAdd(&cn[3], (unsigned long long)n_steps);
                 atomicAdd(&cn[4], (unsigned long long)n_staged);
-                if (s0 == 0) {
+                if (strip == 0) {
                     atomicAdd(&cn[5], (unsigned long long)n);
                     atomicAdd(&cn[6], 1ull);
                 }
             }
         }
-#pragma unroll
-        for (int k = 0; k < NS; k++)
-            store_strip<false>(d, im, o, in.bg + in.s_bg * b, b, tx, ty * GSR_BY + (s0 + k) * 4, lane, acc[k][0],
-                               acc[k][1], T[k], invd[k], last[k]);
+        if (TL && lane == 0 && item < o.timeline_cap) {  // (start, end) in 100 MHz ticks, k-steps, XCC
+            const uint64_t t_end = __builtin_amdgcn_s_memrealtime();
+            uint32_t* rec = o.timeline + 4 * (size_t)item;
+            rec[0] = (uint32_t)t_start;
+            rec[1] = (uint32_t)t_end;
+            rec[2] = (uint32_t)n_steps;
+            rec[3] = __builtin_amdgcn_s_getreg((3 << 11) | 20) & 7u;
+        }
+        store_strip<false>(d, im, o, in.bg + in.s_bg * b, b, tx, ty * GSR_BY + strip * 4, lane, acc0, acc1, T,
+                           invd, last);
     }
 }
 
@@ -307,16 +307,10 @@ void launch_render_fwd(const Dims& d, const Inputs& in, const GeomArena& g, cons
     if (nwaves == 0) return;
     const int grid = min((nwaves + 3) / 4, persistent_grid(8));
     const dim3 gr(grid), bl(GSR_TILE_PIX);
-    static int ns = -1;
-    if (ns < 0) { const char* e = getenv("GSR_RENDER_NS"); ns = e ? atoi(e) : 1; }
-#define GSR_LAUNCH(E, S, N) hipLaunchKernelGGL((k_render_fwd<E, S, N>), gr, bl, 0, s, d, in, g, im, b, o)
-    if (ns == 1) {
-        if (o.stats) { if (exact) GSR_LAUNCH(true, true, 1); else GSR_LAUNCH(false, true, 1); }
-        else { if (exact) GSR_LAUNCH(true, false, 1); else GSR_LAUNCH(false, false, 1); }
-    } else {
-        if (o.stats) { if (exact) GSR_LAUNCH(true, true, 2); else GSR_LAUNCH(false, true, 2); }
-        else { if (exact) GSR_LAUNCH(true, false, 2); else GSR_LAUNCH(false, false, 2); }
-    }
+#define GSR_LAUNCH(E, S, L) hipLaunchKernelGGL((k_render_fwd<E, S, L>), gr, bl, 0, s, d, in, g, im, b, o)
+    if (o.stats) { if (exact) GSR_LAUNCH(true, true, false); else GSR_LAUNCH(false, true, false); }
+    else if (o.timeline) { if (exact) GSR_LAUNCH(true, false, true); else GSR_LAUNCH(false, false, true); }
+    else { if (exact) GSR_LAUNCH(true, false, false); else GSR_LAUNCH(false, false, false); }
 #undef GSR_LAUNCH
 }
 

@@ -138,6 +138,10 @@ int gsr_profile_read(double* ms, int* counts, int n);
  * wave, [4] Gaussians staged (list entries loaded into LDS), [5] list entries of all tiles,
  * [6] tiles rendered, [7] reserved.  NULL restores the production kernel. */
 int gsr_render_counters(uint64_t* device_counters);
+/* Work-item timeline of the render kernel (a lightly instrumented variant runs while set):
+ * record i (4 uint32: start, end in 100 MHz ticks, MFMA k-steps, XCD) for the first `capacity`
+ * work items in longest-first order (strip items first, 4 per non-empty tile). */
+int gsr_render_timeline(uint32_t* device_records, uint32_t capacity);
 
 /* Synchronises `stream`; writes the batch's instance count and overflow flag. */
 int gsr_batch_status(const char* workspace, int B, int P, int64_t* R_total, int* overflow,
