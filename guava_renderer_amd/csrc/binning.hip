@@ -9,14 +9,14 @@
 // MI355X structure: the instances (Gaussian x tile, ~6 per Gaussian) are never sorted.  The
 // Gaussians are sorted once per frame by (depth bits, index); emitting instances in that order
 // with stable per-tile ranks yields every tile's list already ordered.
-//   1. k_scan_blocksums    exclusive scan of the per-256-Gaussian tile counts -> R (1 workgroup)
+//   1. k_frame_totals      per-frame instance counts and depth-key ranges, batch R (1 workgroup)
 //   2. depth sort          per frame: bucket count on the depth bits (range from preprocess),
 //                          bucket scan, scatter of (depth bits, index) keys, in-place ranking of
 //                          small buckets, LDS segment sort of the few large ones -> order[]
 //   3. k_chunk_count       per 256 depth-ordered Gaussians: tile histogram in LDS from 4 corner
 //                          updates per rect (2-D difference array) -> count table row;
 //      k_column_scan       per tile: exclusive scan down the table -> chunk bases, tile counts
-//   4. k_tile_scan         tile counts -> ranges, longest-first render work list
+//   4. k_tile_scan/place   per frame: tile counts -> ranges; longest-first render work list
 //   5. k_ordered_scatter   per chunk: load-balanced expansion of the instances over the workgroup,
 //                          stable rank = tile base + chunk base + earlier slots covering the tile
 //                          (popcount of row/column ballots), plus the exact 16x4 strip mask
@@ -54,44 +54,52 @@ __device__ __forceinline__ TV block_excl_scan(TV v, TV* total, TV* sh /* NT/64 +
     return res;
 }
 
-// ---------------------------------------------------------------- 1. block-sum scan
-// Also reduces the blocks' depth-key ranges to per-frame ranges for the bucket sort.
-__global__ __launch_bounds__(1024) void k_scan_blocksums(uint32_t* __restrict__ bs, int n,
-                                                         uint32_t* ctrl, int64_t R_cap,
-                                                         const uint32_t* __restrict__ bkey, uint32_t* fstat,
-                                                         int nblk) {
-    __shared__ uint64_t sh[1024 / 64 + 1];
-    const int per = (n + 1023) / 1024;
-    const int beg = threadIdx.x * per;
-    const int end = min(n, beg + per);
-    uint64_t s = 0;
-    for (int i = beg; i < end; i++) s += bs[i];
-    uint64_t total;
-    uint64_t ex = block_excl_scan<uint64_t, 1024>(s, &total, sh);
-    uint32_t km = 0, nkm = 0;
-    int f = beg / nblk;
-    for (int i = beg; i < end; i++) {
-        const uint32_t v = bs[i];
-        bs[i] = (uint32_t)ex;
-        ex += v;
-        if (i / nblk != f) {  // frame boundary inside this thread's range
-            if (km) { atomicMax(&fstat[kFsWords * f + kFsKeyMax], km); atomicMax(&fstat[kFsWords * f + kFsNotKeyMax], nkm); }
-            km = nkm = 0;
-            f = i / nblk;
+// ---------------------------------------------------------------- 1. frame totals
+// One workgroup, one wave per frame at a time: the frame's instance count (sum of preprocess's
+// block sums) and depth-key range for the bucket sort; then the batch-wide list offsets and the
+// batch total against the capacity.
+__global__ __launch_bounds__(1024) void k_frame_totals(const uint32_t* __restrict__ bs,
+                                                       const uint32_t* __restrict__ bkey, int B, int nblk,
+                                                       uint32_t* ctrl, uint32_t* fstat, int64_t R_cap) {
+    extern __shared__ uint32_t rf[];  // [B] instances per frame
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    for (int f = wv; f < B; f += 1024 / 64) {
+        const uint32_t* fb = bs + (int64_t)f * nblk;
+        const uint32_t* fk = bkey + 2 * (int64_t)f * nblk;
+        uint32_t r = 0, km = 0, nkm = 0;
+        for (int i = lane; i < nblk; i += 64) {
+            r += fb[i];
+            km = max(km, fk[2 * i]);
+            nkm = max(nkm, fk[2 * i + 1]);
         }
-        km = max(km, bkey[2 * i]);
-        nkm = max(nkm, bkey[2 * i + 1]);
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) {
+            r += __shfl_xor(r, off);
+            km = max(km, (uint32_t)__shfl_xor(km, off));
+            nkm = max(nkm, (uint32_t)__shfl_xor(nkm, off));
+        }
+        if (lane == 0) {
+            rf[f] = r;
+            fstat[kFsWords * f + kFsR] = r;
+            fstat[kFsWords * f + kFsKeyMax] = km;
+            fstat[kFsWords * f + kFsNotKeyMax] = nkm;
+        }
     }
-    if (km) { atomicMax(&fstat[kFsWords * f + kFsKeyMax], km); atomicMax(&fstat[kFsWords * f + kFsNotKeyMax], nkm); }
+    __syncthreads();
     if (threadIdx.x == 0) {
-        ctrl[kCtrlRLo] = (uint32_t)min(total, (uint64_t)0xFFFFFFFFu);
-        ctrl[kCtrlOverflow] = (total > (uint64_t)R_cap || total >= 0xFFFFFFF0ull) ? 1u : 0u;
+        uint64_t base = 0;
+        for (int f = 0; f < B; f++) {
+            fstat[kFsWords * f + kFsRBase] = (uint32_t)min(base, (uint64_t)0xFFFFFFFFu);
+            base += rf[f];
+        }
+        ctrl[kCtrlRLo] = (uint32_t)min(base, (uint64_t)0xFFFFFFFFu);
+        ctrl[kCtrlOverflow] = (base > (uint64_t)R_cap || base >= 0xFFFFFFF0ull) ? 1u : 0u;
     }
 }
 
 void launch_scan_blocksums(const Dims& d, const GeomArena& g, int64_t R_cap, hipStream_t s) {
-    hipLaunchKernelGGL(k_scan_blocksums, dim3(1), dim3(1024), 0, s, g.blocksums, d.B * d.nblk, g.ctrl,
-                       R_cap, g.blockkey, g.fstat, d.nblk);
+    hipLaunchKernelGGL(k_frame_totals, dim3(1), dim3(1024), (size_t)d.B * 4, s, g.blocksums, g.blockkey, d.B,
+                       d.nblk, g.ctrl, g.fstat, R_cap);
 }
 
 // ---------------------------------------------------------------- segment sort (LDS)
@@ -448,54 +456,75 @@ void launch_chunk_count(const Dims& d, const GeomArena& g, const ImageArena& im,
 }
 
 // ---------------------------------------------------------------- 4. tile ranges
-// Also emits the render worklist: every tile of the batch ordered by descending log2 list length
-// (counting sort over 34 buckets; empty tiles last), so persistent render workgroups take the
-// longest tiles first (LPT scheduling) and no XCD is left with only empty tiles.
-__global__ __launch_bounds__(1024) void k_tile_scan(int n, const uint32_t* __restrict__ cnt,
-                                                    uint2* __restrict__ ranges, uint32_t* ctrl,
-                                                    uint32_t* work_list) {
-    constexpr int kBuckets = 34;  // bucket 0: longest (2^32..), bucket 33: empty
+// Per frame (one workgroup each): exclusive scan of the tile counts from the frame's batch-wide
+// offset -> ranges (empty tiles keep the reference's memset value (0,0), rasterizer_impl.cu:313),
+// and a histogram of the tiles over the work-list buckets (clz of the list length).  Then every
+// frame places its tiles into the batch-wide render work list, bucket-major (longest lists first,
+// empty tiles last), so persistent render workgroups take the longest tiles first.
+__global__ __launch_bounds__(1024) void k_tile_scan(Dims d, GeomArena g, ImageArena im) {
     __shared__ uint32_t sh[1024 / 64 + 1];
-    __shared__ uint32_t bcount[kBuckets];
-    const bool ovf = ctrl[kCtrlOverflow] != 0;
-    if (threadIdx.x < kBuckets) bcount[threadIdx.x] = 0;
-    const int per = (n + 1023) / 1024;
-    const int beg = threadIdx.x * per;
-    const int end = min(n, beg + per);
+    __shared__ uint32_t h[kLptBuckets];
+    const int b = blockIdx.x;
+    const bool ovf = g.ctrl[kCtrlOverflow] != 0;
+    if (threadIdx.x < kLptBuckets) h[threadIdx.x] = 0;
+    const int per = (d.T + 1023) / 1024;
+    const int beg = threadIdx.x * per, end = min(d.T, beg + per);
+    const uint32_t* cnt = im.tile_count + (int64_t)b * d.T;
     uint32_t s = 0;
     if (!ovf)
-        for (int i = beg; i < end; i++) s += cnt[i];
+        for (int t = beg; t < end; t++) s += cnt[t];
     uint32_t total;
-    uint32_t ex = block_excl_scan<uint32_t, 1024>(s, &total, sh);  // (barriers order bcount init)
-    for (int i = beg; i < end; i++) {
-        const uint32_t c = ovf ? 0u : cnt[i];
-        // empty tiles keep the reference's memset value (0,0) (rasterizer_impl.cu:313)
-        ranges[i] = c ? make_uint2(ex, ex + c) : make_uint2(0u, 0u);
-        const int bk = c ? __clz(c) : kBuckets - 1;
-        atomicAdd(&bcount[bk], 1u);
+    uint32_t ex = block_excl_scan<uint32_t, 1024>(s, &total, sh) + (ovf ? 0u : g.fstat[kFsWords * b + kFsRBase]);
+    uint2* rg = im.ranges + (int64_t)b * d.T;
+    for (int t = beg; t < end; t++) {
+        const uint32_t c = ovf ? 0u : cnt[t];
+        rg[t] = c ? make_uint2(ex, ex + c) : make_uint2(0u, 0u);
+        atomicAdd(&h[c ? __clz(c) : kLptBuckets - 1], 1u);
         ex += c;
     }
     __syncthreads();
-    if (threadIdx.x == 0) {
+    if (threadIdx.x < kLptBuckets) im.lpt_hist[b * kLptBuckets + threadIdx.x] = h[threadIdx.x];
+}
+
+__global__ __launch_bounds__(1024) void k_tile_place(Dims d, GeomArena g, ImageArena im) {
+    extern __shared__ uint32_t hist[];  // [B][kLptBuckets]
+    __shared__ uint32_t cur[kLptBuckets];
+    const int b = blockIdx.x;
+    for (int i = threadIdx.x; i < d.B * kLptBuckets; i += 1024) hist[i] = im.lpt_hist[i];
+    __syncthreads();
+    if (threadIdx.x < kLptBuckets) {  // bucket totals over all frames, and this frame's share before it
+        const int bk = threadIdx.x;
+        uint32_t tot = 0, mine = 0;
+        for (int f = 0; f < d.B; f++) {
+            const uint32_t v = hist[f * kLptBuckets + bk];
+            tot += v;
+            if (f < b) mine += v;
+        }
+        cur[bk] = tot;
+        hist[bk] = mine;  // (row 0 is no longer needed)
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {  // start of this frame's run in each bucket (bucket-major)
         uint32_t acc = 0;
-        for (int k = 0; k < kBuckets; k++) {
-            if (k == kBuckets - 1) ctrl[kCtrlNonEmpty] = acc;
-            const uint32_t v = bcount[k];
-            bcount[k] = acc;
-            acc += v;
+        for (int bk = 0; bk < kLptBuckets; bk++) {
+            const uint32_t t = cur[bk];
+            if (b == 0 && bk == kLptBuckets - 1) g.ctrl[kCtrlNonEmpty] = acc;  // non-empty tiles
+            cur[bk] = acc + hist[bk];
+            acc += t;
         }
     }
     __syncthreads();
-    for (int i = beg; i < end; i++) {
-        const uint32_t c = ovf ? 0u : cnt[i];
-        const int bk = c ? __clz(c) : kBuckets - 1;
-        work_list[atomicAdd(&bcount[bk], 1u)] = (uint32_t)i;
+    const bool ovf = g.ctrl[kCtrlOverflow] != 0;
+    const uint32_t* cnt = im.tile_count + (int64_t)b * d.T;
+    for (int t = threadIdx.x; t < d.T; t += 1024) {
+        const uint32_t c = ovf ? 0u : cnt[t];
+        im.work_list[atomicAdd(&cur[c ? __clz(c) : kLptBuckets - 1], 1u)] = (uint32_t)(b * d.T + t);
     }
 }
 
 void launch_tile_scan(const Dims& d, const GeomArena& g, const ImageArena& im, hipStream_t s) {
-    hipLaunchKernelGGL(k_tile_scan, dim3(1), dim3(1024), 0, s, d.B * d.T, im.tile_count, im.ranges,
-                       g.ctrl, im.work_list);
+    hipLaunchKernelGGL(k_tile_scan, dim3(d.B), dim3(1024), 0, s, d, g, im);
+    hipLaunchKernelGGL(k_tile_place, dim3(d.B), dim3(1024), (size_t)d.B * kLptBuckets * 4, s, d, g, im);
 }
 
 // ---------------------------------------------------------------- strip masks

@@ -132,6 +132,7 @@ size_t carve_image(char* base, const Dims& d, ImageArena* im) {
     a.ranges = take<uint2>(base, off, nt);
     a.tile_count = take<uint32_t>(base, off, nt);
     a.work_list = take<uint32_t>(base, off, nt);
+    a.lpt_hist = take<uint32_t>(base, off, (size_t)d.B * kLptBuckets);
     if (im) *im = a;
     return align_up(off) + 256;
 }
@@ -338,6 +339,7 @@ int gsr_forward_batch(int B, int P, int width, int height, const float* means3D,
     if (B <= 0 || P <= 0 || width <= 0 || height <= 0 || !workspace || !tanfov)
         return fail(GSR_ERR_ARG, "bad batch arguments");
     if ((int64_t)((width + 15) / 16) * ((height + 15) / 16) > kMaxTiles) return fail(GSR_ERR_ARG, "image too large");
+    if (B > kMaxFrames) return fail(GSR_ERR_ARG, "too many frames per batch");
     if (P >= kMaxGaussians) return fail(GSR_ERR_ARG, "P must be < 2^28");
     if (!colors) return fail(GSR_ERR_NO_COLORS, "For non-RGB, provide precomputed Gaussian colors!");
     if (((uintptr_t)colors & 15) != 0 || ((colors_stride * 4) & 15) != 0)

@@ -39,8 +39,13 @@ enum FrameStat : int {
     kFsNotKeyMax = 0,  // max of ~depth_bits over the frame's visible Gaussians (= ~min key)
     kFsKeyMax = 1,     // max of depth_bits
     kFsVisible = 2,    // visible Gaussians (bucket-scan total)
-    kFsWords = 4
+    kFsR = 3,          // instances of the frame
+    kFsRBase = 4,      // instances of the frames before it (batch-wide list offset)
+    kFsNonEmpty = 5,   // non-empty tiles of the frame
+    kFsWords = 8
 };
+constexpr int kMaxFrames = 256;   // frames per batch (per-frame tables live in LDS)
+constexpr int kLptBuckets = 34;   // render work list: clz(list length), 33 = empty tile
 
 struct GeomArena {
     uint32_t* ctrl;       // kCtrlWords control words, then kFsWords per frame
@@ -72,6 +77,7 @@ struct ImageArena {
     uint2* ranges;        // per tile [start, end) into the batch's point_list
     uint32_t* tile_count;
     uint32_t* work_list;  // every tile of the batch, longest list first (render scheduling)
+    uint32_t* lpt_hist;   // per frame: tiles per work-list bucket
 };
 
 struct BinArena {

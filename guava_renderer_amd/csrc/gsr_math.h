@@ -45,6 +45,26 @@ __device__ __forceinline__ float expf_exact(float x) {
     return (x != x) ? x : r_;  // NaN passes through (select, no branch)
 }
 
+// expf_exact for the blend: the same value wherever it can matter (x in [-87, 0], where alpha may
+// reach 1/255), without the clamp and the NaN select -- the render's alpha_of zeroes alpha outside
+// that range itself, and a NaN propagates through the polynomial on its own.  The power-of-two
+// scaling is v_ldexp_f32, exact like the bit construction above.
+__device__ __forceinline__ float expf_blend(float x) {
+    const float k = rintf(x * 1.44269504088896341f);
+    float r = fmaf(k, -0.693359375f, x);
+    r = fmaf(k, 2.12194440e-4f, r);
+    float p = 1.9875691500e-4f;
+    p = fmaf(p, r, 1.3981999507e-3f);
+    p = fmaf(p, r, 8.3334519073e-3f);
+    p = fmaf(p, r, 4.1665795894e-2f);
+    p = fmaf(p, r, 1.6666665459e-1f);
+    p = fmaf(p, r, 5.0000001201e-1f);
+    const float r2 = r * r;
+    p = fmaf(p, r2, r);
+    p = p + 1.0f;
+    return __builtin_amdgcn_ldexpf(p, (int)k);
+}
+
 // Hardware exp2 path (v_exp_f32), used in "fast" mode.
 __device__ __forceinline__ float expf_fast(float x) {
     return __builtin_amdgcn_exp2f(x * 1.4426950408889634f);

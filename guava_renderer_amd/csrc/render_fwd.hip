@@ -40,8 +40,9 @@ template <bool EXACT>
 __device__ __forceinline__ float alpha_of(const float4 ga, const float4 gc, float pfx, float pfy) {
     const float dx = ga.x - pfx, dy = ga.y - pfy;
     const float power = blend_power(gc.x, gc.y, gc.z, dx, dy);
-    const float alpha = fminf(0.99f, ga.z * blend_exp<EXACT>(power));
-    return (power > 0.0f) ? 0.0f : alpha;
+    const float alpha = fminf(0.99f, ga.z * (EXACT ? expf_blend(power) : expf_fast(power)));
+    // power < -87: exp < 2e-38, alpha < 1/255 -- never taken, as in the reference
+    return (power > 0.0f || power < -87.0f) ? 0.0f : alpha;
 }
 
 __device__ __forceinline__ float take_step(float alpha, float inv_depth, uint32_t pos, float& T, float& invd,

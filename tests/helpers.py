@@ -32,7 +32,7 @@ def geom_layout(P, W, H):
     T = ((W + 15) // 16) * ((H + 15) // 16)
     NB = _nb(P)
     nchunk = (P + 255) // 256
-    return _carve([("ctrl", np.uint32, 9216 + 4), ("depth", np.float32, P), ("invdepth", np.float32, P),
+    return _carve([("ctrl", np.uint32, 9216 + 8), ("depth", np.float32, P), ("invdepth", np.float32, P),
                    ("radii", np.int32, P), ("means2D", np.float32, 2 * P), ("cov3D", np.float32, 6 * P),
                    ("conic", np.float32, 4 * P), ("rect", np.uint32, 2 * P), ("rrec", np.float32, 8 * P),
                    ("tiles", np.uint32, P), ("blocksums", np.uint32, nblk + 1), ("blockkey", np.uint32, 2 * nblk), ("bslot", np.uint32, P),
@@ -43,7 +43,8 @@ def geom_layout(P, W, H):
 def image_layout(W, H):
     T = ((W + 15) // 16) * ((H + 15) // 16)
     return _carve([("final_T", np.float32, W * H), ("n_contrib", np.uint32, W * H),
-                   ("ranges", np.uint32, 2 * T), ("tile_count", np.uint32, T), ("work_list", np.uint32, T)])
+                   ("ranges", np.uint32, 2 * T), ("tile_count", np.uint32, T), ("work_list", np.uint32, T),
+                   ("lpt_hist", np.uint32, 34)])
 
 
 def bin_layout(R):
