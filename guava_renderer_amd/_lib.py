@@ -8,12 +8,14 @@ import os
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "lib", "libgsr.so")
 
-# every symbol declared in include/gsr.h
+# every symbol declared in include/gsr.h and include/gsr_deform.h
 EXPORTS = ("gsr_version", "gsr_last_error", "gsr_set_exact_exp", "gsr_geometry_bytes",
            "gsr_image_bytes", "gsr_binning_bytes", "gsr_mark_visible", "gsr_forward",
            "gsr_backward", "gsr_batch_workspace_bytes", "gsr_forward_batch",
            "gsr_backward_batch", "gsr_batch_status", "gsr_profile_enable", "gsr_profile_read",
-           "gsr_render_counters", "gsr_render_timeline")
+           "gsr_render_counters", "gsr_render_timeline",
+           # include/gsr_deform.h
+           "gsr_lbs_workspace_bytes", "gsr_lbs", "gsr_deform_gaussians")
 
 ALLOC_FN = ctypes.CFUNCTYPE(ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t)
 
@@ -87,6 +89,14 @@ def load(path=None):
     L.gsr_render_counters.restype = _i
     L.gsr_render_timeline.argtypes = [_vp, ctypes.c_uint32]
     L.gsr_render_timeline.restype = _i
+    L.gsr_lbs_workspace_bytes.argtypes = [_i, _i, _i, _i]
+    L.gsr_lbs_workspace_bytes.restype = _sz
+    L.gsr_lbs.argtypes = [_i, _i, _i, _i, _vp, _i64, _vp, _vp, _vp, _i, _vp, _vp, _vp, _vp, _vp, _vp,
+                          _vp, _vp, _vp, _vp, _vp, _vp, _vp]
+    L.gsr_lbs.restype = _i
+    L.gsr_deform_gaussians.argtypes = [_i, _i, _i, _i, _vp, _vp, _vp, _vp, _i64, _vp, _i64, _vp, _vp,
+                                       _vp, _i64, _vp, _i64, _vp, _i64, _vp, _vp, _vp, _vp, _vp]
+    L.gsr_deform_gaussians.restype = _i
     _lib = L
     return L
 

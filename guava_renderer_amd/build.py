@@ -16,7 +16,7 @@ LIB_DIR = os.path.join(HERE, "lib")
 OBJ_DIR = os.path.join(HERE, "lib", "obj")
 LIB = os.path.join(LIB_DIR, "libgsr.so")
 SOURCES = ["preprocess.hip", "binning.hip", "render_fwd.hip", "render_bwd.hip",
-           "preprocess_bwd.hip", "capi.hip"]
+           "preprocess_bwd.hip", "deform.hip", "capi.hip"]
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = os.environ.get("GSR_OFFLOAD_ARCH", "gfx950")
 FLAGS = ["-O3", "-std=c++17", "-fPIC", "-ffp-contract=off", f"--offload-arch={ARCH}",
@@ -38,7 +38,8 @@ def _newer(src_paths, dst):
 def _compile(src):
     obj = os.path.join(OBJ_DIR, os.path.splitext(src)[0] + ".o")
     deps = [os.path.join(CSRC, src)] + [os.path.join(CSRC, h) for h in os.listdir(CSRC) if h.endswith(".h")]
-    deps.append(os.path.join(os.path.dirname(HERE), "include", "gsr.h"))
+    inc = os.path.join(os.path.dirname(HERE), "include")
+    deps += [os.path.join(inc, h) for h in os.listdir(inc) if h.endswith(".h")]
     if _newer(deps, obj):
         cmd = [HIPCC] + FLAGS + EXTRA.get(src, []) + ["-c", os.path.join(CSRC, src), "-o", obj]
         r = subprocess.run(cmd, capture_output=True, text=True)

@@ -168,6 +168,9 @@ int run_binning_and_render(const Dims& d, const Inputs& in, const GeomArena& g, 
 
 }  // namespace
 
+// error reporting for the other C-ABI translation units (deform.hip)
+int gsr::api_fail(int status, const char* msg) { return fail((gsr_status)status, msg); }
+
 extern "C" {
 
 const char* gsr_version(void) { return "gsr-gfx950 0.1"; }

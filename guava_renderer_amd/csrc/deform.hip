@@ -1,0 +1,509 @@
+// deform.hip -- per-frame avatar deformation on gfx950: linear-blend skinning (SMPL-X body /
+// FLAME head) and GUAVA's Gaussian assembly, B frames per launch set (include/gsr_deform.h).
+//
+// Reference (restated, not translated):
+//   lbs / lbs_wobeta                models/modules/flame/lbs.py:142-229 / :255-333
+//   blend_shapes, vertices2joints   lbs.py:355-376, :335-352
+//   batch_rodrigues                 lbs.py:379-410
+//   batch_rigid_transform           lbs.py:426-482
+//   Ubody_Gaussian.forward          models/UbodyAvatar/ubody_gaussian.py:252-278
+//   compute_face_orientation        utils/graphics_utils.py:52-80
+//   roma 1.5.3 rotmat_to_unitquat / quat_product (third-party, scipy-derived; call sites
+//   ubody_gaussian.py:253-254,258,270)
+//
+// Kernels (all B frames per launch):
+//   k_lbs_rodrigues  B*J threads      axis-angle -> R, pose feature R - I
+//   k_lbs_blend      3V x B/8         v_shaped = template + shapedirs.betas, v_posed = v_shaped +
+//                                     posedirs.feature: the bases are streamed once per 8 frames
+//                                     (HBM-bound: 4*(NB + 9(J-1)) bytes per vertex coordinate)
+//   k_lbs_joints     J x B workgroups J_regressor . v_shaped (+ joints_offset)
+//   k_lbs_chain      B waves          the kinematic chain (J sequential 4x4 products) in LDS
+//   k_lbs_skin       V x B            T_v = sum_j w_vj A_j, v = T_v [v_posed; 1]
+//   k_deform_gaussians (V+N) x B      vertex + UV Gaussians straight into the rasterizer's inputs
+// Every sum runs in a fixed order (fmaf chains over k in index order, 3-term dots left to right),
+// so results are deterministic run to run.
+#include <string>
+
+#include "../../include/gsr.h"
+#include "../../include/gsr_deform.h"
+#include "gsr_internal.h"
+
+namespace gsr {
+
+constexpr int kLbsFrames = 8;  // frames per k_lbs_blend thread (accumulators per thread)
+
+struct Parents {
+    int8_t p[GSR_LBS_MAX_JOINTS];
+};
+
+// batch_rodrigues (lbs.py:379-410): angle = |r + 1e-8|, dir = r / angle,
+// R = I + sin K + (1 - cos) K.K with K the cross-product matrix of dir.
+__global__ void k_lbs_rodrigues(int B, int J, const float* __restrict__ pose, int pose2rot,
+                                float* __restrict__ rot, float* __restrict__ feat) {
+    const int t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= B * J) return;
+    const int b = t / J, j = t - b * J;
+    float R[9];
+    if (pose2rot) {
+        const float rx = pose[3 * t], ry = pose[3 * t + 1], rz = pose[3 * t + 2];
+        const float ex = rx + 1e-8f, ey = ry + 1e-8f, ez = rz + 1e-8f;
+        const float angle = sqrtf(ex * ex + ey * ey + ez * ez);
+        const float x = rx / angle, y = ry / angle, z = rz / angle;
+        const float c = cosf(angle), s = sinf(angle);
+        const float K[9] = {0.f, -z, y, z, 0.f, -x, -y, x, 0.f};
+        const float omc = 1.0f - c;
+#pragma unroll
+        for (int r = 0; r < 3; r++)
+#pragma unroll
+            for (int q = 0; q < 3; q++) {
+                const float kk = K[3 * r] * K[q] + K[3 * r + 1] * K[3 + q] + K[3 * r + 2] * K[6 + q];
+                R[3 * r + q] = ((r == q ? 1.0f : 0.0f) + s * K[3 * r + q]) + omc * kk;
+            }
+    } else {
+#pragma unroll
+        for (int e = 0; e < 9; e++) R[e] = pose[9 * t + e];
+    }
+#pragma unroll
+    for (int e = 0; e < 9; e++) rot[9 * t + e] = R[e];
+    if (j > 0) {  // pose_feature = (rot_mats[:, 1:] - I).view(B, -1)   (lbs.py:303)
+        float* f = feat + (int64_t)b * (J - 1) * 9 + (j - 1) * 9;
+#pragma unroll
+        for (int e = 0; e < 9; e++) f[e] = R[e] - ((e % 4) == 0 ? 1.0f : 0.0f);
+    }
+}
+
+// v_shaped = v_template + blend_shapes(betas, shapedirs); v_posed = pose_offsets + v_shaped
+// (lbs.py:186,201,210 / :305,314).  One thread per vertex coordinate m of kLbsFrames frames; the
+// frame coefficients sit in LDS and the k-major bases are read coalesced, once per frame group.
+__global__ __launch_bounds__(256) void k_lbs_blend(int B, int M, int NB, int NP,
+                                                   const float* __restrict__ vt, int64_t vt_stride,
+                                                   const float* __restrict__ betas,
+                                                   const float* __restrict__ sd_t,
+                                                   const float* __restrict__ feat,
+                                                   const float* __restrict__ pd,
+                                                   float* __restrict__ v_shaped,
+                                                   float* __restrict__ v_posed) {
+    extern __shared__ float coef[];  // [(NB + NP)][kLbsFrames]
+    const int b0 = blockIdx.y * kLbsFrames;
+    const int nk = NB + NP;
+    for (int idx = threadIdx.x; idx < nk * kLbsFrames; idx += blockDim.x) {
+        const int k = idx / kLbsFrames, f = idx - k * kLbsFrames;
+        const int b = b0 + f;
+        float v = 0.f;
+        if (b < B) v = k < NB ? betas[(int64_t)b * NB + k] : feat[(int64_t)b * NP + (k - NB)];
+        coef[idx] = v;
+    }
+    __syncthreads();
+    const int m = blockIdx.x * blockDim.x + threadIdx.x;
+    if (m >= M) return;
+    const int nf = min(kLbsFrames, B - b0);
+    float acc[kLbsFrames];
+#pragma unroll
+    for (int f = 0; f < kLbsFrames; f++) acc[f] = 0.f;
+    for (int k = 0; k < NB; k++) {
+        const float s = sd_t[(int64_t)k * M + m];
+        const float4 c0 = *reinterpret_cast<const float4*>(&coef[k * kLbsFrames]);
+        const float4 c1 = *reinterpret_cast<const float4*>(&coef[k * kLbsFrames + 4]);
+        acc[0] = fmaf(c0.x, s, acc[0]); acc[1] = fmaf(c0.y, s, acc[1]);
+        acc[2] = fmaf(c0.z, s, acc[2]); acc[3] = fmaf(c0.w, s, acc[3]);
+        acc[4] = fmaf(c1.x, s, acc[4]); acc[5] = fmaf(c1.y, s, acc[5]);
+        acc[6] = fmaf(c1.z, s, acc[6]); acc[7] = fmaf(c1.w, s, acc[7]);
+    }
+    float vs[kLbsFrames];
+#pragma unroll
+    for (int f = 0; f < kLbsFrames; f++) {
+        const int b = b0 + f;
+        vs[f] = 0.f;
+        if (f < nf) {
+            const float tv = vt[(int64_t)b * vt_stride + m];
+            vs[f] = NB > 0 ? tv + acc[f] : tv;
+            v_shaped[(int64_t)b * M + m] = vs[f];
+        }
+        acc[f] = 0.f;
+    }
+    for (int k = 0; k < NP; k++) {
+        const float p = pd[(int64_t)k * M + m];
+        const float4 c0 = *reinterpret_cast<const float4*>(&coef[(NB + k) * kLbsFrames]);
+        const float4 c1 = *reinterpret_cast<const float4*>(&coef[(NB + k) * kLbsFrames + 4]);
+        acc[0] = fmaf(c0.x, p, acc[0]); acc[1] = fmaf(c0.y, p, acc[1]);
+        acc[2] = fmaf(c0.z, p, acc[2]); acc[3] = fmaf(c0.w, p, acc[3]);
+        acc[4] = fmaf(c1.x, p, acc[4]); acc[5] = fmaf(c1.y, p, acc[5]);
+        acc[6] = fmaf(c1.z, p, acc[6]); acc[7] = fmaf(c1.w, p, acc[7]);
+    }
+#pragma unroll
+    for (int f = 0; f < kLbsFrames; f++)
+        if (f < nf) v_posed[(int64_t)(b0 + f) * M + m] = acc[f] + vs[f];
+}
+
+// vertices2joints (lbs.py:335-352): J[b,j,:] = sum_v J_regressor[j,v] v_shaped[b,v,:], plus
+// joints_offset (lbs.py:191/:295).  One workgroup per (joint, frame); fixed-shape tree reduction.
+__global__ __launch_bounds__(256) void k_lbs_joints(int V, int J, const float* __restrict__ jreg,
+                                                    const float* __restrict__ v_shaped,
+                                                    const float* __restrict__ joff,
+                                                    float* __restrict__ joints) {
+    __shared__ float red[3][256];
+    const int j = blockIdx.x, b = blockIdx.y;
+    const float* vs = v_shaped + (int64_t)b * V * 3;
+    const float* w = jreg + (int64_t)j * V;
+    float ax = 0.f, ay = 0.f, az = 0.f;
+    for (int v = threadIdx.x; v < V; v += blockDim.x) {
+        const float wv = w[v];
+        ax = fmaf(wv, vs[3 * v], ax);
+        ay = fmaf(wv, vs[3 * v + 1], ay);
+        az = fmaf(wv, vs[3 * v + 2], az);
+    }
+    red[0][threadIdx.x] = ax;
+    red[1][threadIdx.x] = ay;
+    red[2][threadIdx.x] = az;
+    __syncthreads();
+    for (int h = 128; h > 0; h >>= 1) {
+        if ((int)threadIdx.x < h)
+            for (int c = 0; c < 3; c++) red[c][threadIdx.x] += red[c][threadIdx.x + h];
+        __syncthreads();
+    }
+    if (threadIdx.x < 3) {
+        float v = red[threadIdx.x][0];
+        if (joff) v = v + joff[((int64_t)b * J + j) * 3 + threadIdx.x];
+        joints[((int64_t)b * J + j) * 3 + threadIdx.x] = v;
+    }
+}
+
+// batch_rigid_transform (lbs.py:426-482) for one frame per 64-lane workgroup: local transforms
+// [R | J_i - J_parent], the chain product in parent order (16 lanes, one matrix element each),
+// posed joints = chain[:, :3, 3], A = chain - pad(chain . [J; 0]).
+__global__ __launch_bounds__(64) void k_lbs_chain(int J, Parents par, const float* __restrict__ rot,
+                                                  const float* __restrict__ joints,
+                                                  float* __restrict__ jtrans,
+                                                  float* __restrict__ A) {
+    __shared__ float tm[GSR_LBS_MAX_JOINTS][16];
+    __shared__ float ch[GSR_LBS_MAX_JOINTS][16];
+    const int b = blockIdx.x, t = threadIdx.x;
+    const float* Jb = joints + (int64_t)b * J * 3;
+    if (t < J) {
+        const float* R = rot + ((int64_t)b * J + t) * 9;
+        float rel[3];
+        for (int c = 0; c < 3; c++) rel[c] = t == 0 ? Jb[c] : Jb[3 * t + c] - Jb[3 * par.p[t] + c];
+        for (int r = 0; r < 3; r++) {
+            for (int c = 0; c < 3; c++) tm[t][4 * r + c] = R[3 * r + c];
+            tm[t][4 * r + 3] = rel[r];
+        }
+        tm[t][12] = 0.f; tm[t][13] = 0.f; tm[t][14] = 0.f; tm[t][15] = 1.f;
+    }
+    __syncthreads();
+    if (t < 16) ch[0][t] = tm[0][t];
+    __syncthreads();
+    const int r = t >> 2, c = t & 3;
+    for (int i = 1; i < J; i++) {
+        if (t < 16) {
+            const float* P = ch[par.p[i]];
+            const float* L = tm[i];
+            ch[i][t] = P[4 * r] * L[c] + P[4 * r + 1] * L[4 + c] + P[4 * r + 2] * L[8 + c] +
+                       P[4 * r + 3] * L[12 + c];
+        }
+        __syncthreads();
+    }
+    if (t < J) {
+        const float* T = ch[t];
+        const float jx = Jb[3 * t], jy = Jb[3 * t + 1], jz = Jb[3 * t + 2];
+        float* a = A + ((int64_t)b * J + t) * 16;
+        for (int rr = 0; rr < 4; rr++) {
+            const float tj = T[4 * rr] * jx + T[4 * rr + 1] * jy + T[4 * rr + 2] * jz + T[4 * rr + 3] * 0.0f;
+            a[4 * rr] = T[4 * rr];
+            a[4 * rr + 1] = T[4 * rr + 1];
+            a[4 * rr + 2] = T[4 * rr + 2];
+            a[4 * rr + 3] = T[4 * rr + 3] - tj;
+        }
+        if (jtrans)
+            for (int rr = 0; rr < 3; rr++) jtrans[((int64_t)b * J + t) * 3 + rr] = T[4 * rr + 3];
+    }
+}
+
+// Skinning (lbs.py:218-227 / :320-331): T = W . A per vertex, v = T [v_posed; 1].
+__global__ __launch_bounds__(256) void k_lbs_skin(int V, int J, const float* __restrict__ w_t,
+                                                  const float* __restrict__ A,
+                                                  const float* __restrict__ v_posed,
+                                                  float* __restrict__ verts,
+                                                  float* __restrict__ vtrans) {
+    __shared__ float As[GSR_LBS_MAX_JOINTS * 16];
+    const int b = blockIdx.y;
+    for (int i = threadIdx.x; i < J * 16; i += blockDim.x) As[i] = A[(int64_t)b * J * 16 + i];
+    __syncthreads();
+    const int v = blockIdx.x * blockDim.x + threadIdx.x;
+    if (v >= V) return;
+    float T[16];
+#pragma unroll
+    for (int e = 0; e < 16; e++) T[e] = 0.f;
+    for (int j = 0; j < J; j++) {
+        const float w = w_t[(int64_t)j * V + v];
+#pragma unroll
+        for (int e = 0; e < 16; e++) T[e] = fmaf(w, As[16 * j + e], T[e]);
+    }
+    const float* p = v_posed + ((int64_t)b * V + v) * 3;
+    const float x = p[0], y = p[1], z = p[2];
+    float* o = verts + ((int64_t)b * V + v) * 3;
+#pragma unroll
+    for (int r = 0; r < 3; r++) o[r] = T[4 * r] * x + T[4 * r + 1] * y + T[4 * r + 2] * z + T[4 * r + 3] * 1.0f;
+    if (vtrans) {
+        float4* tv = reinterpret_cast<float4*>(vtrans + ((int64_t)b * V + v) * 16);
+        tv[0] = make_float4(T[0], T[1], T[2], T[3]);
+        tv[1] = make_float4(T[4], T[5], T[6], T[7]);
+        tv[2] = make_float4(T[8], T[9], T[10], T[11]);
+        tv[3] = make_float4(T[12], T[13], T[14], T[15]);
+    }
+}
+
+// roma.rotmat_to_unitquat (scipy's from_matrix decision scheme), row-major m -> (x, y, z, w).
+__device__ __forceinline__ float4 rotmat_to_unitquat(const float m[9]) {
+    const float d0 = m[0], d1 = m[4], d2 = m[8];
+    const float d3 = (d0 + d1) + d2;
+    int ch = 0;
+    float best = d0;
+    if (d1 > best) { best = d1; ch = 1; }
+    if (d2 > best) { best = d2; ch = 2; }
+    if (d3 > best) { best = d3; ch = 3; }
+    float q[4];
+    if (ch != 3) {
+        const int i = ch, j = (i + 1) % 3, k = (j + 1) % 3;
+        q[i] = (1.0f - d3) + 2.0f * m[4 * i];
+        q[j] = m[3 * j + i] + m[3 * i + j];
+        q[k] = m[3 * k + i] + m[3 * i + k];
+        q[3] = m[3 * k + j] - m[3 * j + k];
+    } else {
+        q[0] = m[7] - m[5];
+        q[1] = m[2] - m[6];
+        q[2] = m[3] - m[1];
+        q[3] = 1.0f + d3;
+    }
+    const float n = sqrtf(((q[0] * q[0] + q[1] * q[1]) + q[2] * q[2]) + q[3] * q[3]);
+    return make_float4(q[0] / n, q[1] / n, q[2] / n, q[3] / n);
+}
+
+// roma.quat_product, xyzw: (p_w q_v + q_w p_v + p_v x q_v, p_w q_w - p_v . q_v)
+__device__ __forceinline__ float4 quat_product(float4 p, float4 q) {
+    float4 o;
+    o.x = (p.w * q.x + q.w * p.x) + (p.y * q.z - p.z * q.y);
+    o.y = (p.w * q.y + q.w * p.y) + (p.z * q.x - p.x * q.z);
+    o.z = (p.w * q.z + q.w * p.z) + (p.x * q.y - p.y * q.x);
+    o.w = p.w * q.w - ((p.x * q.x + p.y * q.y) + p.z * q.z);
+    return o;
+}
+
+__device__ __forceinline__ float dot3(float ax, float ay, float az, float bx, float by, float bz) {
+    return (ax * bx + ay * by) + az * bz;
+}
+
+// Vertex Gaussians (ubody_gaussian.py:252-254): xyz = LBS vertex, rotation =
+// normalize(q(T_v[:3,:3]) (x) q_v) in wxyz, scale unchanged.  UV Gaussians (:257-271): face frame
+// [a0 a1 a2] and scale of the deformed binding face, centre = bary . face vertices, xyz =
+// (frame . local) * s + centre, rotation = q(frame) (x) q_uv (not renormalised), scale = scale * s.
+__global__ __launch_bounds__(256) void k_deform_gaussians(
+    int V, int F, int N, const float* __restrict__ verts, const float* __restrict__ vtrans,
+    const int32_t* __restrict__ faces, const float* __restrict__ vrot, int64_t s_vrot,
+    const float* __restrict__ vscale, int64_t s_vscale, const int32_t* __restrict__ bind,
+    const float* __restrict__ bary, const float* __restrict__ lxyz, int64_t s_lxyz,
+    const float* __restrict__ urot, int64_t s_urot, const float* __restrict__ uscale,
+    int64_t s_uscale, float* __restrict__ means, float* __restrict__ rots,
+    float* __restrict__ scales, uint32_t* __restrict__ bad) {
+    const int b = blockIdx.y;
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    const int P = V + N;
+    if (i >= P) return;
+    const int64_t o = (int64_t)b * P + i;
+    const float* vb = verts + (int64_t)b * V * 3;
+    if (i < V) {
+        const float4* tv = reinterpret_cast<const float4*>(vtrans + ((int64_t)b * V + i) * 16);
+        const float4 r0 = tv[0], r1 = tv[1], r2 = tv[2];
+        const float m[9] = {r0.x, r0.y, r0.z, r1.x, r1.y, r1.z, r2.x, r2.y, r2.z};
+        const float4 qd = rotmat_to_unitquat(m);
+        const float* qv = vrot + b * s_vrot + 4 * (int64_t)i;  // wxyz
+        const float4 q = quat_product(qd, make_float4(qv[1], qv[2], qv[3], qv[0]));
+        // F.normalize over the wxyz vector: x / max(||x||, 1e-12)
+        const float n = fmaxf(sqrtf(((q.w * q.w + q.x * q.x) + q.y * q.y) + q.z * q.z), 1e-12f);
+        reinterpret_cast<float4*>(rots)[o] = make_float4(q.w / n, q.x / n, q.y / n, q.z / n);
+        for (int c = 0; c < 3; c++) {
+            means[3 * o + c] = vb[3 * i + c];
+            scales[3 * o + c] = vscale[b * s_vscale + 3 * (int64_t)i + c];
+        }
+        return;
+    }
+    const int n = i - V;
+    int f = bind[n];
+    int i0 = 0, i1 = 0, i2 = 0;
+    bool ok = f >= 0 && f < F;
+    if (ok) {
+        i0 = faces[3 * f]; i1 = faces[3 * f + 1]; i2 = faces[3 * f + 2];
+        ok = i0 >= 0 && i0 < V && i1 >= 0 && i1 < V && i2 >= 0 && i2 < V;
+    }
+    if (!ok) {  // reference: an IndexError; here a flag and NaN outputs, no out-of-range access
+        if (bad) atomicOr(bad, 1u);
+        const float nan = __int_as_float(0x7fc00000);
+        for (int c = 0; c < 3; c++) { means[3 * o + c] = nan; scales[3 * o + c] = nan; }
+        reinterpret_cast<float4*>(rots)[o] = make_float4(nan, nan, nan, nan);
+        return;
+    }
+    const float v0x = vb[3 * i0], v0y = vb[3 * i0 + 1], v0z = vb[3 * i0 + 2];
+    const float v1x = vb[3 * i1], v1y = vb[3 * i1 + 1], v1z = vb[3 * i1 + 2];
+    const float v2x = vb[3 * i2], v2y = vb[3 * i2 + 1], v2z = vb[3 * i2 + 2];
+    // compute_face_orientation (graphics_utils.py:61-80), safe_normalize with eps 1e-20
+    const float e1x = v1x - v0x, e1y = v1y - v0y, e1z = v1z - v0z;
+    const float e2x = v2x - v0x, e2y = v2y - v0y, e2z = v2z - v0z;
+    const float l1 = sqrtf(fmaxf(dot3(e1x, e1y, e1z, e1x, e1y, e1z), 1e-20f));
+    const float a0x = e1x / l1, a0y = e1y / l1, a0z = e1z / l1;
+    const float c1x = a0y * e2z - a0z * e2y, c1y = a0z * e2x - a0x * e2z, c1z = a0x * e2y - a0y * e2x;
+    const float lc1 = sqrtf(fmaxf(dot3(c1x, c1y, c1z, c1x, c1y, c1z), 1e-20f));
+    const float a1x = c1x / lc1, a1y = c1y / lc1, a1z = c1z / lc1;
+    const float c2x = a1y * a0z - a1z * a0y, c2y = a1z * a0x - a1x * a0z, c2z = a1x * a0y - a1y * a0x;
+    const float lc2 = sqrtf(fmaxf(dot3(c2x, c2y, c2z, c2x, c2y, c2z), 1e-20f));
+    const float a2x = -(c2x / lc2), a2y = -(c2y / lc2), a2z = -(c2z / lc2);
+    const float s = (l1 + fabsf(dot3(a2x, a2y, a2z, e2x, e2y, e2z))) / 2.0f;
+    // orientation columns a0, a1, a2 (row-major m[r][c] = a_c[r])
+    const float m[9] = {a0x, a1x, a2x, a0y, a1y, a2y, a0z, a1z, a2z};
+    const float4 qf = rotmat_to_unitquat(m);
+    const float* qu = urot + b * s_urot + 4 * (int64_t)n;  // wxyz
+    const float4 q = quat_product(qf, make_float4(qu[1], qu[2], qu[3], qu[0]));
+    reinterpret_cast<float4*>(rots)[o] = make_float4(q.w, q.x, q.y, q.z);
+    const float w0 = bary[3 * n], w1 = bary[3 * n + 1], w2 = bary[3 * n + 2];
+    const float* l = lxyz + b * s_lxyz + 3 * (int64_t)n;
+    const float lx = l[0], ly = l[1], lz = l[2];
+    const float cx = (w0 * v0x + w1 * v1x) + w2 * v2x;
+    const float cy = (w0 * v0y + w1 * v1y) + w2 * v2y;
+    const float cz = (w0 * v0z + w1 * v1z) + w2 * v2z;
+    means[3 * o] = dot3(m[0], m[1], m[2], lx, ly, lz) * s + cx;
+    means[3 * o + 1] = dot3(m[3], m[4], m[5], lx, ly, lz) * s + cy;
+    means[3 * o + 2] = dot3(m[6], m[7], m[8], lx, ly, lz) * s + cz;
+    const float* us = uscale + b * s_uscale + 3 * (int64_t)n;
+    for (int c = 0; c < 3; c++) scales[3 * o + c] = us[c] * s;
+}
+
+namespace {
+
+size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
+
+struct LbsArena {
+    float *rot, *feat, *vs, *vp, *joints, *A;
+};
+
+size_t carve_lbs(char* base, int B, int V, int J, LbsArena* a) {
+    size_t off = 0;
+    auto take = [&](size_t bytes) {
+        char* p = base ? base + off : nullptr;
+        off += align256(bytes);
+        return reinterpret_cast<float*>(p);
+    };
+    const size_t f = sizeof(float);
+    LbsArena t;
+    t.rot = take(f * (size_t)B * J * 9);
+    t.feat = take(f * (size_t)B * (J > 1 ? J - 1 : 1) * 9);
+    t.vs = take(f * (size_t)B * V * 3);
+    t.vp = take(f * (size_t)B * V * 3);
+    t.joints = take(f * (size_t)B * J * 3);
+    t.A = take(f * (size_t)B * J * 16);
+    if (a) *a = t;
+    return off;
+}
+
+int hip_check(const char* what) {
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return api_fail(GSR_ERR_HIP, (std::string(what) + ": " + hipGetErrorString(e)).c_str());
+    return 0;
+}
+
+}  // namespace
+}  // namespace gsr
+
+using namespace gsr;
+
+extern "C" {
+
+size_t gsr_lbs_workspace_bytes(int B, int V, int J, int NB) {
+    (void)NB;
+    if (B <= 0 || V <= 0 || J <= 0) return 0;
+    return carve_lbs(nullptr, B, V, J, nullptr);
+}
+
+int gsr_lbs(int B, int V, int J, int NB, const float* v_template, int64_t v_template_stride,
+            const float* betas, const float* shapedirs_t, const float* pose, int pose2rot,
+            const float* posedirs, const float* J_regressor, const int32_t* parents_host,
+            const float* lbs_weights_t, const float* joints_offset, float* verts,
+            float* joints_transformed, float* joints, float* vert_transforms,
+            float* joint_transforms, float* v_shaped, char* workspace, void* stream) {
+    if (B <= 0 || V <= 0) return api_fail(GSR_ERR_ARG, "gsr_lbs: B and V must be positive");
+    if (J < 1 || J > GSR_LBS_MAX_JOINTS) return api_fail(GSR_ERR_ARG, "gsr_lbs: J must be in [1, 64]");
+    if (!v_template || !pose || !J_regressor || !parents_host || !lbs_weights_t || !verts || !workspace)
+        return api_fail(GSR_ERR_ARG, "gsr_lbs: null required pointer");
+    if (J > 1 && !posedirs) return api_fail(GSR_ERR_ARG, "gsr_lbs: posedirs is null");
+    if (v_template_stride != 0 && v_template_stride != (int64_t)V * 3)
+        return api_fail(GSR_ERR_ARG, "gsr_lbs: v_template stride must be 0 or V*3");
+    if (betas) {
+        if (NB <= 0 || !shapedirs_t) return api_fail(GSR_ERR_ARG, "gsr_lbs: betas need NB > 0 and shapedirs");
+    } else {
+        NB = 0;
+    }
+    Parents par;
+    for (int i = 0; i < GSR_LBS_MAX_JOINTS; i++) par.p[i] = -1;
+    if (parents_host[0] != -1) return api_fail(GSR_ERR_ARG, "gsr_lbs: parents[0] must be -1");
+    for (int i = 1; i < J; i++) {
+        if (parents_host[i] < 0 || parents_host[i] >= i)
+            return api_fail(GSR_ERR_ARG, "gsr_lbs: parents must satisfy 0 <= parents[i] < i");
+        par.p[i] = (int8_t)parents_host[i];
+    }
+    hipStream_t s = (hipStream_t)stream;
+    LbsArena a;
+    carve_lbs(workspace, B, V, J, &a);
+    float* vs = v_shaped ? v_shaped : a.vs;
+    float* jr = joints ? joints : a.joints;
+    float* A = joint_transforms ? joint_transforms : a.A;
+    const int NP = (J - 1) * 9;
+    const int M = V * 3;
+
+    hipLaunchKernelGGL(k_lbs_rodrigues, dim3((B * J + 255) / 256), dim3(256), 0, s, B, J, pose,
+                       pose2rot, a.rot, a.feat);
+    if (int rc = hip_check("lbs_rodrigues")) return rc;
+    const size_t lds = sizeof(float) * (size_t)(NB + NP) * kLbsFrames;
+    if (lds > 160 * 1024) return api_fail(GSR_ERR_ARG, "gsr_lbs: NB + 9(J-1) too large for LDS");
+    hipLaunchKernelGGL(k_lbs_blend, dim3((M + 255) / 256, (B + kLbsFrames - 1) / kLbsFrames), dim3(256),
+                       lds, s, B, M, NB, NP, v_template, v_template_stride, betas, shapedirs_t,
+                       a.feat, posedirs, vs, a.vp);
+    if (int rc = hip_check("lbs_blend")) return rc;
+    hipLaunchKernelGGL(k_lbs_joints, dim3(J, B), dim3(256), 0, s, V, J, J_regressor, vs,
+                       joints_offset, jr);
+    if (int rc = hip_check("lbs_joints")) return rc;
+    hipLaunchKernelGGL(k_lbs_chain, dim3(B), dim3(64), 0, s, J, par, a.rot, jr, joints_transformed, A);
+    if (int rc = hip_check("lbs_chain")) return rc;
+    hipLaunchKernelGGL(k_lbs_skin, dim3((V + 255) / 256, B), dim3(256), 0, s, V, J, lbs_weights_t, A,
+                       a.vp, verts, vert_transforms);
+    return hip_check("lbs_skin");
+}
+
+int gsr_deform_gaussians(int B, int V, int F, int N, const float* verts,
+                         const float* vert_transforms, const int32_t* faces,
+                         const float* vtx_rotations, int64_t vtx_rot_stride,
+                         const float* vtx_scales, int64_t vtx_scale_stride,
+                         const int32_t* binding_face, const float* face_bary,
+                         const float* local_xyz, int64_t local_stride,
+                         const float* uv_rotations, int64_t uv_rot_stride,
+                         const float* uv_scales, int64_t uv_scale_stride, float* means3D,
+                         float* rotations, float* scales, uint32_t* bad_index_flag, void* stream) {
+    if (B <= 0 || V < 0 || N < 0 || F < 0) return api_fail(GSR_ERR_ARG, "gsr_deform_gaussians: bad sizes");
+    if (V + N == 0) return 0;
+    if (!verts || !means3D || !rotations || !scales)
+        return api_fail(GSR_ERR_ARG, "gsr_deform_gaussians: null required pointer");
+    if (V > 0 && (!vert_transforms || !vtx_rotations || !vtx_scales))
+        return api_fail(GSR_ERR_ARG, "gsr_deform_gaussians: vertex Gaussians need transforms, rotations, scales");
+    if (N > 0 && (!faces || !binding_face || !face_bary || !local_xyz || !uv_rotations || !uv_scales))
+        return api_fail(GSR_ERR_ARG, "gsr_deform_gaussians: UV Gaussians need faces and binding data");
+    auto bad_stride = [](int64_t st, int64_t full) { return st != 0 && st != full; };
+    if (bad_stride(vtx_rot_stride, 4LL * V) || bad_stride(vtx_scale_stride, 3LL * V) ||
+        bad_stride(local_stride, 3LL * N) || bad_stride(uv_rot_stride, 4LL * N) ||
+        bad_stride(uv_scale_stride, 3LL * N))
+        return api_fail(GSR_ERR_ARG, "gsr_deform_gaussians: strides must be 0 or a whole frame");
+    const int P = V + N;
+    hipLaunchKernelGGL(k_deform_gaussians, dim3((P + 255) / 256, B), dim3(256), 0, (hipStream_t)stream,
+                       V, F, N, verts, vert_transforms, faces, vtx_rotations, vtx_rot_stride, vtx_scales,
+                       vtx_scale_stride, binding_face, face_bary, local_xyz, local_stride, uv_rotations,
+                       uv_rot_stride, uv_scales, uv_scale_stride, means3D, rotations, scales,
+                       bad_index_flag);
+    return hip_check("deform_gaussians");
+}
+
+}  // extern "C"

@@ -156,6 +156,9 @@ struct Grads {
     float* dL_drot;              // [B][P][4] or null
 };
 
+// Records `msg` for gsr_last_error() and returns -status (capi.hip).
+int api_fail(int status, const char* msg);
+
 // Workgroups for a persistent (work-queue) launch: CUs of the current device x per_cu.
 int persistent_grid(int per_cu);
 

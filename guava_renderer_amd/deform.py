@@ -1,0 +1,204 @@
+"""Per-frame avatar deformation on the GPU (C ABI include/gsr_deform.h, csrc/deform.hip).
+
+Host-side mirror of the reference's deformation API, so GUAVA's callers keep their call shapes:
+
+  lbs(betas, pose, v_template, shapedirs, posedirs, J_regressor, parents, lbs_weights,
+      joints_offset=None, pose2rot=True, dtype)          -> (verts, J_transformed)
+                                                         models/modules/flame/lbs.py:142-229
+  lbs_wobeta(pose, v_shaped, posedirs, J_regressor, parents, lbs_weights, joints_offset=None,
+             pose2rot=True, dtype)                       -> (verts, J_transformed, J, T, A)
+                                                         lbs.py:255-333
+  GaussianDeformer(vertex_gaussian_assets, uv_gaussian_assets, faces).forward(verts, T)
+                                                         -> the deformed_assets dict of
+                                                         Ubody_Gaussian.forward
+                                                         (UbodyAvatar/ubody_gaussian.py:245-289)
+
+Every call runs the gfx950 kernels on the current HIP stream of the inputs' device; there is no
+CPU path (CPU tensors raise).  The k-major operand layouts the kernels want (shapedirs, lbs_weights
+transposed) are made once per asset tensor and cached.
+"""
+import ctypes
+
+import numpy as np
+import torch
+
+from . import _lib
+
+_T_CACHE = {}
+
+
+def _dev_check(*ts):
+    for t in ts:
+        if t is not None and not t.is_cuda:
+            raise RuntimeError("guava_renderer_amd.deform runs on the GPU only (got a CPU tensor)")
+
+
+def _f32(t):
+    return t.detach().to(torch.float32).contiguous()
+
+
+def _cached_t(t, fn):
+    """fn(t) cached on the tensor's identity and version (asset tensors are static)."""
+    key = (t.data_ptr(), tuple(t.shape), t._version, fn.__name__)
+    hit = _T_CACHE.get(key)
+    if hit is None:
+        if len(_T_CACHE) > 16:
+            _T_CACHE.clear()
+        hit = fn(t)
+        _T_CACHE[key] = hit
+    return hit
+
+
+def _shapedirs_t(sd):  # [V,3,NB] -> [NB, V*3]
+    return _f32(sd).permute(2, 0, 1).reshape(sd.shape[2], -1).contiguous()
+
+
+def _weights_t(w):  # [V,J] -> [J,V]
+    return _f32(w).t().contiguous()
+
+
+def _ptr(t):
+    return ctypes.c_void_p(t.data_ptr()) if t is not None else None
+
+
+def _stream(dev):
+    return ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
+
+
+def _parents_host(parents):
+    p = parents.detach().cpu().numpy() if torch.is_tensor(parents) else np.asarray(parents)
+    return np.ascontiguousarray(p.astype(np.int32))
+
+
+def _run_lbs(betas, pose, v_template, shapedirs, posedirs, J_regressor, parents, lbs_weights,
+             joints_offset, pose2rot, want_all):
+    _dev_check(pose, v_template, posedirs, J_regressor, lbs_weights, betas, shapedirs, joints_offset)
+    dev = v_template.device
+    B = pose.shape[0] if betas is None else max(betas.shape[0], pose.shape[0])
+    Jn = J_regressor.shape[0]
+    V = J_regressor.shape[1]
+    if v_template.shape[-2:] != (V, 3):
+        raise RuntimeError(f"v_template must be [.., {V}, 3], got {tuple(v_template.shape)}")
+    if lbs_weights.shape != (V, Jn):
+        raise RuntimeError(f"lbs_weights must be [{V}, {Jn}], got {tuple(lbs_weights.shape)}")
+    vt = _f32(v_template)
+    if vt.dim() == 3 and vt.shape[0] == 1 and B > 1:
+        vt = vt[0]
+    vt_stride = 0 if vt.dim() == 2 else V * 3
+    if vt.dim() == 3 and vt.shape[0] != B:
+        raise RuntimeError("v_template batch does not match the pose batch")
+    pose = _f32(pose)
+    if pose2rot:
+        if pose.numel() != B * Jn * 3:
+            raise RuntimeError(f"pose must hold B*J*3 = {B * Jn * 3} axis-angle values")
+    elif pose.numel() != B * Jn * 9:
+        raise RuntimeError(f"pose must hold B*J*9 = {B * Jn * 9} rotation-matrix values")
+    NB = 0
+    sd = None
+    bt = None
+    if betas is not None:
+        NB = betas.shape[1]
+        if shapedirs.shape != (V, 3, NB):
+            raise RuntimeError(f"shapedirs must be [{V}, 3, {NB}], got {tuple(shapedirs.shape)}")
+        sd = _cached_t(shapedirs, _shapedirs_t)
+        bt = _f32(betas).expand(B, NB).contiguous()
+    if Jn > 1 and posedirs.shape != (9 * (Jn - 1), 3 * V):
+        raise RuntimeError(f"posedirs must be [{9 * (Jn - 1)}, {3 * V}], got {tuple(posedirs.shape)}")
+    pd = _f32(posedirs)
+    jreg = _f32(J_regressor)
+    wt = _cached_t(lbs_weights, _weights_t)
+    jo = _f32(joints_offset).expand(B, Jn, 3).contiguous() if joints_offset is not None else None
+    par = _parents_host(parents)
+    o = dict(dtype=torch.float32, device=dev)
+    verts = torch.empty((B, V, 3), **o)
+    jt = torch.empty((B, Jn, 3), **o)
+    jr = torch.empty((B, Jn, 3), **o) if want_all else None
+    T = torch.empty((B, V, 4, 4), **o) if want_all else None
+    A = torch.empty((B, Jn, 4, 4), **o) if want_all else None
+    L = _lib.load()
+    ws = torch.empty((L.gsr_lbs_workspace_bytes(B, V, Jn, NB),), dtype=torch.uint8, device=dev)
+    rc = L.gsr_lbs(B, V, Jn, NB, _ptr(vt), vt_stride, _ptr(bt), _ptr(sd), _ptr(pose),
+                   1 if pose2rot else 0, _ptr(pd), _ptr(jreg),
+                   par.ctypes.data_as(ctypes.c_void_p), _ptr(wt), _ptr(jo), _ptr(verts), _ptr(jt),
+                   _ptr(jr), _ptr(T), _ptr(A), None, _ptr(ws), _stream(dev))
+    _lib.check(rc, "gsr_lbs")
+    return verts, jt, jr, T, A
+
+
+def lbs(betas, pose, v_template, shapedirs, posedirs, J_regressor, parents, lbs_weights,
+        joints_offset=None, pose2rot=True, dtype=torch.float32):
+    """lbs.py:142-229 on the GPU: (verts [B,V,3], J_transformed [B,J,3])."""
+    verts, jt, _, _, _ = _run_lbs(betas, pose, v_template, shapedirs, posedirs, J_regressor,
+                                  parents, lbs_weights, joints_offset, pose2rot, False)
+    return verts, jt
+
+
+def lbs_wobeta(pose, v_shaped, posedirs, J_regressor, parents, lbs_weights, joints_offset=None,
+               pose2rot=True, dtype=torch.float32):
+    """lbs.py:255-333 on the GPU: (verts, J_transformed, J, T [B,V,4,4], A [B,J,4,4])."""
+    return _run_lbs(None, pose, v_shaped, None, posedirs, J_regressor, parents, lbs_weights,
+                    joints_offset, pose2rot, True)
+
+
+class GaussianDeformer:
+    """The Gaussian half of Ubody_Gaussian (ubody_gaussian.py:162-289) over precomputed LBS output.
+
+    vertex_gaussian_assets: dict with 'rotations' [V,4] or [1,V,4] wxyz, 'scales', 'opacities',
+    'colors' (the reference's vertex_gaussian_assets keys, :169-173); uv_gaussian_assets: 'rotations',
+    'scales', 'opacities', 'local_pos', 'binding_face' [N], 'face_bary' [N,3], 'colors' (:175-185).
+    The RGB sigmoid of :186-187 is applied once here, as the reference's constructor does."""
+
+    def __init__(self, vertex_gaussian_assets, uv_gaussian_assets, faces, sh_degree=0,
+                 apply_rgb_sigmoid=True):
+        va, ua = vertex_gaussian_assets, uv_gaussian_assets
+
+        def sq(t):
+            t = t.detach()
+            return _f32(t[0] if t.dim() == 3 and t.shape[0] == 1 else t)
+
+        _dev_check(faces, va["rotations"], ua["rotations"])
+        self.faces = faces.detach().to(torch.int32).contiguous()
+        self.v_rot, self.v_scale = sq(va["rotations"]), sq(va["scales"])
+        self.u_rot, self.u_scale = sq(ua["rotations"]), sq(ua["scales"])
+        self.u_local = sq(ua["local_pos"])
+        self.bind = ua["binding_face"].detach().reshape(-1).to(torch.int32).contiguous()
+        self.bary = _f32(ua["face_bary"].detach().reshape(-1, 3))
+        self.V, self.N = self.v_rot.shape[0], self.u_rot.shape[0]
+        col = torch.cat([sq(va["colors"]), sq(ua["colors"])], 0)
+        if apply_rgb_sigmoid:
+            col[:, :3] = torch.sigmoid(col[:, :3])
+        self.colors = col.contiguous()
+        self.opacity = torch.cat([sq(va["opacities"]), sq(ua["opacities"])], 0).contiguous()
+        self.sh_degree = sh_degree
+        self.bad = torch.zeros(1, dtype=torch.int32, device=self.faces.device)
+
+    def forward(self, verts, vert_transforms):
+        """verts [B,V,3], vert_transforms [B,V,4,4] (EHM's vertices / ver_transform_mat) ->
+        deformed_assets dict of Ubody_Gaussian.forward (ubody_gaussian.py:279-289)."""
+        _dev_check(verts, vert_transforms)
+        B, V = verts.shape[:2]
+        if V != self.V:
+            raise RuntimeError(f"expected {self.V} vertices, got {V}")
+        P = self.V + self.N
+        dev = verts.device
+        o = dict(dtype=torch.float32, device=dev)
+        xyz = torch.empty((B, P, 3), **o)
+        rot = torch.empty((B, P, 4), **o)
+        scl = torch.empty((B, P, 3), **o)
+        verts = _f32(verts)
+        vt = _f32(vert_transforms)
+        rc = _lib.load().gsr_deform_gaussians(
+            B, V, self.faces.shape[0], self.N, _ptr(verts), _ptr(vt), _ptr(self.faces),
+            _ptr(self.v_rot), 0, _ptr(self.v_scale), 0, _ptr(self.bind), _ptr(self.bary),
+            _ptr(self.u_local), 0, _ptr(self.u_rot), 0, _ptr(self.u_scale), 0, _ptr(xyz), _ptr(rot),
+            _ptr(scl), _ptr(self.bad), _stream(dev))
+        _lib.check(rc, "gsr_deform_gaussians")
+        return {"features_color": self.colors.expand(B, -1, -1), "xyz": xyz, "rotation": rot,
+                "scaling": scl, "opacity": self.opacity.expand(B, -1, -1),
+                "sh_degree": self.sh_degree, "smplx_xyz_deform": verts}
+
+    __call__ = forward
+
+    def bad_index(self):
+        """True if any binding-face / face-vertex index was out of range (synchronises)."""
+        return bool(self.bad.item())

@@ -1,0 +1,85 @@
+/*
+ * gsr_deform.h -- C ABI of the MI355X (gfx950) per-frame avatar deformation that feeds the
+ * rasterizer.
+ *
+ * Each entry point replaces one function of the reference's torch code
+ * (/root/reference/models/...):
+ *
+ *   gsr_lbs              <- lbs()                      modules/flame/lbs.py:142-229 (betas != NULL)
+ *                           lbs_wobeta()               modules/flame/lbs.py:255-333 (betas == NULL)
+ *                           with blend_shapes :355-376, vertices2joints :335-352,
+ *                           batch_rodrigues :379-410, batch_rigid_transform :426-482 fused in.
+ *                           Used by EHM.forward (modules/ehm/EHM.py:67-70 FLAME head,
+ *                           :134-137 SMPL-X body).
+ *   gsr_deform_gaussians <- the Gaussian part of Ubody_Gaussian.forward
+ *                           UbodyAvatar/ubody_gaussian.py:252-278: vertex Gaussians
+ *                           (rotmat_to_unitquat of the per-vertex skinning matrix, quat_product,
+ *                           normalize) and UV Gaussians (compute_face_orientation,
+ *                           utils/graphics_utils.py:61-80, face binding, barycentric centre,
+ *                           face-scaled local offset and scale), concatenated vertex-first.
+ *
+ * Conventions: device pointers, float32, the reference's layouts unless stated.  Two operands are
+ * taken k-major (transposed once at avatar load, so the per-frame kernels read them coalesced):
+ *   shapedirs_t   [NB, V*3]  = the reference's shapedirs [V,3,NB] permuted to (NB, V, 3)
+ *   lbs_weights_t [J, V]     = the reference's lbs_weights [V,J] transposed
+ * posedirs keeps the reference layout [(J-1)*9, V*3] (already k-major).  `parents` is a HOST array
+ * of J int32 with parents[0] = -1 and 0 <= parents[i] < i (the order batch_rigid_transform walks).
+ * Per-frame tensors with a `_stride` argument are [B, n, k] when the stride is n*k and shared by
+ * every frame ([n, k]) when it is 0.  Return codes: 0 = success, < 0 = -gsr_status
+ * (gsr_last_error() explains).
+ */
+#ifndef GSR_DEFORM_H
+#define GSR_DEFORM_H
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define GSR_LBS_MAX_JOINTS 64
+
+/* Scratch bytes for gsr_lbs (rotation matrices, pose features, v_shaped, v_posed, rest joints,
+ * joint transforms of B frames). */
+size_t gsr_lbs_workspace_bytes(int B, int V, int J, int NB);
+
+/* lbs / lbs_wobeta for B frames.
+ *   v_template [V,3] (stride 0) or [B,V,3] (stride V*3); for lbs_wobeta this is v_shaped.
+ *   betas [B,NB] + shapedirs_t [NB,V*3], or betas == NULL (NB ignored): lbs_wobeta.
+ *   pose: pose2rot != 0 -> [B,J,3] axis-angle (batch_rodrigues); 0 -> [B,J,9] rotation matrices.
+ *   joints_offset [B,J,3] or NULL (added to the regressed joints, lbs.py:191/:295).
+ * Outputs (each may be NULL except verts):
+ *   verts [B,V,3]; joints_transformed [B,J,3] (posed joints); joints [B,J,3] (rest joints incl.
+ *   offset, lbs_wobeta's J); vert_transforms [B,V,16] (row-major 4x4, EHM's ver_transform_mat);
+ *   joint_transforms [B,J,16] (A, joint_transform_mat); v_shaped [B,V,3]. */
+int gsr_lbs(int B, int V, int J, int NB, const float* v_template, int64_t v_template_stride,
+            const float* betas, const float* shapedirs_t, const float* pose, int pose2rot,
+            const float* posedirs, const float* J_regressor, const int32_t* parents_host,
+            const float* lbs_weights_t, const float* joints_offset, float* verts,
+            float* joints_transformed, float* joints, float* vert_transforms,
+            float* joint_transforms, float* v_shaped, char* workspace, void* stream);
+
+/* Ubody_Gaussian.forward's Gaussian assembly for B frames; P = V + N Gaussians per frame, the V
+ * vertex Gaussians first.
+ *   verts [B,V,3], vert_transforms [B,V,16] (from gsr_lbs), faces [F,3] int32.
+ *   vertex Gaussians: rotations [V,4] wxyz and scales [V,3] (with strides: shared or per frame).
+ *   UV Gaussians: binding_face [N] int32 in [0,F), face_bary [N,3], local_xyz [N,3],
+ *   rotations [N,4] wxyz, scales [N,3] (local/rot/scale with strides).
+ * Outputs: means3D [B,P,3], rotations [B,P,4] wxyz, scales [B,P,3].  Indices are validated on the
+ * device: an out-of-range binding face or face-vertex index ORs 1 into *bad_index_flag (a device
+ * uint32, may be NULL) and writes NaN for that Gaussian instead of reading out of range (the
+ * reference raises IndexError). */
+int gsr_deform_gaussians(int B, int V, int F, int N, const float* verts,
+                         const float* vert_transforms, const int32_t* faces,
+                         const float* vtx_rotations, int64_t vtx_rot_stride,
+                         const float* vtx_scales, int64_t vtx_scale_stride,
+                         const int32_t* binding_face, const float* face_bary,
+                         const float* local_xyz, int64_t local_stride,
+                         const float* uv_rotations, int64_t uv_rot_stride,
+                         const float* uv_scales, int64_t uv_scale_stride, float* means3D,
+                         float* rotations, float* scales, uint32_t* bad_index_flag, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

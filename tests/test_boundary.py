@@ -1,5 +1,5 @@
 """CPU tests of the drop-in boundary: the C ABI library loads and exports every symbol declared in
-include/gsr.h, the Python mirror keeps the reference's signatures and error behaviour
+include/*.h, the Python mirror keeps the reference's signatures and error behaviour
 (diff_gaussian_rasterization_32/__init__.py:143-207, rasterize_points.cu:58-60), and there is no
 CPU fallback (GPU-less calls with P > 0 raise)."""
 import inspect
@@ -16,8 +16,11 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 def test_library_exports_every_header_symbol():
     from guava_renderer_amd import _lib
     L = _lib.load()
-    hdr = open(os.path.join(ROOT, "include", "gsr.h")).read()
-    declared = set(re.findall(r"^\s*(?:const\s+)?[a-z_0-9]+\*?\s+\**(gsr_[a-z_0-9]+)\s*\(", hdr, re.M))
+    declared = set()
+    for h in sorted(os.listdir(os.path.join(ROOT, "include"))):
+        if h.endswith(".h"):
+            hdr = open(os.path.join(ROOT, "include", h)).read()
+            declared |= set(re.findall(r"^\s*(?:const\s+)?[a-z_0-9]+\*?\s+\**(gsr_[a-z_0-9]+)\s*\(", hdr, re.M))
     assert declared, "no declarations parsed"
     assert declared <= set(_lib.EXPORTS), declared - set(_lib.EXPORTS)
     for sym in declared:
@@ -120,3 +123,25 @@ def test_scene_generators_shapes():
     # canonical camera: R = I, t = (0, 0.6, 22) (data_loader.py:377-394), row-vector view matrix
     np.testing.assert_allclose(cam["viewmatrix"][3, :3], [0, 0.6, 22])
     assert cam["projmatrix"].dtype == np.float32
+
+
+def test_deform_abi_validates_before_touching_memory():
+    """gsr_lbs / gsr_deform_gaussians reject bad trees and sizes on the host (no launch)."""
+    import ctypes
+    from guava_renderer_amd import _lib, deform
+    L = _lib.load()
+    bogus = ctypes.c_void_p(16)  # never dereferenced: validation fails first
+    bad_par = (ctypes.c_int32 * 3)(-1, 2, 1)  # parents[1] = 2 >= 1
+    rc = L.gsr_lbs(1, 4, 3, 0, bogus, 0, None, None, bogus, 1, bogus, bogus,
+                   ctypes.cast(bad_par, ctypes.c_void_p), bogus, None, bogus, None, None, None,
+                   None, None, bogus, None)
+    assert rc == -1 and b"parents" in L.gsr_last_error()
+    rc = L.gsr_lbs(1, 4, 65, 0, bogus, 0, None, None, bogus, 1, bogus, bogus, bogus, bogus, None,
+                   bogus, None, None, None, None, None, bogus, None)
+    assert rc == -1 and b"J must be" in L.gsr_last_error()
+    rc = L.gsr_deform_gaussians(1, 4, 2, 3, bogus, bogus, None, bogus, 0, bogus, 0, None, None, None,
+                                0, None, 0, None, 0, bogus, bogus, bogus, None, None)
+    assert rc == -1 and b"UV Gaussians" in L.gsr_last_error()
+    with pytest.raises(RuntimeError, match="GPU only"):
+        deform.lbs_wobeta(torch.zeros(1, 3, 3), torch.zeros(1, 4, 3), torch.zeros(18, 12),
+                          torch.zeros(3, 4), torch.tensor([-1, 0, 1]), torch.zeros(4, 3))

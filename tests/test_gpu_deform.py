@@ -1,0 +1,137 @@
+"""GPU parity of the deformation path (csrc/deform.hip via include/gsr_deform.h) against the CPU
+oracle (oracle/lbs_oracle.py, itself pinned to the reference's lbs.py in test_lbs_oracle.py).
+
+Tolerances (float32 GPU vs float64 oracle):
+  vertices, joints, transforms  2e-5 absolute (coordinates are O(1))
+  Gaussian means / scales       2e-5 absolute
+  quaternions                   2e-5 absolute up to sign, on Gaussians whose rotmat_to_unitquat
+                                decision margin is >= 1e-4 (below it float32 may take another
+                                branch of the decision scheme, which the test counts separately)
+Indices (faces, binding faces) are integers: the gathered vertices must be the oracle's exactly,
+which the 2e-5 bound on UV means checks.
+"""
+import os
+import sys
+
+import numpy as np
+import pytest
+import torch
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(HERE, "golden"))
+import lbs_cases  # noqa: E402
+import lbs_oracle as lo  # noqa: E402
+
+pytestmark = pytest.mark.gpu
+ATOL = 2e-5
+DEV = "cuda:0"
+
+
+def _t(x):
+    return torch.from_numpy(np.ascontiguousarray(x)).to(DEV) if x is not None else None
+
+
+def _gpu_wobeta(c):
+    from guava_renderer_amd import deform
+    out = deform.lbs_wobeta(_t(c["pose"]), _t(c["v_shaped"]), _t(c["posedirs"]), _t(c["J_regressor"]),
+                            torch.from_numpy(c["parents"]), _t(c["lbs_weights"]),
+                            joints_offset=_t(c["joints_offset"]), pose2rot=c["pose2rot"])
+    return [o.cpu().numpy() for o in out]
+
+
+@pytest.mark.parametrize("name", ["smplx_wobeta", "smplx_rotmat"])
+def test_lbs_wobeta_golden_cases(name):
+    c = lbs_cases.all_cases()[name]
+    got = _gpu_wobeta(c)
+    ref = lo.lbs_wobeta(c["pose"], c["v_shaped"], c["posedirs"], c["J_regressor"], c["parents"],
+                        c["lbs_weights"], c["joints_offset"], c["pose2rot"])
+    for key, g, r in zip(("verts", "J_transformed", "J", "T", "A"), got, ref):
+        np.testing.assert_allclose(g, r, atol=ATOL, rtol=0, err_msg=key)
+
+
+def test_lbs_with_betas_golden_case():
+    from guava_renderer_amd import deform
+    c = lbs_cases.all_cases()["flame_lbs"]
+    verts, jt = deform.lbs(_t(c["betas"]), _t(c["pose"]), _t(c["v_template"]), _t(c["shapedirs"]),
+                           _t(c["posedirs"]), _t(c["J_regressor"]), torch.from_numpy(c["parents"]),
+                           _t(c["lbs_weights"]))
+    r_verts, r_jt, *_ = lo.lbs(c["betas"], c["pose"], c["v_template"], c["shapedirs"], c["posedirs"],
+                               c["J_regressor"], c["parents"], c["lbs_weights"])
+    np.testing.assert_allclose(verts.cpu().numpy(), r_verts, atol=ATOL, rtol=0)
+    np.testing.assert_allclose(jt.cpu().numpy(), r_jt, atol=ATOL, rtol=0)
+
+
+def _full_avatar(B=4, P=40000):
+    from guava_renderer_amd import avatar
+    verts, faces, tex = avatar.template_mesh()
+    m = avatar.lbs_model(verts, J=55, NB=350, seed=0)
+    g = avatar.gaussians(verts, faces, tex, P=P, seed=0)
+    rng = np.random.default_rng(7)
+    betas = rng.normal(size=(B, 350)).astype(np.float32)
+    pose = avatar.random_pose(B, seed=1000)
+    return m, g, faces, betas, pose
+
+
+def test_full_smplx_lbs_and_gaussian_assembly():
+    """SMPL-X size (V=10,475, J=55, NB=350 shape+expression), B=4 frames: lbs -> Gaussians."""
+    from guava_renderer_amd import deform
+    m, g, faces, betas, pose = _full_avatar()
+    B = betas.shape[0]
+    # body LBS with betas (EHM.forward = blend_shapes + lbs_wobeta, EHM.py:115,134-137)
+    verts, jt = deform.lbs(_t(betas), _t(pose), _t(m["v_template"]), _t(m["shapedirs"]), _t(m["posedirs"]),
+                           _t(m["J_regressor"]), torch.from_numpy(m["parents"]), _t(m["lbs_weights"]))
+    r_verts, r_jt, r_J, r_T, r_A, r_vs = lo.lbs(betas, pose, m["v_template"], m["shapedirs"], m["posedirs"],
+                                                m["J_regressor"], m["parents"], m["lbs_weights"])
+    np.testing.assert_allclose(verts.cpu().numpy(), r_verts, atol=ATOL, rtol=0)
+    np.testing.assert_allclose(jt.cpu().numpy(), r_jt, atol=ATOL, rtol=0)
+    # vertex transforms from lbs_wobeta on the oracle's v_shaped
+    v2, jt2, J2, T2, A2 = deform.lbs_wobeta(_t(pose), _t(r_vs.astype(np.float32)), _t(m["posedirs"]),
+                                            _t(m["J_regressor"]), torch.from_numpy(m["parents"]),
+                                            _t(m["lbs_weights"]))
+    np.testing.assert_allclose(T2.cpu().numpy(), r_T, atol=ATOL, rtol=0)
+    np.testing.assert_allclose(A2.cpu().numpy(), r_A, atol=ATOL, rtol=0)
+
+    dfm = deform.GaussianDeformer(
+        {"rotations": _t(g["vtx_rotations"]), "scales": _t(g["vtx_scales"]),
+         "opacities": _t(g["opacities"][:10475]), "colors": _t(g["colors"][:10475])},
+        {"rotations": _t(g["uv_rotations"]), "scales": _t(g["uv_scales"]),
+         "opacities": _t(g["opacities"][10475:]), "colors": _t(g["colors"][10475:]),
+         "local_pos": _t(g["local_xyz"]), "binding_face": _t(g["binding_face"]),
+         "face_bary": _t(g["face_bary"])}, _t(faces))
+    out = dfm(v2, T2)
+    assert not dfm.bad_index()
+    ref = lo.deform_gaussians(v2.cpu().numpy(), T2.cpu().numpy(), faces, g["vtx_rotations"],
+                              g["vtx_scales"], g["binding_face"], g["face_bary"], g["local_xyz"],
+                              g["uv_rotations"], g["uv_scales"])
+    np.testing.assert_allclose(out["xyz"].cpu().numpy(), ref["xyz"], atol=ATOL, rtol=0)
+    np.testing.assert_allclose(out["scaling"].cpu().numpy(), ref["scaling"], atol=ATOL, rtol=0)
+    q, rq = out["rotation"].cpu().numpy(), ref["rotation"]
+    err = np.minimum(np.abs(q - rq).max(-1), np.abs(q + rq).max(-1))
+    firm = ref["margin"] >= 1e-4
+    assert firm.mean() > 0.99
+    assert err[firm].max() < ATOL, err[firm].max()
+    assert out["opacity"].shape == (B, 40000, 1) and out["features_color"].shape == (B, 40000, 32)
+
+
+def test_bad_binding_index_is_flagged_not_faulted():
+    from guava_renderer_amd import deform
+    rng = np.random.default_rng(0)
+    V, F, N = 30, 20, 64
+    faces = np.stack([rng.choice(V, 3, replace=False) for _ in range(F)]).astype(np.int32)
+    bind = rng.integers(0, F, N).astype(np.int32)
+    bind[5] = F + 7  # out of range
+    q = np.tile(np.array([1, 0, 0, 0], np.float32), (N, 1))
+    dfm = deform.GaussianDeformer(
+        {"rotations": _t(np.tile(np.array([1, 0, 0, 0], np.float32), (V, 1))),
+         "scales": _t(np.ones((V, 3), np.float32)), "opacities": _t(np.ones((V, 1), np.float32)),
+         "colors": _t(np.zeros((V, 32), np.float32))},
+        {"rotations": _t(q), "scales": _t(np.ones((N, 3), np.float32)),
+         "opacities": _t(np.ones((N, 1), np.float32)), "colors": _t(np.zeros((N, 32), np.float32)),
+         "local_pos": _t(np.zeros((N, 3), np.float32)), "binding_face": _t(bind),
+         "face_bary": _t(np.full((N, 3), 1 / 3, np.float32))}, _t(faces))
+    verts = _t(rng.normal(size=(1, V, 3)).astype(np.float32))
+    T = _t(np.broadcast_to(np.eye(4, dtype=np.float32), (1, V, 4, 4)))
+    out = dfm(verts, T)
+    assert dfm.bad_index()
+    xyz = out["xyz"].cpu().numpy()
+    assert np.isnan(xyz[0, V + 5]).all() and np.isfinite(np.delete(xyz[0], V + 5, 0)).all()
