@@ -1,10 +1,14 @@
 #!/usr/bin/env python
 """Headline benchmark: rendered frames/sec at 512x512 with ~100k Gaussians (BASELINE.json).
 
-One step = one pass of the rasterizer hot path (preprocess -> tile binning -> per-tile depth
-sort -> 32-channel front-to-back compositing) over a batch of `--batch` frames of the synthetic
-GUAVA-like avatar (config 2: P=100,000 Gaussians, 512x512, one camera per frame), with every
-input resident in HBM before the timed region.  N GPUs: one process per GPU, each renders its
+One step = one pass of GUAVA's per-frame animation path over a batch of `--batch` tracked frames
+(config 2 "self-reenactment": main/test.py:70-76 times Ubody_Gaussian.forward + render per frame):
+  --pipeline avatar (default): EHM deformation (FLAME head LBS + SMPL-X body LBS, per-frame pose,
+      expression, eyelids), vertex + UV Gaussian assembly, then the rasterizer hot path
+      (preprocess -> tile binning -> per-tile depth order -> 32-channel compositing);
+  --pipeline raster: the rasterizer alone over one static cloud seen by a camera per frame.
+Synthetic avatar: P=100,000 Gaussians (10,475 SMPL-X vertex Gaussians + UV Gaussians), 512x512,
+one camera and one pose per frame; every input resident in HBM before the timed region.  N GPUs: one process per GPU, each renders its
 own `--batch` frames (frames are independent -> weak scaling, no collective in the data path;
 torch.distributed is used only for the barrier and the max-over-ranks time).
 
@@ -37,6 +41,7 @@ def _args():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--batch", type=int, default=32, help="frames per step per GPU")
     ap.add_argument("--config", default="c2", choices=["c2", "c5"])
+    ap.add_argument("--pipeline", default="avatar", choices=["avatar", "raster"])
     ap.add_argument("--fast-exp", action="store_true", help="hardware exp (not bit-exact)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -62,19 +67,33 @@ def _path_alg_bytes(P, W, H):
     return 176.0 * P + 132.0 * W * H
 
 
-def cpu_baseline(scene, cams, W, H, budget_s):
+def cpu_baseline(scene, cams, W, H, budget_s, avatar_inputs=None):
+    """The CPU oracle timed on a bounded sample of the same workload (rank 0, N=1)."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle  # CPU restatement of the reference algorithm (checker / baseline only)
+    import lbs_oracle  # CPU restatement of the deformation (numpy)
     threads = max(1, min(16, os.cpu_count() or 1))
     oracle.set_threads(threads)
     bg = np.zeros(C, np.float32)
     t0 = time.perf_counter()
     frames = 0
     while True:
-        cam = cams[frames % len(cams)]
-        oracle.forward(scene["means3D"], scene["colors"], scene["opacities"], scene["scales"],
-                       scene["rotations"], None, cam["viewmatrix"], cam["projmatrix"], W, H,
-                       cam["tanfovx"], cam["tanfovy"], bg)
+        i = frames % len(cams)
+        cam = cams[i]
+        means, rots, scales = scene.get("means3D"), scene.get("rotations"), scene.get("scales")
+        if avatar_inputs is not None:  # deform this frame on the CPU too
+            body, flame, extra, g, bp, fp = avatar_inputs
+            one = lambda d: {k: v[i:i + 1] for k, v in d.items()}  # noqa: E731
+            e = lbs_oracle.ehm_forward(body, flame, extra, one(bp), one(fp))
+            dg = lbs_oracle.deform_gaussians(e["vertices"], e["ver_transform_mat"], extra["faces"],
+                                             g["vtx_rotations"], g["vtx_scales"], g["binding_face"],
+                                             g["face_bary"], g["local_xyz"], g["uv_rotations"],
+                                             g["uv_scales"])
+            means = dg["xyz"][0].astype(np.float32)
+            rots = dg["rotation"][0].astype(np.float32)
+            scales = dg["scaling"][0].astype(np.float32)
+        oracle.forward(means, scene["colors"], scene["opacities"], scales, rots, None,
+                       cam["viewmatrix"], cam["projmatrix"], W, H, cam["tanfovx"], cam["tanfovy"], bg)
         frames += 1
         el = time.perf_counter() - t0
         if el >= budget_s or frames >= 512:
@@ -84,9 +103,11 @@ def cpu_baseline(scene, cams, W, H, budget_s):
         model = next(ln.split(":", 1)[1].strip() for ln in open("/proc/cpuinfo") if ln.startswith("model name"))
     except (OSError, StopIteration):
         pass
+    what = "deform (numpy) + preprocess+bin+sort+render (C)" if avatar_inputs is not None else \
+        "preprocess+bin+sort+render"
     return dict(value=frames / el, unit="frames/s", cores=threads, kind="port",
-                sample=f"{frames} frames of the same {W}x{H} workload through the C oracle "
-                       f"(preprocess+bin+sort+render, OpenMP {threads} threads on {model}) in {el:.1f}s")
+                sample=f"{frames} frames of the same {W}x{H} workload through the CPU oracle "
+                       f"({what}, OpenMP {threads} threads on {model}) in {el:.1f}s")
 
 
 def main():
@@ -109,30 +130,58 @@ def main():
 
     wl = _workload(a.config)
     P, W, H, B = wl["P"], wl["W"], wl["H"], a.batch
-    scene = scenes.avatar_cloud(P, seed=0, gaussians_per_texel=wl["gpt"])
-    P = scene["means3D"].shape[0]
     cams_all = scenes.frame_cameras(B * world, W, H, seed=1000)
     cams = parallel.shard_frames(cams_all, rank, world)  # B frames per rank, no data-path collective
-
     t = lambda x: torch.tensor(np.ascontiguousarray(x), device=dev)  # noqa: E731
-    means, colors = t(scene["means3D"]), t(scene["colors"])
-    opac, scales, rots = t(scene["opacities"]), t(scene["scales"]), t(scene["rotations"])
     views = t(np.stack([c["viewmatrix"].reshape(16) for c in cams]))
     projs = t(np.stack([c["projmatrix"].reshape(16) for c in cams]))
     tanf = t(np.array([[c["tanfovx"], c["tanfovy"]] for c in cams], np.float32))
     bgs = torch.zeros((B, C), dtype=torch.float32, device=dev)
+    avatar_inputs = None
+    workload = wl["name"] + ("-deform+raster" if a.pipeline == "avatar" else "-raster")
 
-    # size the instance capacity from one probe batch
-    probe = BatchRasterizer(B, P, W, H, R_capacity=24 * P * B, device=dev)
-    probe.forward(means, colors, opac, scales, rots, views, projs, tanf, bgs)
-    R_probe, ovf = probe.status()
-    assert not ovf, "probe overflow"
-    del probe
-    torch.cuda.empty_cache()
-    rast = BatchRasterizer(B, P, W, H, R_capacity=int(R_probe * 1.25) + 1024, device=dev)
+    if a.pipeline == "avatar":
+        from guava_renderer_amd import avatar
+        from guava_renderer_amd.pipeline import AvatarPipeline
+        body, flame, extra = avatar.ehm_assets(seed=0)
+        verts, faces, tex = avatar.template_mesh()
+        g = avatar.gaussians(verts, faces, tex, P=P, seed=0)
+        bp_all, fp_all = avatar.ehm_params(B * world, seed=1000)
+        lo, hi = parallel.shard_range(B * world, rank, world)
+        bp = {k: v[lo:hi] for k, v in bp_all.items()}
+        fp = {k: v[lo:hi] for k, v in fp_all.items()}
+        bpt = {k: t(v) for k, v in bp.items()}
+        fpt = {k: t(v) for k, v in fp.items()}
+        probe = AvatarPipeline(body, flame, extra, g, B, W, H, R_capacity=24 * P * B, device=dev)
+        probe.render(bpt, fpt, views, projs, tanf)
+        R_probe, ovf = probe.rast.status()
+        assert not ovf, "probe overflow"
+        del probe
+        torch.cuda.empty_cache()
+        pipe = AvatarPipeline(body, flame, extra, g, B, W, H, R_capacity=int(R_probe * 1.25) + 1024, device=dev)
+        P = pipe.P
+        rast = pipe.rast
+        scene = {"colors": g["colors"], "opacities": g["opacities"]}
+        avatar_inputs = (body, flame, extra, g, bp, fp)
 
-    def step():
-        return rast.forward(means, colors, opac, scales, rots, views, projs, tanf, bgs)
+        def step():
+            return pipe.render(bpt, fpt, views, projs, tanf)
+    else:
+        scene = scenes.avatar_cloud(P, seed=0, gaussians_per_texel=wl["gpt"])
+        P = scene["means3D"].shape[0]
+        means, colors = t(scene["means3D"]), t(scene["colors"])
+        opac, scales, rots = t(scene["opacities"]), t(scene["scales"]), t(scene["rotations"])
+        # size the instance capacity from one probe batch
+        probe = BatchRasterizer(B, P, W, H, R_capacity=24 * P * B, device=dev)
+        probe.forward(means, colors, opac, scales, rots, views, projs, tanf, bgs)
+        R_probe, ovf = probe.status()
+        assert not ovf, "probe overflow"
+        del probe
+        torch.cuda.empty_cache()
+        rast = BatchRasterizer(B, P, W, H, R_capacity=int(R_probe * 1.25) + 1024, device=dev)
+
+        def step():
+            return rast.forward(means, colors, opac, scales, rots, views, projs, tanf, bgs)
 
     for _ in range(a.warmup):
         step()
@@ -155,6 +204,15 @@ def main():
         dist.barrier()
     prof = profile_read()
     profile_enable(())
+    deform_ms = None
+    if a.pipeline == "avatar":  # deformation alone (EHM + Gaussian assembly), outside the timed region
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(a.steps):
+            pipe.deform(bpt, fpt)
+        e1.record()
+        torch.cuda.synchronize(dev)
+        deform_ms = e0.elapsed_time(e1) / a.steps
     # work counters of one extra (instrumented, untimed) step: which wall the render kernel hits
     work = render_counters(step, device=dev)
     R_after, ovf = rast.status()
@@ -176,7 +234,7 @@ def main():
     if os.path.exists(pmc_path):
         try:
             pm = json.load(open(pmc_path))
-            if pm.get("config") == wl["name"] and pm.get("batch") == B:
+            if pm.get("config") == workload and pm.get("batch") == B:
                 traffic = pm.get("hbm_bytes_per_launch")
         except Exception:  # noqa: BLE001
             traffic = None
@@ -194,9 +252,14 @@ def main():
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "f32",
-        "data": "synthetic (SMPL-X-template avatar cloud, GUAVA attribute distributions, "
-                "one orbit camera per frame)",
-        "config": {"workload": wl["name"], "gaussians": P, "image": [W, H], "channels": C,
+        "data": ("synthetic avatar (SMPL-X template mesh + UV-texel Gaussians, synthetic LBS bases, "
+                 "GUAVA attribute distributions), one pose + one orbit camera per frame"
+                 if a.pipeline == "avatar" else
+                 "synthetic (SMPL-X-template avatar cloud, GUAVA attribute distributions, "
+                 "one orbit camera per frame)"),
+        "config": {"workload": workload,
+                   "pipeline": "EHM LBS -> Gaussian assembly -> rasterize" if a.pipeline == "avatar"
+                   else "rasterize", "gaussians": P, "image": [W, H], "channels": C,
                    "frames_per_step_per_gpu": B, "global_batch": B * world,
                    "parallelism": f"frame-sharded x{world}",
                    "exp": "hw" if a.fast_exp else "exact-poly",
@@ -218,10 +281,12 @@ def main():
     out["render_mfma"] = {"issued_tflops": round(mfma_flops / (render_ms * 1e-3) / 1e12, 2) if render_ms else None,
                           "peak_tflops": F32_MFMA_PEAK_TFLOPS,
                           "useful_frac": round(work["pairs_contributing"] / max(64 * work["strip_pairs_blended"], 1), 4)}
+    if deform_ms is not None:
+        out["deform_ms_per_step"] = round(deform_ms, 4)
     if a.stages:
         out["stage_ms_per_step"] = {k: round(v[0] / max(v[1], 1), 4) for k, v in prof.items()}
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
-        out["cpu_baseline"] = cpu_baseline(scene, cams, W, H, a.cpu_seconds)
+        out["cpu_baseline"] = cpu_baseline(scene, cams, W, H, a.cpu_seconds, avatar_inputs)
     if rank == 0:
         print(json.dumps(out), flush=True)
     if dist is not None:

@@ -15,7 +15,8 @@ EXPORTS = ("gsr_version", "gsr_last_error", "gsr_set_exact_exp", "gsr_geometry_b
            "gsr_backward_batch", "gsr_batch_status", "gsr_profile_enable", "gsr_profile_read",
            "gsr_render_counters", "gsr_render_timeline",
            # include/gsr_deform.h
-           "gsr_lbs_workspace_bytes", "gsr_lbs", "gsr_deform_gaussians")
+           "gsr_lbs_workspace_bytes", "gsr_lbs", "gsr_blend_joints", "gsr_splice_head",
+           "gsr_deform_gaussians")
 
 ALLOC_FN = ctypes.CFUNCTYPE(ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t)
 
@@ -94,6 +95,11 @@ def load(path=None):
     L.gsr_lbs.argtypes = [_i, _i, _i, _i, _vp, _i64, _vp, _vp, _vp, _i, _vp, _vp, _vp, _vp, _vp, _vp,
                           _vp, _vp, _vp, _vp, _vp, _vp, _vp]
     L.gsr_lbs.restype = _i
+    L.gsr_blend_joints.argtypes = [_i, _i, _i, _i, _vp, _i64, _vp, _vp, _vp, _vp, _vp, _vp, _vp]
+    L.gsr_blend_joints.restype = _i
+    L.gsr_splice_head.argtypes = [_i, _i, _i, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i, _i, _i, _vp, _i,
+                                  _i, _i, _vp, _vp, _vp]
+    L.gsr_splice_head.restype = _i
     L.gsr_deform_gaussians.argtypes = [_i, _i, _i, _i, _vp, _vp, _vp, _vp, _i64, _vp, _i64, _vp, _vp,
                                        _vp, _i64, _vp, _i64, _vp, _i64, _vp, _vp, _vp, _vp, _vp]
     L.gsr_deform_gaussians.restype = _i

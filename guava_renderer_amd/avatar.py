@@ -45,14 +45,16 @@ def lbs_model(verts, J=55, NB=350, parents=None, seed=0, shape_scale=2e-4, pose_
     V = verts.shape[0]
     parents = SMPLX_PARENTS if parents is None else np.asarray(parents, np.int32)
     assert parents.shape[0] == J
-    # joint centres: J template vertices spread over the mesh (farthest-point order from a seed)
+    # joint centres: a spatially coherent tree -- the root at the vertex nearest the centroid, each
+    # child a random vertex 8-20 cm from its parent joint (so a joint rotation moves nearby skin)
     centres = np.empty((J, 3), np.float32)
-    pick = int(rng.integers(V))
-    dmin = np.full(V, np.inf)
-    for j in range(J):
-        centres[j] = verts[pick]
-        dmin = np.minimum(dmin, ((verts - verts[pick]) ** 2).sum(1))
-        pick = int(np.argmax(dmin))
+    centres[0] = verts[int(np.argmin(((verts - verts.mean(0)) ** 2).sum(1)))]
+    for j in range(1, J):
+        d = np.sqrt(((verts - centres[parents[j]]) ** 2).sum(1))
+        cand = np.nonzero((d > 0.08) & (d < 0.2))[0]
+        if cand.size == 0:
+            cand = np.argsort(d)[: max(1, V // 10)]
+        centres[j] = verts[int(rng.choice(cand))]
     d2 = ((verts[:, None, :] - centres[None]) ** 2).sum(-1)  # V,J
     jreg = np.zeros((J, V), np.float32)
     near_v = np.argsort(d2, axis=0)[:8]  # 8 nearest vertices per joint
@@ -116,3 +118,41 @@ def gaussians(verts, faces, texel_count, P=100000, seed=0):
         uv_scales=np.exp(rng.normal(-0.7, 0.3, (N, 3))).astype(np.float32),
         opacities=np.concatenate([opac(V), opac(N)], 0),
         colors=np.concatenate([feats(V), feats(N)], 0))
+
+
+def ehm_assets(seed=0, n_shape=300, n_exp=50):
+    """SMPL-X body + FLAME head LBS assets wired as EHM (modules/ehm/EHM.py:14-34): the FLAME
+    template is the SMPL-X template's FLAME-mapped region (SMPL-X__FLAME_vertex_ids.npy), the
+    eyelid blend shapes are the reference's flame_{l,r}_eyelid.npy.  Returns (body, flame, extra)."""
+    fx = np.load(scenes._FIXTURE)
+    verts, faces, _ = template_mesh()
+    nb = n_shape + n_exp
+    body = lbs_model(verts, J=55, NB=nb, parents=SMPLX_PARENTS, seed=seed)
+    idx = fx["smplx2flame_ind"].astype(np.int32)
+    flame = lbs_model(verts[idx], J=5, NB=nb, parents=FLAME_PARENTS, seed=seed + 1)
+    # the splice re-anchors the head from FLAME joints 3:5 to body joints 23:25 (EHM.py:123): regress
+    # the body's 23, 24 from the same (mapped) vertices so the head stays on the neck at rest
+    for jb, jh in ((23, 3), (24, 4)):
+        body["J_regressor"][jb] = 0.0
+        np.add.at(body["J_regressor"][jb], idx, flame["J_regressor"][jh])
+    extra = dict(smplx2flame_ind=idx, l_eyelid=fx["l_eyelid"].astype(np.float32),
+                 r_eyelid=fx["r_eyelid"].astype(np.float32), faces=faces)
+    return body, flame, extra
+
+
+def ehm_params(B, seed=1000, n_shape=300, n_exp=50, body_sigma=0.15):
+    """Per-frame EHM inputs (the keys EHM.forward reads, EHM.py:42-91) for B tracked frames: a fixed
+    identity (shape), per-frame expression / jaw / eyes / eyelids / body and hand poses."""
+    rng = np.random.default_rng(seed)
+    shape = np.broadcast_to(rng.normal(0, 1, (1, n_shape)), (B, n_shape)).astype(np.float32)
+    f = lambda *s: rng.normal(0, 1, s).astype(np.float32)  # noqa: E731
+    body = dict(shape=shape.copy(), exp=0.5 * f(B, n_exp),
+                global_pose=0.05 * f(B, 1, 3), body_pose=random_pose(B, J=22, sigma=body_sigma, seed=seed)[:, 1:],
+                left_hand_pose=0.2 * f(B, 15, 3), right_hand_pose=0.2 * f(B, 15, 3),
+                joints_offset=0.002 * f(B, 55, 3),
+                head_scale=(1.0 + 0.02 * f(B, 3)).astype(np.float32))
+    flame = dict(shape_params=shape.copy(), expression_params=0.5 * f(B, n_exp),
+                 pose_params=0.05 * f(B, 3), jaw_params=0.1 * np.abs(f(B, 3)),
+                 eye_pose_params=0.05 * f(B, 6),
+                 eyelid_params=np.clip(0.5 + 0.2 * f(B, 2), 0.0, 1.0).astype(np.float32))
+    return body, flame

@@ -130,6 +130,7 @@ __global__ __launch_bounds__(256) void k_lbs_blend(int B, int M, int NB, int NP,
         acc[4] = fmaf(c1.x, p, acc[4]); acc[5] = fmaf(c1.y, p, acc[5]);
         acc[6] = fmaf(c1.z, p, acc[6]); acc[7] = fmaf(c1.w, p, acc[7]);
     }
+    if (!v_posed) return;  // blend_shapes + joints only (gsr_blend_joints)
 #pragma unroll
     for (int f = 0; f < kLbsFrames; f++)
         if (f < nf) v_posed[(int64_t)(b0 + f) * M + m] = acc[f] + vs[f];
@@ -249,6 +250,39 @@ __global__ __launch_bounds__(256) void k_lbs_skin(int V, int J, const float* __r
         tv[1] = make_float4(T[4], T[5], T[6], T[7]);
         tv[2] = make_float4(T[8], T[9], T[10], T[11]);
         tv[3] = make_float4(T[12], T[13], T[14], T[15]);
+    }
+}
+
+// EHM.forward's head splice (EHM.py:72-75, :121-124): the FLAME head vertices (+ eyelid blend
+// shapes, times head_scale) replace the body template's FLAME-mapped vertices, re-anchored from the
+// mean of head joints [hj0, hj1) to the mean of body joints [bj0, bj1).
+__global__ __launch_bounds__(256) void k_splice_head(
+    int Vb, int Nh, const int32_t* __restrict__ idx, const float* __restrict__ head,
+    const float* __restrict__ r_eyelid, const float* __restrict__ l_eyelid,
+    const float* __restrict__ eyelid, const float* __restrict__ head_scale,
+    const float* __restrict__ hjoints, int Jh, int hj0, int hj1, const float* __restrict__ bjoints,
+    int Jb, int bj0, int bj1, float* __restrict__ body, uint32_t* __restrict__ bad) {
+    const int b = blockIdx.y;
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= Nh) return;
+    const int d = idx[i];
+    if (d < 0 || d >= Vb) {
+        if (bad) atomicOr(bad, 2u);
+        return;
+    }
+    const float* hj = hjoints + (int64_t)b * Jh * 3;
+    const float* bjt = bjoints + (int64_t)b * Jb * 3;
+    for (int c = 0; c < 3; c++) {
+        float h = head[((int64_t)b * Nh + i) * 3 + c];
+        if (eyelid) {
+            h = h + r_eyelid[3 * i + c] * eyelid[2 * b + 1];
+            h = h + l_eyelid[3 * i + c] * eyelid[2 * b];
+        }
+        if (head_scale) h = h * head_scale[3 * b + c];
+        float hs = 0.f, bs = 0.f;
+        for (int j = hj0; j < hj1; j++) hs += hj[3 * j + c];
+        for (int j = bj0; j < bj1; j++) bs += bjt[3 * j + c];
+        body[((int64_t)b * Vb + d) * 3 + c] = (h - hs / (float)(hj1 - hj0)) + bs / (float)(bj1 - bj0);
     }
 }
 
@@ -473,6 +507,50 @@ int gsr_lbs(int B, int V, int J, int NB, const float* v_template, int64_t v_temp
     hipLaunchKernelGGL(k_lbs_skin, dim3((V + 255) / 256, B), dim3(256), 0, s, V, J, lbs_weights_t, A,
                        a.vp, verts, vert_transforms);
     return hip_check("lbs_skin");
+}
+
+int gsr_blend_joints(int B, int V, int J, int NB, const float* v_template, int64_t v_template_stride,
+                     const float* betas, const float* shapedirs_t, const float* J_regressor,
+                     const float* joints_offset, float* v_shaped, float* joints, void* stream) {
+    if (B <= 0 || V <= 0 || J < 1) return api_fail(GSR_ERR_ARG, "gsr_blend_joints: bad sizes");
+    if (!v_template || !J_regressor || !v_shaped || !joints)
+        return api_fail(GSR_ERR_ARG, "gsr_blend_joints: null required pointer");
+    if (v_template_stride != 0 && v_template_stride != (int64_t)V * 3)
+        return api_fail(GSR_ERR_ARG, "gsr_blend_joints: v_template stride must be 0 or V*3");
+    if (betas && (NB <= 0 || !shapedirs_t))
+        return api_fail(GSR_ERR_ARG, "gsr_blend_joints: betas need NB > 0 and shapedirs");
+    if (!betas) NB = 0;
+    const size_t lds = sizeof(float) * (size_t)NB * kLbsFrames;
+    if (lds > 160 * 1024) return api_fail(GSR_ERR_ARG, "gsr_blend_joints: NB too large for LDS");
+    hipStream_t s = (hipStream_t)stream;
+    const int M = V * 3;
+    hipLaunchKernelGGL(k_lbs_blend, dim3((M + 255) / 256, (B + kLbsFrames - 1) / kLbsFrames), dim3(256),
+                       lds, s, B, M, NB, 0, v_template, v_template_stride, betas, shapedirs_t,
+                       nullptr, nullptr, v_shaped, nullptr);
+    if (int rc = hip_check("blend_shapes")) return rc;
+    hipLaunchKernelGGL(k_lbs_joints, dim3(J, B), dim3(256), 0, s, V, J, J_regressor, v_shaped,
+                       joints_offset, joints);
+    return hip_check("vertices2joints");
+}
+
+int gsr_splice_head(int B, int V_body, int N_head, const int32_t* head_index, const float* head_verts,
+                    const float* r_eyelid, const float* l_eyelid, const float* eyelid_params,
+                    const float* head_scale, const float* head_joints, int J_head, int hj0, int hj1,
+                    const float* body_joints, int J_body, int bj0, int bj1, float* body_v_shaped,
+                    uint32_t* bad_index_flag, void* stream) {
+    if (B <= 0 || V_body <= 0 || N_head < 0) return api_fail(GSR_ERR_ARG, "gsr_splice_head: bad sizes");
+    if (N_head == 0) return 0;
+    if (!head_index || !head_verts || !head_joints || !body_joints || !body_v_shaped)
+        return api_fail(GSR_ERR_ARG, "gsr_splice_head: null required pointer");
+    if (eyelid_params && (!r_eyelid || !l_eyelid))
+        return api_fail(GSR_ERR_ARG, "gsr_splice_head: eyelid_params need both eyelid bases");
+    if (hj0 < 0 || hj1 <= hj0 || hj1 > J_head || bj0 < 0 || bj1 <= bj0 || bj1 > J_body)
+        return api_fail(GSR_ERR_ARG, "gsr_splice_head: bad reference joint ranges");
+    hipLaunchKernelGGL(k_splice_head, dim3((N_head + 255) / 256, B), dim3(256), 0, (hipStream_t)stream,
+                       V_body, N_head, head_index, head_verts, r_eyelid, l_eyelid, eyelid_params,
+                       head_scale, head_joints, J_head, hj0, hj1, body_joints, J_body, bj0, bj1,
+                       body_v_shaped, bad_index_flag);
+    return hip_check("splice_head");
 }
 
 int gsr_deform_gaussians(int B, int V, int F, int N, const float* verts,

@@ -8,6 +8,8 @@ Host-side mirror of the reference's deformation API, so GUAVA's callers keep the
   lbs_wobeta(pose, v_shaped, posedirs, J_regressor, parents, lbs_weights, joints_offset=None,
              pose2rot=True, dtype)                       -> (verts, J_transformed, J, T, A)
                                                          lbs.py:255-333
+  EHMDeformer(body, flame, ...).forward(body_param_dict, flame_param_dict)
+                                                         -> EHM.forward's dict (modules/ehm/EHM.py:36-156)
   GaussianDeformer(vertex_gaussian_assets, uv_gaussian_assets, faces).forward(verts, T)
                                                          -> the deformed_assets dict of
                                                          Ubody_Gaussian.forward
@@ -202,3 +204,105 @@ class GaussianDeformer:
     def bad_index(self):
         """True if any binding-face / face-vertex index was out of range (synchronises)."""
         return bool(self.bad.item())
+
+
+class EHMDeformer:
+    """EHM.forward (models/modules/ehm/EHM.py:36-156) for B frames on the GPU: FLAME head lbs ->
+    eyelids and head scale -> body blend shapes and joints -> head splice -> body lbs_wobeta, with
+    every per-frame step a gfx950 kernel (gsr_lbs, gsr_blend_joints, gsr_splice_head) and no host
+    synchronisation.
+
+    body / flame: dicts of the LBS assets in the reference layouts (v_template [V,3], shapedirs
+    [V,3,NB], posedirs, J_regressor, parents, lbs_weights); smplx2flame_ind [Nh] (SMPLX.py:191);
+    l_eyelid / r_eyelid [Nh,3] (FLAME.py:105-106).  The k-major copies are made once here.
+    Inputs of forward() are the reference's parameter dicts (tensors on the device)."""
+
+    HEAD_REF = (3, 5)    # head_joints[:, 3:5] (EHM.py:123)
+    BODY_REF = (23, 25)  # tbody_joints[:, 23:25]
+
+    def __init__(self, body, flame, smplx2flame_ind, l_eyelid, r_eyelid, device="cuda"):
+        dev = torch.device(device)
+        t = lambda x: torch.as_tensor(np.ascontiguousarray(x), device=dev)  # noqa: E731
+        self.dev = dev
+        self.body = {k: (t(v) if k != "parents" else np.asarray(v, np.int32)) for k, v in body.items()}
+        self.flame = {k: (t(v) if k != "parents" else np.asarray(v, np.int32)) for k, v in flame.items()}
+        for a in (self.body, self.flame):
+            a["shapedirs_t"] = _shapedirs_t(a["shapedirs"])
+            a["lbs_weights_t"] = _weights_t(a["lbs_weights"])
+        self.head_index = t(np.asarray(smplx2flame_ind, np.int32))
+        self.l_eyelid, self.r_eyelid = t(np.asarray(l_eyelid, np.float32)), t(np.asarray(r_eyelid, np.float32))
+        self.bad = torch.zeros(1, dtype=torch.int32, device=dev)
+        self._ws = {}
+
+    def _workspace(self, B, V, J, NB):
+        key = (B, V, J, NB)
+        if key not in self._ws:
+            n = _lib.load().gsr_lbs_workspace_bytes(B, V, J, NB)
+            self._ws[key] = torch.empty((n,), dtype=torch.uint8, device=self.dev)
+        return self._ws[key]
+
+    def forward(self, body_param_dict, flame_param_dict):
+        L = _lib.load()
+        st = _stream(self.dev)
+        bp, fp = body_param_dict, flame_param_dict
+        if bp.get("hand_scale") is not None:
+            raise NotImplementedError("hand_scale (EHM.py:126-132) needs the MANO vertex map, not bundled")
+        fa, ba = self.flame, self.body
+        B = fp["shape_params"].shape[0]
+        o = dict(dtype=torch.float32, device=self.dev)
+        # FLAME head (EHM.py:41-75): betas = shape ++ expression; pose = 0 global, 0 neck, jaw, eyes
+        Vh, Jh, NBh = fa["J_regressor"].shape[1], fa["J_regressor"].shape[0], fa["shapedirs"].shape[2]
+        betas_h = torch.cat([_f32(fp["shape_params"]), _f32(fp["expression_params"])], 1)
+        if betas_h.shape[1] < NBh:
+            betas_h = torch.cat([betas_h, torch.zeros(B, NBh - betas_h.shape[1], **o)], 1)
+        z3 = torch.zeros(B, 3, **o)
+        pose_h = torch.cat([z3, z3, _f32(fp["jaw_params"]).reshape(B, 3),
+                            _f32(fp["eye_pose_params"]).reshape(B, 6)], 1).contiguous()
+        hv = torch.empty((B, Vh, 3), **o)
+        hj = torch.empty((B, Jh, 3), **o)
+        rc = L.gsr_lbs(B, Vh, Jh, NBh, _ptr(fa["v_template"]), 0, _ptr(betas_h.contiguous()),
+                       _ptr(fa["shapedirs_t"]), _ptr(pose_h), 1, _ptr(fa["posedirs"]),
+                       _ptr(fa["J_regressor"]), fa["parents"].ctypes.data_as(ctypes.c_void_p),
+                       _ptr(fa["lbs_weights_t"]), None, _ptr(hv), _ptr(hj), None, None, None, None,
+                       _ptr(self._workspace(B, Vh, Jh, NBh)), st)
+        _lib.check(rc, "gsr_lbs (FLAME head)")
+        # body template (EHM.py:101-118): blend shapes of shape ++ exp, regressed joints + offset
+        Vb, Jb, NBb = ba["J_regressor"].shape[1], ba["J_regressor"].shape[0], ba["shapedirs"].shape[2]
+        n_shape = NBb - bp["exp"].shape[1]  # EHM.py:101-106: pad or cut shape to n_shape, then ++ exp
+        shp = _f32(bp["shape"])[:, :n_shape]
+        if shp.shape[1] < n_shape:
+            shp = torch.cat([shp, torch.zeros(B, n_shape - shp.shape[1], **o)], 1)
+        sc = torch.cat([shp, _f32(bp["exp"])], 1).contiguous()
+        joff = _f32(bp["joints_offset"]) if bp.get("joints_offset") is not None else None
+        vt = torch.empty((B, Vb, 3), **o)
+        tj = torch.empty((B, Jb, 3), **o)
+        _lib.check(L.gsr_blend_joints(B, Vb, Jb, NBb, _ptr(ba["v_template"]), 0, _ptr(sc),
+                                      _ptr(ba["shapedirs_t"]), _ptr(ba["J_regressor"]), _ptr(joff),
+                                      _ptr(vt), _ptr(tj), st), "gsr_blend_joints")
+        # head splice (EHM.py:72-75, 121-124)
+        eyelid = _f32(fp["eyelid_params"]) if fp.get("eyelid_params") is not None else None
+        hs = bp.get("head_scale")
+        hs = _f32(hs).expand(B, 3).contiguous() if hs is not None else None
+        _lib.check(L.gsr_splice_head(B, Vb, Vh, _ptr(self.head_index), _ptr(hv), _ptr(self.r_eyelid),
+                                     _ptr(self.l_eyelid), _ptr(eyelid), _ptr(hs), _ptr(hj), Jh,
+                                     self.HEAD_REF[0], self.HEAD_REF[1], _ptr(tj), Jb, self.BODY_REF[0],
+                                     self.BODY_REF[1], _ptr(vt), _ptr(self.bad), st), "gsr_splice_head")
+        # body pose (EHM.py:94-112): global, body, jaw = 0, eyes = 0, hands
+        gp = _f32(bp["global_pose"]).reshape(B, 1, 3) if bp.get("global_pose") is not None else torch.zeros(B, 1, 3, **o)
+        bpose = _f32(bp["body_pose"]).reshape(B, 21, 3) if bp.get("body_pose") is not None else torch.zeros(B, 21, 3, **o)
+        pose = torch.cat([gp, bpose, torch.zeros(B, 3, 3, **o), _f32(bp["left_hand_pose"]).reshape(B, 15, 3),
+                          _f32(bp["right_hand_pose"]).reshape(B, 15, 3)], 1).contiguous()
+        verts = torch.empty((B, Vb, 3), **o)
+        jt2 = torch.empty((B, Jb, 3), **o)
+        J = torch.empty((B, Jb, 3), **o)
+        T = torch.empty((B, Vb, 4, 4), **o)
+        A = torch.empty((B, Jb, 4, 4), **o)
+        rc = L.gsr_lbs(B, Vb, Jb, 0, _ptr(vt), Vb * 3, None, None, _ptr(pose), 1, _ptr(ba["posedirs"]),
+                       _ptr(ba["J_regressor"]), ba["parents"].ctypes.data_as(ctypes.c_void_p),
+                       _ptr(ba["lbs_weights_t"]), _ptr(joff), _ptr(verts), _ptr(jt2), _ptr(J), _ptr(T),
+                       _ptr(A), None, _ptr(self._workspace(B, Vb, Jb, 0)), st)
+        _lib.check(rc, "gsr_lbs (SMPL-X body)")
+        return {"vertices": verts, "joints": J, "joints_transform": jt2, "ver_transform_mat": T,
+                "joint_transform_mat": A}
+
+    __call__ = forward

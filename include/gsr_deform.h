@@ -11,6 +11,9 @@
  *                           batch_rodrigues :379-410, batch_rigid_transform :426-482 fused in.
  *                           Used by EHM.forward (modules/ehm/EHM.py:67-70 FLAME head,
  *                           :134-137 SMPL-X body).
+ *   gsr_blend_joints     <- blend_shapes + vertices2joints (lbs.py:355-376, :335-352), the body
+ *                           template step of EHM.forward (EHM.py:114-118)
+ *   gsr_splice_head      <- EHM.forward's FLAME-head splice (EHM.py:72-75, :121-124)
  *   gsr_deform_gaussians <- the Gaussian part of Ubody_Gaussian.forward
  *                           UbodyAvatar/ubody_gaussian.py:252-278: vertex Gaussians
  *                           (rotmat_to_unitquat of the per-vertex skinning matrix, quat_product,
@@ -58,6 +61,25 @@ int gsr_lbs(int B, int V, int J, int NB, const float* v_template, int64_t v_temp
             const float* lbs_weights_t, const float* joints_offset, float* verts,
             float* joints_transformed, float* joints, float* vert_transforms,
             float* joint_transforms, float* v_shaped, char* workspace, void* stream);
+
+/* blend_shapes + vertices2joints (lbs.py:355-376, :335-352; EHM.py:115-118): v_shaped [B,V,3] =
+ * v_template + shapedirs . betas (betas == NULL: a copy of v_template), joints [B,J,3] =
+ * J_regressor . v_shaped (+ joints_offset [B,J,3] or NULL). */
+int gsr_blend_joints(int B, int V, int J, int NB, const float* v_template, int64_t v_template_stride,
+                     const float* betas, const float* shapedirs_t, const float* J_regressor,
+                     const float* joints_offset, float* v_shaped, float* joints, void* stream);
+
+/* EHM.forward's head splice (EHM.py:72-75, :121-124) into the body template, in place:
+ *   h = (head_verts + r_eyelid * eyelid[:,1] + l_eyelid * eyelid[:,0]) * head_scale
+ *   body_v_shaped[b, head_index[i]] = h - mean(head_joints[b, hj0:hj1]) + mean(body_joints[b, bj0:bj1])
+ * head_verts [B,N_head,3] (FLAME lbs output), r/l_eyelid [N_head,3], eyelid_params [B,2] (or NULL:
+ * no eyelids), head_scale [B,3] (or NULL), head_joints [B,J_head,3], body_joints [B,J_body,3]
+ * (EHM: hj = [3,5), bj = [23,25)).  An out-of-range head_index ORs 2 into *bad_index_flag. */
+int gsr_splice_head(int B, int V_body, int N_head, const int32_t* head_index, const float* head_verts,
+                    const float* r_eyelid, const float* l_eyelid, const float* eyelid_params,
+                    const float* head_scale, const float* head_joints, int J_head, int hj0, int hj1,
+                    const float* body_joints, int J_body, int bj0, int bj1, float* body_v_shaped,
+                    uint32_t* bad_index_flag, void* stream);
 
 /* Ubody_Gaussian.forward's Gaussian assembly for B frames; P = V + N Gaussians per frame, the V
  * vertex Gaussians first.

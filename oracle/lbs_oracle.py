@@ -20,8 +20,9 @@ Pinning: lbs / lbs_wobeta / batch_rodrigues / batch_rigid_transform against outp
 reference's own lbs.py run in the build container (tests/golden/lbs_golden.npz,
 tests/golden/make_lbs_golden.py); the roma and graphics_utils restatements (not importable here:
 roma absent, graphics_utils needs pytorch3d/lightning) are "parity unpinned" against the reference
-and checked by properties (unit norm, rotation round trip through the reference's importable
-utils/rotation_converter.quaternion_to_rotation_matrix, orthonormal frames).
+and checked by properties (unit norm, rotation round trip through an independent quaternion->matrix
+formula and scipy's Rotation.from_matrix, Hamilton composition, right-handed orthonormal frames).
+  ehm_forward            models/modules/ehm/EHM.py:36-137 (composition of the above + head splice)
 """
 import numpy as np
 
@@ -209,3 +210,31 @@ def deform_gaussians(verts, vert_transforms, faces, vtx_rotations, vtx_scales, b
                 rotation=np.concatenate([qv, qu], 1),
                 scaling=np.concatenate([per_frame(vtx_scales), per_frame(uv_scales) * s_n], 1),
                 margin=np.concatenate([m_v, m_f[:, bind]], 1))
+
+
+def ehm_forward(body, flame, extra, body_params, flame_params):
+    """EHM.forward (modules/ehm/EHM.py:36-137) on numpy assets (avatar.ehm_assets layout):
+    FLAME head lbs (jaw + eyes; global and neck zeroed, :59-63) + eyelids + head_scale (:72-75),
+    body blend_shapes + joints (:114-118), head splice (:121-124), body lbs_wobeta with jaw and eyes
+    zeroed (:98-99, :134-137).  Returns dict(vertices, joints, joints_transform, ver_transform_mat,
+    joint_transform_mat)."""
+    fp, bp = flame_params, body_params
+    B = fp["shape_params"].shape[0]
+    betas = np.concatenate([fp["shape_params"], fp["expression_params"]], 1)
+    zeros3 = np.zeros((B, 3))
+    full = np.concatenate([zeros3, zeros3, fp["jaw_params"], fp["eye_pose_params"]], 1)
+    hv, hj, *_ = lbs(betas, full, flame["v_template"], flame["shapedirs"], flame["posedirs"],
+                     flame["J_regressor"], flame["parents"], flame["lbs_weights"])
+    hv = hv + extra["r_eyelid"][None] * np.asarray(fp["eyelid_params"], np.float64)[:, 1:2, None]
+    hv = hv + extra["l_eyelid"][None] * np.asarray(fp["eyelid_params"], np.float64)[:, 0:1, None]
+    hv = hv * np.asarray(bp["head_scale"], np.float64)[:, None]
+    sc = np.concatenate([bp["shape"], bp["exp"]], 1)
+    vt = np.asarray(body["v_template"], np.float64) + blend_shapes(sc, body["shapedirs"])
+    tj = vertices2joints(body["J_regressor"], vt) + np.asarray(bp["joints_offset"], np.float64)
+    idx = np.asarray(extra["smplx2flame_ind"]).astype(np.int64)
+    vt[:, idx] = hv - hj[:, 3:5].mean(1, keepdims=True) + tj[:, 23:25].mean(1, keepdims=True)
+    pose = np.concatenate([bp["global_pose"].reshape(B, 1, 3), bp["body_pose"], np.zeros((B, 3, 3)),
+                           bp["left_hand_pose"], bp["right_hand_pose"]], 1)
+    verts, jt, J, T, A = lbs_wobeta(pose, vt, body["posedirs"], body["J_regressor"], body["parents"],
+                                    body["lbs_weights"], bp["joints_offset"])
+    return dict(vertices=verts, joints=J, joints_transform=jt, ver_transform_mat=T, joint_transform_mat=A)

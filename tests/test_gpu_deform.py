@@ -135,3 +135,18 @@ def test_bad_binding_index_is_flagged_not_faulted():
     assert dfm.bad_index()
     xyz = out["xyz"].cpu().numpy()
     assert np.isnan(xyz[0, V + 5]).all() and np.isfinite(np.delete(xyz[0], V + 5, 0)).all()
+
+
+def test_ehm_forward_then_gaussians_match_oracle():
+    """EHM.forward (FLAME head lbs + eyelids + head scale + splice + SMPL-X body lbs) for B=3
+    frames, then Ubody_Gaussian's assembly, against the oracle composition."""
+    from guava_renderer_amd import avatar, deform
+    body, flame, extra = avatar.ehm_assets(seed=0)
+    bp, fp = avatar.ehm_params(3, seed=1000)
+    ehm = deform.EHMDeformer(body, flame, extra["smplx2flame_ind"], extra["l_eyelid"], extra["r_eyelid"],
+                             device=DEV)
+    out = ehm({k: _t(v) for k, v in bp.items()}, {k: _t(v) for k, v in fp.items()})
+    ref = lo.ehm_forward(body, flame, extra, bp, fp)
+    for k in ("vertices", "joints", "joints_transform", "ver_transform_mat", "joint_transform_mat"):
+        np.testing.assert_allclose(out[k].cpu().numpy(), ref[k], atol=ATOL, rtol=0, err_msg=k)
+    assert int(ehm.bad.item()) == 0
