@@ -42,6 +42,9 @@ def _args():
     ap.add_argument("--batch", type=int, default=32, help="frames per step per GPU")
     ap.add_argument("--config", default="c2", choices=["c2", "c5"])
     ap.add_argument("--pipeline", default="avatar", choices=["avatar", "raster"])
+    ap.add_argument("--refine", action="store_true",
+                    help="fuse the refiner's first 1x1 conv 32->16 + leaky ReLU into the render "
+                         "epilogue (inference output: 16 refiner features + 4 raw channels)")
     ap.add_argument("--fast-exp", action="store_true", help="hardware exp (not bit-exact)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -164,8 +167,15 @@ def main():
         scene = {"colors": g["colors"], "opacities": g["opacities"]}
         avatar_inputs = (body, flame, extra, g, bp, fp)
 
+        head = None
+        if a.refine:
+            from guava_renderer_amd.batch import RefineHead
+            rng = np.random.default_rng(5)  # random-init conv_body_first (nn.Conv2d(32, 16, 1))
+            head = RefineHead(t(rng.uniform(-0.18, 0.18, (16, 32)).astype(np.float32)),
+                              t(rng.uniform(-0.18, 0.18, 16).astype(np.float32)), keep_channels=4)
+
         def step():
-            return pipe.render(bpt, fpt, views, projs, tanf)
+            return pipe.render(bpt, fpt, views, projs, tanf, refine=head)
     else:
         scene = scenes.avatar_cloud(P, seed=0, gaussians_per_texel=wl["gpt"])
         P = scene["means3D"].shape[0]
@@ -258,8 +268,8 @@ def main():
                  "synthetic (SMPL-X-template avatar cloud, GUAVA attribute distributions, "
                  "one orbit camera per frame)"),
         "config": {"workload": workload,
-                   "pipeline": "EHM LBS -> Gaussian assembly -> rasterize" if a.pipeline == "avatar"
-                   else "rasterize", "gaussians": P, "image": [W, H], "channels": C,
+                   "pipeline": ("EHM LBS -> Gaussian assembly -> rasterize" if a.pipeline == "avatar"
+                                else "rasterize") + (" + fused refiner conv_body_first" if a.refine else ""), "gaussians": P, "image": [W, H], "channels": C,
                    "frames_per_step_per_gpu": B, "global_batch": B * world,
                    "parallelism": f"frame-sharded x{world}",
                    "exp": "hw" if a.fast_exp else "exact-poly",

@@ -13,7 +13,8 @@ EXPORTS = ("gsr_version", "gsr_last_error", "gsr_set_exact_exp", "gsr_geometry_b
            "gsr_image_bytes", "gsr_binning_bytes", "gsr_mark_visible", "gsr_forward",
            "gsr_backward", "gsr_batch_workspace_bytes", "gsr_forward_batch",
            "gsr_backward_batch", "gsr_batch_status", "gsr_profile_enable", "gsr_profile_read",
-           "gsr_render_counters", "gsr_render_timeline",
+           "gsr_render_counters", "gsr_render_timeline", "gsr_forward_batch_refine",
+           "gsr_refine_prepare",
            # include/gsr_deform.h
            "gsr_lbs_workspace_bytes", "gsr_lbs", "gsr_blend_joints", "gsr_splice_head",
            "gsr_deform_gaussians")
@@ -27,6 +28,12 @@ _f = ctypes.c_float
 _sz = ctypes.c_size_t
 
 _lib = None
+
+
+class RefineEpilogue(ctypes.Structure):
+    """gsr_refine_epilogue (include/gsr.h)."""
+    _fields_ = [("weight", _vp), ("bias", _vp), ("n_out", _i), ("negative_slope", _f),
+                ("out_refine", _vp), ("keep_channels", _i)]
 
 
 class GsrError(RuntimeError):
@@ -76,6 +83,11 @@ def load(path=None):
                                     _i64, _f, _vp, _vp, _vp, _vp, _i64, _vp, _i64, _vp, _vp, _vp, _i,
                                     _vp]
     L.gsr_forward_batch.restype = _i
+    L.gsr_forward_batch_refine.argtypes = list(L.gsr_forward_batch.argtypes[:-1]) + [
+        ctypes.POINTER(RefineEpilogue), _vp]
+    L.gsr_forward_batch_refine.restype = _i
+    L.gsr_refine_prepare.argtypes = [_i, _vp, _vp, _i, _i, _vp, _vp]
+    L.gsr_refine_prepare.restype = _i
     L.gsr_backward_batch.argtypes = [_i, _i, _i, _i, _vp, _i64, _vp, _i64, _vp, _i64, _vp, _i64, _vp,
                                      _i64, _f, _vp, _vp, _vp, _vp, _i64, _vp, _i64, _vp, _vp, _vp, _vp,
                                      _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i, _vp]

@@ -44,19 +44,33 @@ class BatchRasterizer:
         return ctypes.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)
 
     def forward(self, means3D, colors, opacities, scales, rotations, viewmatrices, projmatrices,
-                tanfov, backgrounds, scale_modifier=1.0, antialiasing=False):
+                tanfov, backgrounds, scale_modifier=1.0, antialiasing=False, refine=None):
+        """Render B frames.  refine: optional RefineHead -- the refiner's first 1x1 conv + leaky ReLU
+        fused into the render epilogue (include/gsr.h gsr_refine_epilogue); its output is
+        refine.out [B,n_out,H,W] and only out_color[:, :refine.keep_channels] is written."""
         B = self.B
         bg_stride = backgrounds.shape[-1] if backgrounds.dim() == 2 else 0
-        rc = self.L.gsr_forward_batch(
-            B, self.P, self.W, self.H,
-            means3D.data_ptr(), _stride(means3D, B, 3), colors.data_ptr(), _stride(colors, B, C),
-            opacities.data_ptr(), _stride(opacities, B, 1), scales.data_ptr(), _stride(scales, B, 3),
-            rotations.data_ptr(), _stride(rotations, B, 4), float(scale_modifier),
-            viewmatrices.data_ptr(), projmatrices.data_ptr(), tanfov.data_ptr(),
-            backgrounds.data_ptr(), bg_stride, self.workspace.data_ptr(), self.R_capacity,
-            self.out_color.data_ptr(), self.out_invdepth.data_ptr(), self.radii.data_ptr(),
-            int(bool(antialiasing)), self._stream())
-        _lib.check(rc, "gsr_forward_batch")
+        args = (B, self.P, self.W, self.H,
+                means3D.data_ptr(), _stride(means3D, B, 3), colors.data_ptr(), _stride(colors, B, C),
+                opacities.data_ptr(), _stride(opacities, B, 1), scales.data_ptr(), _stride(scales, B, 3),
+                rotations.data_ptr(), _stride(rotations, B, 4), float(scale_modifier),
+                viewmatrices.data_ptr(), projmatrices.data_ptr(), tanfov.data_ptr(),
+                backgrounds.data_ptr(), bg_stride, self.workspace.data_ptr(), self.R_capacity,
+                self.out_color.data_ptr(), self.out_invdepth.data_ptr(), self.radii.data_ptr(),
+                int(bool(antialiasing)))
+        if refine is None:
+            _lib.check(self.L.gsr_forward_batch(*args, self._stream()), "gsr_forward_batch")
+        else:
+            # composite the pre-contracted rows (include/gsr.h gsr_refine_prepare): features and
+            # backgrounds both go through the head's 32 -> keep + n_out map
+            pc = refine.prepare(colors, self._stream())
+            pb = refine.prepare(backgrounds.reshape(-1, C), self._stream(), cache=False)
+            args = list(args)
+            args[6] = pc.data_ptr()
+            args[18] = pb.data_ptr()
+            ep = refine.epilogue(B, self.H, self.W)
+            _lib.check(self.L.gsr_forward_batch_refine(*args, ctypes.byref(ep), self._stream()),
+                       "gsr_forward_batch_refine")
         return self.out_color, self.out_invdepth, self.radii
 
     def backward(self, means3D, colors, opacities, scales, rotations, viewmatrices, projmatrices,
@@ -95,6 +109,50 @@ class BatchRasterizer:
                                            ctypes.byref(R), ctypes.byref(ovf), self._stream()),
                    "gsr_batch_status")
         return int(R.value), bool(ovf.value)
+
+
+class RefineHead:
+    """StyleUNet.conv_body_first (nn.Conv2d(32, n_out, 1), styleunet.py:110) + F.leaky_relu_(., 0.2)
+    (:178), evaluated inside the render kernel.  weight [n_out,32] or [n_out,32,1,1], bias [n_out]."""
+
+    def __init__(self, weight, bias=None, negative_slope=0.2, keep_channels=4):
+        w = weight.detach().reshape(weight.shape[0], -1).to(torch.float32).contiguous()
+        assert w.shape[1] == C and 1 <= w.shape[0] <= C, w.shape
+        self.weight = w
+        self.bias = bias.detach().to(torch.float32).contiguous() if bias is not None else None
+        self.n_out = w.shape[0]
+        self.slope = float(negative_slope)
+        self.keep_channels = int(keep_channels)
+        assert self.keep_channels + self.n_out <= C
+        self.out = None
+        self._prep_key, self._prep = None, None
+
+    @classmethod
+    def from_conv(cls, conv, negative_slope=0.2, keep_channels=4):
+        return cls(conv.weight, conv.bias, negative_slope, keep_channels)
+
+    def prepare(self, rows, stream, cache=True):
+        """[..., 32] feature rows -> the pre-contracted rows the refine epilogue composites; cached
+        on the tensor's identity and version (an avatar's features are static across frames)."""
+        key = (rows.data_ptr(), tuple(rows.shape), rows._version)
+        if cache and self._prep_key == key:
+            return self._prep
+        out = torch.empty_like(rows)
+        n = rows.numel() // C
+        _lib.check(_lib.load().gsr_refine_prepare(n, rows.data_ptr(), self.weight.data_ptr(), self.n_out,
+                                                  self.keep_channels, out.data_ptr(), stream),
+                   "gsr_refine_prepare")
+        if cache:
+            self._prep_key, self._prep = key, out
+        return out
+
+    def epilogue(self, B, H, W):
+        shape = (B, self.n_out, H, W)
+        if self.out is None or tuple(self.out.shape) != shape:
+            self.out = torch.empty(shape, dtype=torch.float32, device=self.weight.device)
+        return _lib.RefineEpilogue(self.weight.data_ptr(),
+                                   self.bias.data_ptr() if self.bias is not None else None,
+                                   self.n_out, self.slope, self.out.data_ptr(), self.keep_channels)
 
 
 def profile_enable(stages=("render_fwd",)):

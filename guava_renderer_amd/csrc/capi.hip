@@ -338,7 +338,28 @@ int gsr_forward_batch(int B, int P, int width, int height, const float* means3D,
                       const float* tanfov, const float* backgrounds, int64_t bg_stride,
                       char* workspace, int64_t R_capacity, float* out_color, float* out_invdepth,
                       int* radii, int antialiasing, void* stream) {
+    return gsr_forward_batch_refine(B, P, width, height, means3D, means_stride, colors, colors_stride,
+                                    opacities, opac_stride, scales, scales_stride, rotations, rot_stride,
+                                    scale_modifier, viewmatrices, projmatrices, tanfov, backgrounds,
+                                    bg_stride, workspace, R_capacity, out_color, out_invdepth, radii,
+                                    antialiasing, nullptr, stream);
+}
+
+int gsr_forward_batch_refine(int B, int P, int width, int height, const float* means3D,
+                             int64_t means_stride, const float* colors, int64_t colors_stride,
+                             const float* opacities, int64_t opac_stride, const float* scales,
+                             int64_t scales_stride, const float* rotations, int64_t rot_stride,
+                             float scale_modifier, const float* viewmatrices, const float* projmatrices,
+                             const float* tanfov, const float* backgrounds, int64_t bg_stride,
+                             char* workspace, int64_t R_capacity, float* out_color, float* out_invdepth,
+                             int* radii, int antialiasing, const gsr_refine_epilogue* refine,
+                             void* stream) {
     hipStream_t s = (hipStream_t)stream;
+    if (refine) {
+        if (!refine->out_refine || refine->n_out < 1 || refine->keep_channels < 0 ||
+            refine->keep_channels + refine->n_out > GSR_C)
+            return fail(GSR_ERR_ARG, "refine epilogue: out_refine required, n_out >= 1, keep + n_out <= 32");
+    }
     if (B <= 0 || P <= 0 || width <= 0 || height <= 0 || !workspace || !tanfov)
         return fail(GSR_ERR_ARG, "bad batch arguments");
     if ((int64_t)((width + 15) / 16) * ((height + 15) / 16) > kMaxTiles) return fail(GSR_ERR_ARG, "image too large");
@@ -366,12 +387,32 @@ int gsr_forward_batch(int B, int P, int width, int height, const float* means3D,
     in.prefiltered = 0; in.antialiasing = antialiasing;
     { const char* e = getenv("GSR_PRIO_ITEMS"); in.prio_items = e ? (uint32_t)atoi(e) : 0u; }
     Outputs o{out_color, out_invdepth, radii, g_render_counters, g_timeline, g_timeline_cap};
+    if (refine) {
+        o.rb = refine->bias;
+        o.out_refine = refine->out_refine;
+        o.n_out = refine->n_out;
+        o.keep = refine->keep_channels;
+        o.slope = refine->negative_slope;
+    }
     HIP_TRY(hipMemsetAsync(g.ctrl, 0, ctrl_words(d) * 4, s));
     HIP_TRY(hipMemsetAsync(g.bstart, 0, (size_t)d.B * (d.NB + 1) * 4, s));
     { StageTimer st_(0, s); launch_preprocess(d, in, g, o, s); }
     { StageTimer st_(1, s); launch_scan_blocksums(d, g, R_capacity, s); }
     int rc = run_binning_and_render(d, in, g, im, bn, o, 0, s);
     if (rc < 0) return rc;
+    return 0;
+}
+
+int gsr_refine_prepare(int n, const float* rows, const float* weight, int n_out, int keep_channels,
+                       float* prepared, void* stream) {
+    if (n < 0 || !weight || n_out < 1 || keep_channels < 0 || keep_channels + n_out > GSR_C)
+        return fail(GSR_ERR_ARG, "gsr_refine_prepare: need weight, n_out >= 1, keep + n_out <= 32");
+    if (n == 0) return 0;
+    if (!rows || !prepared || ((uintptr_t)rows & 15) != 0)
+        return fail(GSR_ERR_ARG, "gsr_refine_prepare: rows must be 16-byte aligned, prepared non-null");
+    launch_refine_prepare(n, rows, weight, n_out, keep_channels, prepared, (hipStream_t)stream);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return fail(GSR_ERR_HIP, std::string("refine_prepare: ") + hipGetErrorString(e));
     return 0;
 }
 

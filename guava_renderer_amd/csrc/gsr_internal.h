@@ -140,6 +140,14 @@ struct Outputs {
     uint64_t* stats;      // gsr_render_counters words, or null (production kernel)
     uint32_t* timeline;   // gsr_render_timeline records (instrumented kernel only), or null
     uint32_t timeline_cap;
+    // refiner-head epilogue (gsr_forward_batch_refine) over gsr_refine_prepare'd features:
+    // out_refine [B][n_out][H][W] = leaky_relu(channels [keep, keep+n_out) + b); null = off.
+    // keep: channels of out_color written.
+    const float* rb = nullptr;  // [n_out] or null
+    float* out_refine = nullptr;
+    int n_out = 0;
+    int keep = GSR_C;
+    float slope = 0.2f;
 };
 
 struct Grads {
@@ -179,6 +187,8 @@ void launch_render_fwd(const Dims& d, const Inputs& in, const GeomArena& g, cons
 void launch_render_bwd(const Dims& d, const Inputs& in, const GeomArena& g, const ImageArena& im,
                        const BinArena& b, const Grads& gr, bool exact, hipStream_t s);
 void launch_preprocess_bwd(const Dims& d, const Inputs& in, const GeomArena& g, const Grads& gr,
+                           hipStream_t s);
+void launch_refine_prepare(int n, const float* in, const float* w, int n_out, int keep, float* out,
                            hipStream_t s);
 void launch_mark_visible(int P, const float* means3D, const float* view, const float* proj,
                          uint8_t* present, hipStream_t s);

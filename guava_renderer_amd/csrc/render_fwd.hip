@@ -62,7 +62,11 @@ __device__ __forceinline__ float take_step(float alpha, float inv_depth, uint32_
 // Epilogue of one 16x4 strip: final_T, n_contrib, inverse depth (lane = pixel) and the 32
 // channel-major colour rows C + T*bg from the MFMA accumulators.  acc_n[r] at lane l holds channel
 // (r&3)+8*(r>>2)+4*(l>>5) of strip pixel 32n + (l&31), whose transmittance lives in lane 32n + (l&31).
-template <bool EMPTY>
+// REFINE (gsr_forward_batch_refine): the features were pre-contracted by gsr_refine_prepare, so
+// channels [keep, keep + n_out) already hold the refiner head's 1x1 conv W.(C + T bg); they get the
+// bias and the leaky ReLU here and go to out_refine, channels [0, keep) to out_color, the rest
+// nowhere.  No extra registers: the blend loop is the same kernel.
+template <bool EMPTY, bool REFINE>
 __device__ __forceinline__ void store_strip(const Dims& d, const ImageArena& im, const Outputs& o,
                                             const float* bg, int b, int tx, int sy0, int lane,
                                             const floatx16& acc0, const floatx16& acc1, float T,
@@ -86,19 +90,82 @@ __device__ __forceinline__ void store_strip(const Dims& d, const ImageArena& im,
     const int qx = tx * GSR_BX + (j & 15);
     const int qy0 = sy0 + (j >> 4);
     const int qy1 = qy0 + 2;
-    const int hoff = (lane >> 5) * 4 * (int)HW;  // channels +4 for the upper half-wave
+    const int hi = lane >> 5;
+    const int hoff = hi * 4 * (int)HW;  // channels +4 for the upper half-wave
     const int v0 = (qx < d.W && qy0 < d.H) ? (hoff + qy0 * d.W + qx) * 4 : 0x7FFFFFF0;
     const int v1 = (qx < d.W && qy1 < d.H) ? (hoff + qy1 * d.W + qx) * 4 : 0x7FFFFFF0;
+    __amdgpu_buffer_rsrc_t rr = rs;
+    if (REFINE)
+        rr = __builtin_amdgcn_make_buffer_rsrc(o.out_refine + (int64_t)b * o.n_out * HW, 0,
+                                               (int)((int64_t)o.n_out * HW * 4), 0x00020000);
 #pragma unroll
     for (int r = 0; r < 16; r++) {
         const int c = (r & 3) + 8 * (r >> 2);  // + 4 in the upper half-wave (in hoff)
-        const float bgc = (lane >> 5) ? bg[c + 4] : bg[c];
+        const float bgc = hi ? bg[c + 4] : bg[c];
         const int so = c * (int)HW * 4;
-        const float x0 = EMPTY ? bgc : fmaf(T0, bgc, acc0[r]);
-        const float x1 = EMPTY ? bgc : fmaf(T1, bgc, acc1[r]);
-        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(x0), rs, v0, so, 0);
-        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(x1), rs, v1, so, 0);
+        float x0 = EMPTY ? bgc : fmaf(T0, bgc, acc0[r]);
+        float x1 = EMPTY ? bgc : fmaf(T1, bgc, acc1[r]);
+        if (!REFINE) {
+            __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(x0), rs, v0, so, 0);
+            __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(x1), rs, v1, so, 0);
+        } else {
+            // branch-free: every channel is offered to both outputs; the one it does not belong to
+            // gets an offset past its buffer (dropped by the buffer range check)
+            const int ch_lo = c, ch_hi = c + 4;  // this register's channel in either half-wave
+            const int oc_lo = ch_lo - o.keep, oc_hi = ch_hi - o.keep;  // wave-uniform
+            const bool col_lo = ch_lo < o.keep, col_hi = ch_hi < o.keep;
+            const bool ref_lo = oc_lo >= 0 && oc_lo < o.n_out, ref_hi = oc_hi >= 0 && oc_hi < o.n_out;
+            const float b_lo = (ref_lo && o.rb) ? o.rb[oc_lo] : 0.0f;  // scalar loads
+            const float b_hi = (ref_hi && o.rb) ? o.rb[oc_hi] : 0.0f;
+            const bool col = hi ? col_hi : col_lo, ref = hi ? ref_hi : ref_lo;
+            const int oc = hi ? oc_hi : oc_lo;
+            const float bias = hi ? b_hi : b_lo;
+            __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(x0), rs, col ? v0 : 0x7FFFFFF0, so, 0);
+            __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(x1), rs, col ? v1 : 0x7FFFFFF0, so, 0);
+            float y0 = x0 + bias, y1 = x1 + bias;
+            y0 = y0 >= 0.0f ? y0 : y0 * o.slope;  // F.leaky_relu_(x, 0.2)
+            y1 = y1 >= 0.0f ? y1 : y1 * o.slope;
+            // out_refine rows: the same pixel offsets without the +4-channel half-wave shift
+            const int w0 = (ref && v0 != 0x7FFFFFF0) ? v0 - hoff * 4 + oc * (int)HW * 4 : 0x7FFFFFF0;
+            const int w1 = (ref && v1 != 0x7FFFFFF0) ? v1 - hoff * 4 + oc * (int)HW * 4 : 0x7FFFFFF0;
+            __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(y0), rr, w0, 0, 0);
+            __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(y1), rr, w1, 0, 0);
+            __builtin_amdgcn_sched_barrier(0);  // one channel at a time: no register build-up
+        }
     }
+}
+
+// gsr_refine_prepare: rows [f_0..f_{keep-1}, W.f (n_out values), 0...] of 32 floats.
+__global__ __launch_bounds__(256) void k_refine_prepare(int n, const float* __restrict__ in,
+                                                        const float* __restrict__ w, int n_out,
+                                                        int keep, float* __restrict__ out) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    float f[GSR_C];
+    const float4* src = reinterpret_cast<const float4*>(in + (int64_t)i * GSR_C);
+#pragma unroll
+    for (int q = 0; q < GSR_C / 4; q++) {
+        const float4 v = src[q];
+        f[4 * q] = v.x; f[4 * q + 1] = v.y; f[4 * q + 2] = v.z; f[4 * q + 3] = v.w;
+    }
+    float* dst = out + (int64_t)i * GSR_C;
+    for (int c = 0; c < GSR_C; c++) {
+        float v = 0.0f;
+        if (c < keep) {
+            v = f[c];
+        } else if (c < keep + n_out) {
+            const float* wr = w + (c - keep) * GSR_C;
+#pragma unroll
+            for (int k = 0; k < GSR_C; k++) v = fmaf(wr[k], f[k], v);
+        }
+        dst[c] = v;
+    }
+}
+
+void launch_refine_prepare(int n, const float* in, const float* w, int n_out, int keep, float* out,
+                           hipStream_t s) {
+    if (n <= 0) return;
+    hipLaunchKernelGGL(k_refine_prepare, dim3((n + 255) / 256), dim3(256), 0, s, n, in, w, n_out, keep, out);
 }
 
 // Work items, in k_tile_scan's longest-first order: the 4 strips of each non-empty tile
@@ -110,9 +177,10 @@ __device__ __forceinline__ void store_strip(const Dims& d, const ImageArena& im,
 // in three rotating register slots: the records and feature operand of step s+3 are loaded while
 // step s+1's alphas (the exp-heavy, transmittance-independent part) are computed and step s's
 // serial blend and MFMA accumulation run.
-template <bool EXACT, bool STATS, bool TL>
-__global__ __launch_bounds__(GSR_TILE_PIX) void k_render_fwd(Dims d, Inputs in, GeomArena g,
-                                                             ImageArena im, BinArena bn, Outputs o) {
+template <bool EXACT, bool STATS, bool TL, bool REFINE>
+__device__ __forceinline__ void render_fwd_body(const Dims& d, const Inputs& in, const GeomArena& g,
+                                                const ImageArena& im, const BinArena& bn,
+                                                const Outputs& o) {
     if (g.ctrl[kCtrlOverflow]) return;
     const uint32_t ne = g.ctrl[kCtrlNonEmpty];
     const uint32_t nstrip = (uint32_t)kStrips * ne;
@@ -141,7 +209,7 @@ __global__ __launch_bounds__(GSR_TILE_PIX) void k_render_fwd(Dims d, Inputs in, 
             const int t = tile_g - b * d.T;
             const floatx16 unused = {};
             for (int sp = 0; sp < kStrips; sp++)
-                store_strip<true>(d, im, o, in.bg + in.s_bg * b, b, t % d.gx, (t / d.gx) * GSR_BY + sp * 4,
+                store_strip<true, REFINE>(d, im, o, in.bg + in.s_bg * b, b, t % d.gx, (t / d.gx) * GSR_BY + sp * 4,
                                   lane, unused, unused, 1.0f, 0.f, 0u);
             continue;
         }
@@ -297,9 +365,24 @@ __global__ __launch_bounds__(GSR_TILE_PIX) void k_render_fwd(Dims d, Inputs in, 
             rec[2] = (uint32_t)n_steps;
             rec[3] = __builtin_amdgcn_s_getreg((3 << 11) | 20) & 7u;
         }
-        store_strip<false>(d, im, o, in.bg + in.s_bg * b, b, tx, ty * GSR_BY + strip * 4, lane, acc0, acc1, T,
+        store_strip<false, REFINE>(d, im, o, in.bg + in.s_bg * b, b, tx, ty * GSR_BY + strip * 4, lane, acc0, acc1, T,
                            invd, last);
     }
+}
+
+template <bool EXACT, bool STATS, bool TL>
+__global__ __launch_bounds__(GSR_TILE_PIX) void k_render_fwd(Dims d, Inputs in, GeomArena g,
+                                                             ImageArena im, BinArena bn, Outputs o) {
+    render_fwd_body<EXACT, STATS, TL, false>(d, in, g, im, bn, o);
+}
+
+// The refiner-head variant: the epilogue's extra stores would raise the register count past the
+// 4-waves-per-SIMD budget of the blend loop; pin the budget (the few extra live values of the
+// epilogue spill instead).
+template <bool EXACT>
+__global__ __launch_bounds__(GSR_TILE_PIX) __attribute__((amdgpu_waves_per_eu(4))) void k_render_fwd_refine(
+    Dims d, Inputs in, GeomArena g, ImageArena im, BinArena bn, Outputs o) {
+    render_fwd_body<EXACT, false, false, true>(d, in, g, im, bn, o);
 }
 
 void launch_render_fwd(const Dims& d, const Inputs& in, const GeomArena& g, const ImageArena& im,
@@ -311,6 +394,10 @@ void launch_render_fwd(const Dims& d, const Inputs& in, const GeomArena& g, cons
 #define GSR_LAUNCH(E, S, L) hipLaunchKernelGGL((k_render_fwd<E, S, L>), gr, bl, 0, s, d, in, g, im, b, o)
     if (o.stats) { if (exact) GSR_LAUNCH(true, true, false); else GSR_LAUNCH(false, true, false); }
     else if (o.timeline) { if (exact) GSR_LAUNCH(true, false, true); else GSR_LAUNCH(false, false, true); }
+    else if (o.out_refine) {
+        if (exact) hipLaunchKernelGGL((k_render_fwd_refine<true>), gr, bl, 0, s, d, in, g, im, b, o);
+        else hipLaunchKernelGGL((k_render_fwd_refine<false>), gr, bl, 0, s, d, in, g, im, b, o);
+    }
     else { if (exact) GSR_LAUNCH(true, false, false); else GSR_LAUNCH(false, false, false); }
 #undef GSR_LAUNCH
 }

@@ -42,10 +42,12 @@ class AvatarPipeline:
         e = self.ehm(body_params, flame_params)
         return self.gauss(e["vertices"], e["ver_transform_mat"])
 
-    def render(self, body_params, flame_params, views, projs, tanfov):
+    def render(self, body_params, flame_params, views, projs, tanfov, refine=None):
         """views / projs [B,16] (graphics_utils.py:44-50 layout), tanfov [B,2] ->
-        (color [B,32,H,W], invdepth [B,H,W], radii [B,P], deformed assets)."""
+        (color [B,32,H,W], invdepth [B,H,W], radii [B,P], deformed assets).  refine: optional
+        batch.RefineHead (the refiner's first conv fused into the render; output in refine.out)."""
         d = self.deform(body_params, flame_params)
         col, inv, radii = self.rast.forward(d["xyz"], self.gauss.colors, self.gauss.opacity,
-                                            d["scaling"], d["rotation"], views, projs, tanfov, self.bg)
+                                            d["scaling"], d["rotation"], views, projs, tanfov, self.bg,
+                                            refine=refine)
         return col, inv, radii, d

@@ -121,6 +121,40 @@ int gsr_backward_batch(int B, int P, int width, int height, const float* means3D
                        float* dL_dopacity, float* dL_dcolor, float* dL_dinvdepth_g,
                        float* dL_dmean3D, float* dL_dcov3D, float* dL_dscale, float* dL_drot,
                        int antialiasing, void* stream);
+/* Refiner-head epilogue: GaussianRenderer feeds the 32-channel render to the
+ * StyleUNet refiner (gaussian_render.py:73), whose first layer is a 1x1 conv 32 -> 16 + leaky ReLU
+ * (styleunet.py:110,178).  The conv is linear in the features, so it commutes with compositing:
+ *   W.(sum_g f_g alpha_g T_g + T bg) = sum_g (W.f_g) alpha_g T_g + T (W.bg).
+ * gsr_refine_prepare turns each 32-float row (a Gaussian's features, or a frame's background) into
+ *   [f_0 .. f_{keep-1}, W.f (n_out values), 0 ...]
+ * and gsr_forward_batch_refine, given prepared colors AND prepared backgrounds, composites those rows
+ * with the unchanged blend kernel and finishes in the epilogue:
+ *   out_color[b][c]   = channel c           for c < keep_channels (raw renders; GaussianRenderer
+ *                                            keeps 0-2 as raw_renders, 3 as extra_renders,
+ *                                            gaussian_render.py:71,83); other channels unwritten
+ *   out_refine[b][o]  = leaky_relu(channel keep+o + bias[o], negative_slope),  o < n_out
+ * so the 33-channel feature image is never written nor re-read.  Forward-only (inference:
+ * main/test.py, render_motion.py); keep_channels + n_out <= 32. */
+typedef struct {
+    const float* weight;   /* [n_out][32] (Conv2d weight [n_out,32,1,1]); used by gsr_refine_prepare */
+    const float* bias;     /* [n_out] or NULL */
+    int n_out;             /* >= 1 */
+    float negative_slope;  /* 0.2 in StyleUNet */
+    float* out_refine;     /* [B][n_out][H][W] */
+    int keep_channels;     /* raw channels of out_color still written */
+} gsr_refine_epilogue;
+/* rows [n,32] (16-byte aligned) -> prepared [n,32]. */
+int gsr_refine_prepare(int n, const float* rows, const float* weight, int n_out, int keep_channels,
+                       float* prepared, void* stream);
+int gsr_forward_batch_refine(int B, int P, int width, int height, const float* means3D,
+                             int64_t means_stride, const float* colors, int64_t colors_stride,
+                             const float* opacities, int64_t opac_stride, const float* scales,
+                             int64_t scales_stride, const float* rotations, int64_t rot_stride,
+                             float scale_modifier, const float* viewmatrices, const float* projmatrices,
+                             const float* tanfov, const float* backgrounds, int64_t bg_stride,
+                             char* workspace, int64_t R_capacity, float* out_color, float* out_invdepth,
+                             int* radii, int antialiasing, const gsr_refine_epilogue* refine,
+                             void* stream);
 /* Stage timing with HIP events recorded on the launch stream around each stage whose bit is set in
  * `stage_mask` (bit i = stage i: 0 preprocess, 1 block scan, 2 depth sort, 3 chunk count,
  * 4 tile scan, 5 ordered scatter, 6 render fwd, 7 render bwd, 8 preprocess bwd); 0 disables.

@@ -110,3 +110,38 @@ def test_render_counters_match_oracle(kind, P, W, H):
     assert contrib <= cnt["strip_pairs_blended"] * 64
     # survivors are taken two per k-step, an odd round tail pads with the null Gaussian
     assert cnt["strip_pairs_blended"] <= 2 * cnt["mfma_ksteps"] <= cnt["strip_pairs_blended"] + cnt["gaussians_staged"]
+
+
+def test_refine_epilogue_matches_conv():
+    """The fused StyleUNet conv_body_first + leaky ReLU (styleunet.py:110,178) equals torch's conv2d
+    on the full render within 1e-5 of scale (the conv is applied to each Gaussian's features before
+    compositing -- an exact algebraic reassociation, rounded differently); the kept raw channels
+    are bit-identical to the plain render and the others are not written."""
+    import torch
+    import torch.nn.functional as F
+    from guava_renderer_amd.batch import BatchRasterizer, RefineHead
+    from guava_renderer_amd import scenes
+    dev = "cuda:0"
+    B, P, W, H = 3, 6000, 96, 80  # ragged image: partial tiles on both axes
+    sc = scenes.random_cloud(P, seed=3)
+    t = lambda x: torch.tensor(np.ascontiguousarray(x), device=dev)  # noqa: E731
+    cams = scenes.frame_cameras(B, W, H, seed=7)
+    views = t(np.stack([c["viewmatrix"].reshape(16) for c in cams]))
+    projs = t(np.stack([c["projmatrix"].reshape(16) for c in cams]))
+    tanf = t(np.array([[c["tanfovx"], c["tanfovy"]] for c in cams], np.float32))
+    bgs = t(np.random.default_rng(0).normal(size=(B, 32)).astype(np.float32))
+    args = (t(sc["means3D"]), t(sc["colors"]), t(sc["opacities"]), t(sc["scales"]), t(sc["rotations"]),
+            views, projs, tanf, bgs)
+    r = BatchRasterizer(B, P, W, H, device=dev)
+    full = r.forward(*args)[0].clone()
+    rng = np.random.default_rng(1)
+    head = RefineHead(t(rng.normal(0, 0.2, (16, 32)).astype(np.float32)),
+                      t(rng.normal(0, 0.1, 16).astype(np.float32)), keep_channels=4)
+    r.out_color.fill_(12345.0)
+    col = r.forward(*args, refine=head)[0]
+    torch.cuda.synchronize()
+    assert torch.equal(col[:, :4], full[:, :4])
+    assert (col[:, 4:] == 12345.0).all()
+    ref = F.leaky_relu(F.conv2d(full, head.weight[:, :, None, None], head.bias), 0.2)
+    err = (head.out - ref).abs().max().item() / ref.abs().max().item()
+    assert err < 1e-5, err
