@@ -8,7 +8,7 @@ import os
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "lib", "libgsr.so")
 
-# every symbol declared in include/gsr.h and include/gsr_deform.h
+# every symbol declared in include/*.h
 EXPORTS = ("gsr_version", "gsr_last_error", "gsr_set_exact_exp", "gsr_geometry_bytes",
            "gsr_image_bytes", "gsr_binning_bytes", "gsr_mark_visible", "gsr_forward",
            "gsr_backward", "gsr_batch_workspace_bytes", "gsr_forward_batch",
@@ -17,7 +17,9 @@ EXPORTS = ("gsr_version", "gsr_last_error", "gsr_set_exact_exp", "gsr_geometry_b
            "gsr_refine_prepare",
            # include/gsr_deform.h
            "gsr_lbs_workspace_bytes", "gsr_lbs", "gsr_blend_joints", "gsr_splice_head",
-           "gsr_deform_gaussians")
+           "gsr_deform_gaussians",
+           # include/gsr_ssim.h
+           "gsr_fused_ssim", "gsr_fused_ssim_backward")
 
 ALLOC_FN = ctypes.CFUNCTYPE(ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t)
 
@@ -115,6 +117,10 @@ def load(path=None):
     L.gsr_deform_gaussians.argtypes = [_i, _i, _i, _i, _vp, _vp, _vp, _vp, _i64, _vp, _i64, _vp, _vp,
                                        _vp, _i64, _vp, _i64, _vp, _i64, _vp, _vp, _vp, _vp, _vp]
     L.gsr_deform_gaussians.restype = _i
+    L.gsr_fused_ssim.argtypes = [_i, _i, _i, _i, _f, _f, _vp, _vp, _vp, _vp, _vp, _vp, _vp]
+    L.gsr_fused_ssim.restype = _i
+    L.gsr_fused_ssim_backward.argtypes = [_i, _i, _i, _i, _f, _f, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp]
+    L.gsr_fused_ssim_backward.restype = _i
     _lib = L
     return L
 
