@@ -41,7 +41,9 @@ def _args():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--batch", type=int, default=32, help="frames per step per GPU")
     ap.add_argument("--config", default="c2", choices=["c2", "c5"])
-    ap.add_argument("--pipeline", default="avatar", choices=["avatar", "raster"])
+    ap.add_argument("--pipeline", default="avatar", choices=["avatar", "raster", "train"],
+                    help="train = BASELINE config 4: raster fwd + fused-SSIM/L1 loss + raster bwd + "
+                         "gradient all-reduce + Adam (use --batch 6)")
     ap.add_argument("--refine", action="store_true",
                     help="fuse the refiner's first 1x1 conv 32->16 + leaky ReLU into the render "
                          "epilogue (inference output: 16 refiner features + 4 raw channels)")
@@ -141,7 +143,7 @@ def main():
     tanf = t(np.array([[c["tanfovx"], c["tanfovy"]] for c in cams], np.float32))
     bgs = torch.zeros((B, C), dtype=torch.float32, device=dev)
     avatar_inputs = None
-    workload = wl["name"] + ("-deform+raster" if a.pipeline == "avatar" else "-raster")
+    workload = wl["name"] + {"avatar": "-deform+raster", "raster": "-raster", "train": "-train"}[a.pipeline]
 
     if a.pipeline == "avatar":
         from guava_renderer_amd import avatar
@@ -176,6 +178,25 @@ def main():
 
         def step():
             return pipe.render(bpt, fpt, views, projs, tanf, refine=head)
+    elif a.pipeline == "train":
+        from guava_renderer_amd.train import SplatTrainer
+        scene = scenes.avatar_cloud(P, seed=0, gaussians_per_texel=wl["gpt"])
+        P = scene["means3D"].shape[0]
+        params = {k: t(scene[k]) for k in ("means3D", "colors", "opacities", "scales", "rotations")}
+        probe = BatchRasterizer(B, P, W, H, R_capacity=24 * P * B, device=dev)
+        probe.forward(params["means3D"], params["colors"], params["opacities"], params["scales"],
+                      params["rotations"], views, projs, tanf, bgs)
+        R_probe, ovf = probe.status()
+        assert not ovf, "probe overflow"
+        del probe
+        torch.cuda.empty_cache()
+        # headroom for the attributes drifting under the optimizer
+        trainer = SplatTrainer(params, B, W, H, R_capacity=int(R_probe * 1.5) + 1024, device=dev)
+        rast = trainer.rast
+        target = torch.rand((B, 3, H, W), device=dev, generator=torch.Generator(device=dev).manual_seed(rank))
+
+        def step():
+            return trainer.step(views, projs, tanf, target)
     else:
         scene = scenes.avatar_cloud(P, seed=0, gaussians_per_texel=wl["gpt"])
         P = scene["means3D"].shape[0]
@@ -201,7 +222,7 @@ def main():
     P_vis = int((rast.radii > 0).sum().item())
     profile_read()  # reset accumulators
     profile_enable(("preprocess", "scan", "depth_sort", "chunk_count", "tile_scan", "ordered_scatter",
-                    "render_fwd") if a.stages else ("render_fwd",))
+                    "render_fwd", "render_bwd", "preprocess_bwd") if a.stages else ("render_fwd",))
     if dist is not None:
         dist.barrier()
     torch.cuda.synchronize(dev)
@@ -250,8 +271,10 @@ def main():
             traffic = None
 
     out = {
-        "metric": "rendered frames/sec @512x512, ~100k Gaussians" if a.config == "c2"
-                  else "rendered frames/sec @1024x1024, ~300k Gaussians",
+        "metric": ("training frames/sec (raster fwd+bwd + fused-SSIM loss) @512x512, ~100k Gaussians"
+                   if a.pipeline == "train" else
+                   "rendered frames/sec @512x512, ~100k Gaussians" if a.config == "c2"
+                   else "rendered frames/sec @1024x1024, ~300k Gaussians"),
         "value": round(fps, 2),
         "unit": "frames/s",
         "n_gpus": world,
@@ -268,8 +291,10 @@ def main():
                  "synthetic (SMPL-X-template avatar cloud, GUAVA attribute distributions, "
                  "one orbit camera per frame)"),
         "config": {"workload": workload,
-                   "pipeline": ("EHM LBS -> Gaussian assembly -> rasterize" if a.pipeline == "avatar"
-                                else "rasterize") + (" + fused refiner conv_body_first" if a.refine else ""), "gaussians": P, "image": [W, H], "channels": C,
+                   "pipeline": {"avatar": "EHM LBS -> Gaussian assembly -> rasterize",
+                                "raster": "rasterize",
+                                "train": "raster fwd -> L1 + fused SSIM -> raster bwd -> grad all-reduce -> Adam"
+                                }[a.pipeline] + (" + fused refiner conv_body_first" if a.refine else ""), "gaussians": P, "image": [W, H], "channels": C,
                    "frames_per_step_per_gpu": B, "global_batch": B * world,
                    "parallelism": f"frame-sharded x{world}",
                    "exp": "hw" if a.fast_exp else "exact-poly",
@@ -295,7 +320,7 @@ def main():
         out["deform_ms_per_step"] = round(deform_ms, 4)
     if a.stages:
         out["stage_ms_per_step"] = {k: round(v[0] / max(v[1], 1), 4) for k, v in prof.items()}
-    if rank == 0 and world == 1 and not a.no_cpu_baseline:
+    if rank == 0 and world == 1 and not a.no_cpu_baseline and a.pipeline != "train":
         out["cpu_baseline"] = cpu_baseline(scene, cams, W, H, a.cpu_seconds, avatar_inputs)
     if rank == 0:
         print(json.dumps(out), flush=True)
