@@ -532,11 +532,10 @@ void launch_tile_scan(const Dims& d, const GeomArena& g, const ImageArena& im, h
 // of the conic's quadratic form Q = a dx^2 + 2b dx dy + c dy^2 (power = -Q/2 in the blend).  Q is
 // convex (a, c > 0, ac > b^2), so the minimum is 0 if the mean lies inside, else it lies on an edge:
 // each edge is a 1-D quadratic minimised by clamping its vertex.
-__device__ __forceinline__ float rect_qmin(float a, float b, float c, float dxl, float dxh, float dyl,
-                                           float dyh) {
+__device__ __forceinline__ float rect_qmin(float a, float b, float c, float ia, float ic, float dxl, float dxh,
+                                           float dyl, float dyh) {
     if (dxl <= 0.f && dxh >= 0.f && dyl <= 0.f && dyh >= 0.f) return 0.f;
     float q = 3.0e38f;
-    const float ia = 1.0f / a, ic = 1.0f / c;
     const float xs[2] = {dxl, dxh}, ys[2] = {dyl, dyh};
 #pragma unroll
     for (int k = 0; k < 2; k++) {
@@ -550,17 +549,29 @@ __device__ __forceinline__ float rect_qmin(float a, float b, float c, float dxl,
     return q;
 }
 
+// Per-Gaussian part of the strip test, computed once per Gaussian (not once per instance):
+// (K = 2 ln(255 o), 1/a, 1/c, mode) with mode 0 = test the strips, 1 = no strip (o < 1/255:
+// alpha <= o < 1/255 at every pixel), 2 = every strip (non-finite or non-positive-definite conic).
+__device__ __forceinline__ float4 strip_pre(float4 co) {
+    const float a = co.x, b = co.y, c = co.z, o = co.w;
+    if (o < 1.0f / 255.0f) return make_float4(0.f, 0.f, 0.f, __uint_as_float(1u));
+    if (!(a > 0.f) || !(c > 0.f) || !(a * c - b * b > 0.f) || !(o <= 3.0e38f))
+        return make_float4(0.f, 0.f, 0.f, __uint_as_float(2u));
+    return make_float4(2.0f * logf(255.0f * o), 1.0f / a, 1.0f / c, __uint_as_float(0u));
+}
+
 // Strip mask of one (Gaussian, tile) instance: bit s is set unless no pixel centre of the tile's
 // s-th 16x4 strip can give alpha = min(0.99, o*exp(-Q/2)) >= 1/255, i.e. unless Q > 2 ln(255 o)
 // on the whole strip.  A cleared bit only ever removes pairs the blend skips anyway (alpha < 1/255,
 // forward.cu:362-363), so culling with it is decision-preserving; the slack (1e-4 of the form's
 // term magnitudes + 1e-3 relative) covers float rounding of both this test and the blend's power.
 // Non-finite or non-positive-definite conics keep every strip.
-__device__ __forceinline__ uint32_t strip_mask(float4 co, float2 m, int tx, int ty) {
-    const float a = co.x, b = co.y, c = co.z, o = co.w;
-    if (o < 1.0f / 255.0f) return 0u;  // alpha <= o < 1/255 at every pixel
-    if (!(a > 0.f) || !(c > 0.f) || !(a * c - b * b > 0.f) || !(o <= 3.0e38f)) return (1u << kStrips) - 1u;
-    const float K = 2.0f * logf(255.0f * o);
+__device__ __forceinline__ uint32_t strip_mask(float4 co, float4 pre, float2 m, int tx, int ty) {
+    const uint32_t mode = __float_as_uint(pre.w);
+    if (mode == 1u) return 0u;
+    if (mode == 2u) return (1u << kStrips) - 1u;
+    const float a = co.x, b = co.y, c = co.z;
+    const float K = pre.x;
     const float dxl = m.x - (float)(tx * GSR_BX + GSR_BX - 1), dxh = m.x - (float)(tx * GSR_BX);
     const float mx = fmaxf(fabsf(dxl), fabsf(dxh));
     uint32_t bits = 0;
@@ -570,7 +581,7 @@ __device__ __forceinline__ uint32_t strip_mask(float4 co, float2 m, int tx, int 
         const float dyl = m.y - (y0 + (float)(GSR_BY / kStrips - 1)), dyh = m.y - y0;
         const float my = fmaxf(fabsf(dyl), fabsf(dyh));
         const float slack = 1e-4f * (a * mx * mx + 2.f * fabsf(b) * mx * my + c * my * my) + 1e-3f * K + 1e-3f;
-        const float q = rect_qmin(a, b, c, dxl, dxh, dyl, dyh);
+        const float q = rect_qmin(a, b, c, pre.y, pre.z, dxl, dxh, dyl, dyh);
         if (!(q > K + slack)) bits |= 1u << s;
     }
     return bits;
@@ -590,6 +601,7 @@ __global__ __launch_bounds__(kChunk) void k_ordered_scatter(Dims d, GeomArena g,
     __shared__ uint2 s_rect[kChunk];
     __shared__ uint32_t s_gi[kChunk];
     __shared__ float4 s_co[kChunk];
+    __shared__ float4 s_pre[kChunk];
     __shared__ float2 s_m[kChunk];
     if (g.ctrl[kCtrlOverflow]) return;
     const int b = blockIdx.y, c = blockIdx.x;
@@ -611,7 +623,9 @@ __global__ __launch_bounds__(kChunk) void k_ordered_scatter(Dims d, GeomArena g,
         const int64_t gid = (int64_t)b * d.P + gi;
         r = g.rect[gid];
         nt = ((r.y & 0xFFFF) - (r.x & 0xFFFF)) * ((r.y >> 16) - (r.x >> 16));
-        s_co[tid] = g.conic[gid];
+        const float4 co = g.conic[gid];
+        s_co[tid] = co;
+        s_pre[tid] = strip_pre(co);
         s_m[tid] = g.means2D[gid];
     }
     uint32_t total;
@@ -648,7 +662,7 @@ __global__ __launch_bounds__(kChunk) void k_ordered_scatter(Dims d, GeomArena g,
         for (int w = 0; w < w_o; w++) lr += (uint32_t)__popcll(colm[4 * tx + w] & rowm[4 * ty + w]);
         const uint64_t below = l_o ? (~0ull >> (64 - l_o)) : 0ull;
         lr += (uint32_t)__popcll(colm[4 * tx + w_o] & rowm[4 * ty + w_o] & below);
-        bn.point_list[base[t] + lr] = s_gi[o] | (strip_mask(s_co[o], s_m[o], tx, ty) << 28);
+        bn.point_list[base[t] + lr] = s_gi[o] | (strip_mask(s_co[o], s_pre[o], s_m[o], tx, ty) << 28);
     }
 }
 
@@ -662,6 +676,121 @@ void launch_ordered_scatter(const Dims& d, const GeomArena& g, const ImageArena&
         hipFuncSetAttribute((const void*)k_ordered_scatter, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     }
     hipLaunchKernelGGL(k_ordered_scatter, dim3(d.nchunk, d.B), dim3(kChunk), lds, s, d, g, im, b);
+}
+
+// ---------------------------------------------------------------- 6. strip work list
+// The render kernels' unit of work is one 16x4 strip, and its cost is the number of list entries
+// whose strip bit is set (before early termination).  The tile-level longest-first list above
+// orders by list length in octaves, which lets strips of 10x the mean work start late and set the
+// kernel's length; this orders the strips themselves, 4 buckets per octave of survivors.
+__device__ __forceinline__ uint32_t strip_bucket(uint32_t c) {
+    if (!c) return kStripBuckets - 1;
+    const uint32_t e = 31u - __clz(c);
+    const uint32_t sub = e >= 2u ? (c >> (e - 2u)) & 3u : (c << (2u - e)) & 3u;
+    return 127u - (e * 4u + sub);
+}
+
+// One wave per tile: popcount of each strip bit over the tile's list.
+__global__ __launch_bounds__(256) void k_strip_count(Dims d, ImageArena im, BinArena bn) {
+    const int tile_g = (int)((blockIdx.x * 256u + threadIdx.x) >> 6);
+    const int lane = threadIdx.x & 63;
+    if (tile_g >= d.B * d.T) return;
+    const uint2 r = im.ranges[tile_g];
+    uint32_t c[kStrips] = {};
+    for (uint32_t i = r.x + lane; i < r.y; i += 256) {
+        uint32_t e[4];
+#pragma unroll
+        for (int u = 0; u < 4; u++) e[u] = i + 64u * u < r.y ? bn.point_list[i + 64u * u] : 0u;
+#pragma unroll
+        for (int u = 0; u < 4; u++)
+#pragma unroll
+            for (int s = 0; s < kStrips; s++) c[s] += (e[u] >> (28 + s)) & 1u;
+    }
+#pragma unroll
+    for (int s = 0; s < kStrips; s++) {
+        uint32_t v = c[s];
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
+        c[s] = v;
+    }
+    if (lane < kStrips) {
+        uint32_t v = c[0];
+#pragma unroll
+        for (int s = 1; s < kStrips; s++) v = lane == s ? c[s] : v;
+        im.strip_cnt[(int64_t)tile_g * kStrips + lane] = v;
+    }
+}
+
+// Per frame: histogram of its non-empty tiles' strips over the buckets.
+__global__ __launch_bounds__(1024) void k_strip_hist(Dims d, ImageArena im) {
+    __shared__ uint32_t h[kStripBuckets];
+    const int b = blockIdx.x;
+    for (int i = threadIdx.x; i < kStripBuckets; i += 1024) h[i] = 0;
+    __syncthreads();
+    for (int t = threadIdx.x; t < d.T; t += 1024) {
+        const int64_t tg = (int64_t)b * d.T + t;
+        if (!im.tile_count[tg]) continue;
+#pragma unroll
+        for (int s = 0; s < kStrips; s++) atomicAdd(&h[strip_bucket(im.strip_cnt[tg * kStrips + s])], 1u);
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < kStripBuckets; i += 1024) im.strip_hist[b * kStripBuckets + i] = h[i];
+}
+
+// Per frame: place its strips into the batch-wide strip list, bucket-major (most survivors first);
+// the order inside a bucket is whatever the LDS atomics give (scheduling only).
+__global__ __launch_bounds__(1024) void k_strip_place(Dims d, ImageArena im) {
+    extern __shared__ uint32_t hist[];  // [B][kStripBuckets]
+    __shared__ uint32_t cur[kStripBuckets];
+    __shared__ uint32_t before[kStripBuckets];
+    const int b = blockIdx.x;
+    for (int i = threadIdx.x; i < d.B * kStripBuckets; i += 1024) hist[i] = im.strip_hist[i];
+    __syncthreads();
+    for (int bk = threadIdx.x; bk < kStripBuckets; bk += 1024) {  // bucket totals; this frame's share before it
+        uint32_t tot = 0, mine = 0;
+        for (int f = 0; f < d.B; f++) {
+            const uint32_t v = hist[f * kStripBuckets + bk];
+            tot += v;
+            if (f < b) mine += v;
+        }
+        cur[bk] = tot;
+        before[bk] = mine;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {  // start of this frame's run in each bucket (bucket-major)
+        uint32_t acc = 0;
+        for (int bk = 0; bk < kStripBuckets; bk++) {
+            const uint32_t t = cur[bk];
+            cur[bk] = acc + before[bk];
+            acc += t;
+        }
+    }
+    __syncthreads();
+    for (int t = threadIdx.x; t < d.T; t += 1024) {
+        const int64_t tg = (int64_t)b * d.T + t;
+        if (!im.tile_count[tg]) continue;
+#pragma unroll
+        for (int s = 0; s < kStrips; s++) {
+            const uint32_t bk = strip_bucket(im.strip_cnt[tg * kStrips + s]);
+            im.strip_list[atomicAdd(&cur[bk], 1u)] = ((uint32_t)tg << 2) | (uint32_t)s;
+        }
+    }
+}
+
+void launch_strip_order(const Dims& d, const GeomArena& g, const ImageArena& im, const BinArena& b,
+                        hipStream_t s) {
+    (void)g;
+    if (d.B == 0 || d.T == 0) return;
+    const int nt = d.B * d.T;
+    hipLaunchKernelGGL(k_strip_count, dim3((nt + 3) / 4), dim3(256), 0, s, d, im, b);
+    hipLaunchKernelGGL(k_strip_hist, dim3(d.B), dim3(1024), 0, s, d, im);
+    const size_t lds = (size_t)d.B * kStripBuckets * 4;
+    static size_t attr = 0;
+    if (lds > 65536 && attr < lds) {
+        attr = lds;
+        hipFuncSetAttribute((const void*)k_strip_place, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    }
+    hipLaunchKernelGGL(k_strip_place, dim3(d.B), dim3(1024), lds, s, d, im);
 }
 
 }  // namespace gsr

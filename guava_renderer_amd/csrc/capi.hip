@@ -84,6 +84,13 @@ inline T* take(char* base, size_t& off, size_t count) {
 
 namespace gsr {
 
+// Scheduling knob read from the environment (no effect on results): GSR_PRIO_ITEMS = render_fwd
+// work items (longest first) run at raised issue priority (default 0).
+static void env_tuning(Inputs& in) {
+    static const uint32_t prio = [] { const char* e = getenv("GSR_PRIO_ITEMS"); return e ? (uint32_t)atoi(e) : 0u; }();
+    in.prio_items = prio;
+}
+
 int persistent_grid(int per_cu) {
     static int cus = 0;
     if (cus == 0) {
@@ -133,6 +140,9 @@ size_t carve_image(char* base, const Dims& d, ImageArena* im) {
     a.tile_count = take<uint32_t>(base, off, nt);
     a.work_list = take<uint32_t>(base, off, nt);
     a.lpt_hist = take<uint32_t>(base, off, (size_t)d.B * kLptBuckets);
+    a.strip_cnt = take<uint32_t>(base, off, (size_t)kStrips * nt);
+    a.strip_list = take<uint32_t>(base, off, (size_t)kStrips * nt);
+    a.strip_hist = take<uint32_t>(base, off, (size_t)d.B * kStripBuckets);
     if (im) *im = a;
     return align_up(off) + 256;
 }
@@ -159,7 +169,11 @@ int run_binning_and_render(const Dims& d, const Inputs& in, const GeomArena& g, 
     STAGE(debug, s, "chunk_count");
     { StageTimer st_(4, s); launch_tile_scan(d, g, im, s); }
     STAGE(debug, s, "tile_scan");
-    { StageTimer st_(5, s); launch_ordered_scatter(d, g, im, bn, s); }
+    {
+        StageTimer st_(5, s);
+        launch_ordered_scatter(d, g, im, bn, s);
+        launch_strip_order(d, g, im, bn, s);
+    }
     STAGE(debug, s, "ordered_scatter");
     { StageTimer st_(6, s); launch_render_fwd(d, in, g, im, bn, o, g_exact_exp != 0, s); }
     STAGE(debug, s, "render_fwd");
@@ -227,6 +241,7 @@ int gsr_forward(gsr_alloc_fn geometryBuffer, gsr_alloc_fn binningBuffer, gsr_all
         return fail(GSR_ERR_ARG, "scales/rotations or cov3D_precomp required");
 
     Inputs in{};
+    env_tuning(in);
     in.means3D = means3D; in.s_means = 0;
     in.scales = scales; in.s_scales = 0;
     in.rot = rotations; in.s_rot = 0;
@@ -285,6 +300,7 @@ int gsr_backward(int P, int D, int M, int R, const float* background, int width,
     carve_image(image_buffer, d, &im);
     carve_bin(binning_buffer, R, &bn);
     Inputs in{};
+    env_tuning(in);
     in.means3D = means3D;
     in.scales = scales;
     in.rot = rotations;
@@ -374,6 +390,7 @@ int gsr_forward_batch_refine(int B, int P, int width, int height, const float* m
     BinArena bn;
     carve_workspace(workspace, d, R_capacity, &g, &im, &bn);
     Inputs in{};
+    env_tuning(in);
     in.means3D = means3D; in.s_means = means_stride;
     in.scales = scales; in.s_scales = scales_stride;
     in.rot = rotations; in.s_rot = rot_stride;
@@ -385,7 +402,6 @@ int gsr_forward_batch_refine(int B, int P, int width, int height, const float* m
     in.bg = backgrounds; in.s_bg = bg_stride;
     in.scale_mod = scale_modifier;
     in.prefiltered = 0; in.antialiasing = antialiasing;
-    { const char* e = getenv("GSR_PRIO_ITEMS"); in.prio_items = e ? (uint32_t)atoi(e) : 0u; }
     Outputs o{out_color, out_invdepth, radii, g_render_counters, g_timeline, g_timeline_cap};
     if (refine) {
         o.rb = refine->bias;
@@ -435,6 +451,7 @@ int gsr_backward_batch(int B, int P, int width, int height, const float* means3D
     BinArena bn;
     carve_workspace(workspace, d, R_capacity, &g, &im, &bn);
     Inputs in{};
+    env_tuning(in);
     in.means3D = means3D; in.s_means = means_stride;
     in.scales = scales; in.s_scales = scales_stride;
     in.rot = rotations; in.s_rot = rot_stride;

@@ -46,6 +46,7 @@ enum FrameStat : int {
 };
 constexpr int kMaxFrames = 256;   // frames per batch (per-frame tables live in LDS)
 constexpr int kLptBuckets = 34;   // render work list: clz(list length), 33 = empty tile
+constexpr int kStripBuckets = 129;  // strip work list: 4 buckets per octave of survivors, 128 = none
 
 struct GeomArena {
     uint32_t* ctrl;       // kCtrlWords control words, then kFsWords per frame
@@ -78,6 +79,9 @@ struct ImageArena {
     uint32_t* tile_count;
     uint32_t* work_list;  // every tile of the batch, longest list first (render scheduling)
     uint32_t* lpt_hist;   // per frame: tiles per work-list bucket
+    uint32_t* strip_cnt;  // per tile x 4 strips: list entries whose strip bit is set
+    uint32_t* strip_list; // the strips of the non-empty tiles, most survivors first: tile << 2 | strip
+    uint32_t* strip_hist; // per frame: strips per kStripBuckets bucket
 };
 
 struct BinArena {
@@ -180,6 +184,9 @@ void launch_depth_sort(const Dims& d, const GeomArena& g, hipStream_t s);
 void launch_chunk_count(const Dims& d, const GeomArena& g, const ImageArena& im, hipStream_t s);
 void launch_tile_scan(const Dims& d, const GeomArena& g, const ImageArena& im, hipStream_t s);
 // depth-ordered instance emission -> point_list (index | strip mask << 28)
+// survivors per strip -> strip_cnt; strips of the non-empty tiles, most survivors first -> strip_list
+void launch_strip_order(const Dims& d, const GeomArena& g, const ImageArena& im, const BinArena& b,
+                        hipStream_t s);
 void launch_ordered_scatter(const Dims& d, const GeomArena& g, const ImageArena& im,
                             const BinArena& b, hipStream_t s);
 void launch_render_fwd(const Dims& d, const Inputs& in, const GeomArena& g, const ImageArena& im,

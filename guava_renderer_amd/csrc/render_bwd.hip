@@ -51,7 +51,7 @@ __device__ __forceinline__ void wave_transpose_reduce40(float (&v)[40], float (&
         for (int k = 0; k < 5; k++) out[k] += __shfl_xor(out[k], off);
 }
 
-// Work: the 16x4 strips of the non-empty tiles, in k_tile_scan's longest-first order, dealt to
+// Work: the 16x4 strips of the non-empty tiles, in strip_list order (most survivors first), dealt to
 // per-XCD queues exactly like render_fwd (separate counters).  One wave owns a strip (lane = pixel)
 // and replays its tile's depth-sorted list back to front from the strip's largest n_contrib,
 // taking only the Gaussians whose strip bit is set in point_list (binning's exact test that the
@@ -85,8 +85,9 @@ __global__ __launch_bounds__(GSR_TILE_PIX) void k_render_bwd(Dims d, Inputs in, 
             q_left--;
         }
         if (!q_left) break;
-        const int tile_g = (int)im.work_list[item >> 2];
-        const int strip = (int)(item & 3u);
+        const uint32_t code = im.strip_list[item];
+        const int tile_g = (int)(code >> 2);
+        const int strip = (int)(code & 3u);
         const int b = tile_g / d.T;
         const int t = tile_g - b * d.T;
         const int tx = t % d.gx, ty = t / d.gx;

@@ -168,8 +168,8 @@ void launch_refine_prepare(int n, const float* in, const float* w, int n_out, in
     hipLaunchKernelGGL(k_refine_prepare, dim3((n + 255) / 256), dim3(256), 0, s, n, in, w, n_out, keep, out);
 }
 
-// Work items, in k_tile_scan's longest-first order: the 4 strips of each non-empty tile
-// (items [0, 4*NE)), then each empty tile whole (items [4*NE, 3*NE + B*T)).  Eight queues, one per
+// Work items: the 4 strips of each non-empty tile in strip_list order, most survivors first (items
+// [0, 4*NE)), then each empty tile whole (items [4*NE, 3*NE + B*T)).  Eight queues, one per
 // XCD, take every eighth item (item = x + 8k); a wave dequeues from its own XCD's queue and, once
 // that is drained, from the others, so no counter sees more than a fraction of the traffic.
 //
@@ -177,7 +177,7 @@ void launch_refine_prepare(int n, const float* in, const float* w, int n_out, in
 // in three rotating register slots: the records and feature operand of step s+3 are loaded while
 // step s+1's alphas (the exp-heavy, transmittance-independent part) are computed and step s's
 // serial blend and MFMA accumulation run.
-template <bool EXACT, bool STATS, bool TL, bool REFINE>
+template <bool EXACT, bool STATS, bool TL, bool REFINE, int ABL = 0>
 __device__ __forceinline__ void render_fwd_body(const Dims& d, const Inputs& in, const GeomArena& g,
                                                 const ImageArena& im, const BinArena& bn,
                                                 const Outputs& o) {
@@ -217,8 +217,9 @@ __device__ __forceinline__ void render_fwd_body(const Dims& d, const Inputs& in,
         if (item < in.prio_items) __builtin_amdgcn_s_setprio(3);
         else __builtin_amdgcn_s_setprio(0);
         const uint64_t t_start = TL ? __builtin_amdgcn_s_memrealtime() : 0;
-        const int tile_g = (int)im.work_list[item >> 2];
-        const int strip = (int)(item & 3u);
+        const uint32_t code = im.strip_list[item];
+        const int tile_g = (int)(code >> 2);
+        const int strip = (int)(code & 3u);
         const int b = tile_g / d.T;
         const int t = tile_g - b * d.T;
         const int tx = t % d.gx, ty = t / d.gx;
@@ -281,7 +282,7 @@ __device__ __forceinline__ void render_fwd_body(const Dims& d, const Inputs& in,
             S##pa = pa_; S##pb = pb_;                                                               \
             S##a0 = rrec[2 * ga_]; S##a1 = rrec[2 * ga_ + 1];                                       \
             S##b0 = rrec[2 * gb_]; S##b1 = rrec[2 * gb_ + 1];                                       \
-            S##f = colors[(int64_t)(hi ? gb_ : ga_) * GSR_C + ch];                                  \
+            S##f = ABL == 2 ? 0.f : colors[(int64_t)(hi ? gb_ : ga_) * GSR_C + ch];                 \
         }
         // stage 2: the pixel-local alphas of slot S (a missing survivor has alpha 0)
 #define GSR_ALPHA(S)                                                                                \
@@ -308,8 +309,14 @@ __device__ __forceinline__ void render_fwd_body(const Dims& d, const Inputs& in,
             if (STATS || TL) n_steps += S##v ? 1 : 0;                                               \
             const auto sw_ = __builtin_amdgcn_permlane32_swap(__float_as_uint(wa_),                 \
                                                               __float_as_uint(wb_), false, false);  \
-            acc0 = __builtin_amdgcn_mfma_f32_32x32x2f32(f_, __uint_as_float(sw_[0]), acc0, 0, 0, 0); \
-            acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(f_, __uint_as_float(sw_[1]), acc1, 0, 0, 0); \
+            if (ABL == 1) {  /* timing ablation: VALU stand-in for the MFMAs */                  \
+                acc0[0] = fmaf(f_, __uint_as_float(sw_[0]), acc0[0]);                               \
+                acc1[0] = fmaf(f_, __uint_as_float(sw_[1]), acc1[0]);                               \
+            } else {                                                                                \
+                const float fa_ = ABL == 2 ? 1.0f : f_;  /* timing ablation: no feature operand */  \
+                acc0 = __builtin_amdgcn_mfma_f32_32x32x2f32(fa_, __uint_as_float(sw_[0]), acc0, 0, 0, 0); \
+                acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(fa_, __uint_as_float(sw_[1]), acc1, 0, 0, 0); \
+            }                                                                                       \
         }
 #define GSR_SLOT(S) bool S##v, S##hb; int S##pa, S##pb; float4 S##a0, S##a1, S##b0, S##b1; \
         float S##f, S##al, S##bl, S##ai, S##bi;
@@ -376,6 +383,14 @@ __global__ __launch_bounds__(GSR_TILE_PIX) void k_render_fwd(Dims d, Inputs in, 
     render_fwd_body<EXACT, STATS, TL, false>(d, in, g, im, bn, o);
 }
 
+// Timing ablations of the production kernel (GSR_RENDER_ABLATE=1: VALU stand-in for the MFMAs,
+// 2: no feature loads).  Wrong images by construction; for attributing render_fwd time only.
+template <int ABL>
+__global__ __launch_bounds__(GSR_TILE_PIX) void k_render_fwd_ablate(Dims d, Inputs in, GeomArena g,
+                                                                    ImageArena im, BinArena bn, Outputs o) {
+    render_fwd_body<true, false, false, false, ABL>(d, in, g, im, bn, o);
+}
+
 // The refiner-head variant: the epilogue's extra stores would raise the register count past the
 // 4-waves-per-SIMD budget of the blend loop; pin the budget (the few extra live values of the
 // epilogue spill instead).
@@ -387,6 +402,7 @@ __global__ __launch_bounds__(GSR_TILE_PIX) __attribute__((amdgpu_waves_per_eu(4)
 
 void launch_render_fwd(const Dims& d, const Inputs& in, const GeomArena& g, const ImageArena& im,
                        const BinArena& b, const Outputs& o, bool exact, hipStream_t s) {
+    static const int ablate = [] { const char* e = getenv("GSR_RENDER_ABLATE"); return e ? atoi(e) : 0; }();
     const int nwaves = d.B * d.T * kStrips;  // upper bound of the work items
     if (nwaves == 0) return;
     const int grid = min((nwaves + 3) / 4, persistent_grid(8));
@@ -398,6 +414,8 @@ void launch_render_fwd(const Dims& d, const Inputs& in, const GeomArena& g, cons
         if (exact) hipLaunchKernelGGL((k_render_fwd_refine<true>), gr, bl, 0, s, d, in, g, im, b, o);
         else hipLaunchKernelGGL((k_render_fwd_refine<false>), gr, bl, 0, s, d, in, g, im, b, o);
     }
+    else if (ablate == 1) hipLaunchKernelGGL((k_render_fwd_ablate<1>), gr, bl, 0, s, d, in, g, im, b, o);
+    else if (ablate == 2) hipLaunchKernelGGL((k_render_fwd_ablate<2>), gr, bl, 0, s, d, in, g, im, b, o);
     else { if (exact) GSR_LAUNCH(true, false, false); else GSR_LAUNCH(false, false, false); }
 #undef GSR_LAUNCH
 }
