@@ -380,26 +380,28 @@ void launch_depth_sort(const Dims& d, const GeomArena& g, hipStream_t s) {
 }
 
 // ---------------------------------------------------------------- 3. instance count table
-// Tile histogram of one chunk of kChunk depth-ordered Gaussians: each rect adds +1/-1 at its four
+// Tile histogram of one chunk of d.chunk depth-ordered Gaussians: each rect adds +1/-1 at its four
 // corners of a (gx+1) x (gy+1) difference array in LDS; a 2-D prefix sum gives the per-tile counts.
 __global__ __launch_bounds__(kScanBlock) void k_chunk_count(Dims d, GeomArena g) {
     extern __shared__ int diff[];  // (gx+1)*(gy+1)
     if (g.ctrl[kCtrlOverflow]) return;
     const int b = blockIdx.y, c = blockIdx.x;
     const uint32_t V = g.fstat[kFsWords * b + kFsVisible];
-    if ((uint32_t)c * kChunk >= V) return;
+    if ((uint32_t)c * d.chunk >= V) return;
     const int W1 = d.gx + 1, H1 = d.gy + 1;
     for (int k = threadIdx.x; k < W1 * H1; k += kScanBlock) diff[k] = 0;
     __syncthreads();
-    const uint32_t j = (uint32_t)c * kChunk + threadIdx.x;
-    if (j < V) {
-        const uint32_t gi = g.order[(int64_t)b * d.P + j];
-        const uint2 r = g.rect[(int64_t)b * d.P + gi];
-        const int x0 = r.x & 0xFFFF, y0 = r.x >> 16, x1 = r.y & 0xFFFF, y1 = r.y >> 16;
-        atomicAdd(&diff[y0 * W1 + x0], 1);
-        atomicAdd(&diff[y0 * W1 + x1], -1);
-        atomicAdd(&diff[y1 * W1 + x0], -1);
-        atomicAdd(&diff[y1 * W1 + x1], 1);
+    for (int k = 0; k < d.chunk; k += kScanBlock) {
+        const uint32_t j = (uint32_t)c * d.chunk + k + threadIdx.x;
+        if (j < V) {
+            const uint32_t gi = g.order[(int64_t)b * d.P + j];
+            const uint2 r = g.rect[(int64_t)b * d.P + gi];
+            const int x0 = r.x & 0xFFFF, y0 = r.x >> 16, x1 = r.y & 0xFFFF, y1 = r.y >> 16;
+            atomicAdd(&diff[y0 * W1 + x0], 1);
+            atomicAdd(&diff[y0 * W1 + x1], -1);
+            atomicAdd(&diff[y1 * W1 + x0], -1);
+            atomicAdd(&diff[y1 * W1 + x1], 1);
+        }
     }
     __syncthreads();
     for (int y = threadIdx.x; y < d.gy; y += kScanBlock) {  // prefix along x
@@ -421,7 +423,7 @@ __global__ __launch_bounds__(kScanBlock) void k_column_scan(Dims d, GeomArena g,
     if (t >= d.T) return;
     uint32_t acc = 0;
     if (!g.ctrl[kCtrlOverflow]) {
-        const int nc = (int)((g.fstat[kFsWords * b + kFsVisible] + kChunk - 1) / kChunk);
+        const int nc = (int)((g.fstat[kFsWords * b + kFsVisible] + d.chunk - 1) / d.chunk);
         uint32_t* col = g.table + (int64_t)b * d.nchunk * d.T + t;
         int c = 0;
         for (; c + 4 <= nc; c += 4) {
@@ -588,82 +590,105 @@ __device__ __forceinline__ uint32_t strip_mask(float4 co, float4 pre, float2 m, 
 }
 
 // ---------------------------------------------------------------- 5. ordered scatter
-// One workgroup per chunk of kChunk depth-ordered Gaussians (one per thread, "slot").  The chunk's
-// instances are spread evenly over the threads (binary search in the slots' inclusive tile-count
-// scan), so one huge splat does not serialise a wave.  An instance (slot o, tile t) lands at
-//     ranges[t].x + table[chunk][t] + #(slots o' < o whose rect covers t)
-// and the last term is a popcount of per-wave ballots of "rect covers tile column tx" and "... row
-// ty" (4 x 64-bit masks per column and per row, in LDS).
-__global__ __launch_bounds__(kChunk) void k_ordered_scatter(Dims d, GeomArena g, ImageArena im, BinArena bn) {
+// One workgroup per chunk of d.chunk depth-ordered Gaussians (one count-table row), in d.chunk/kSlots
+// passes of kSlots Gaussians (one per thread, "slot").  A pass spreads its instances evenly over the
+// threads (binary search in the slots' inclusive tile-count scan), so one huge splat does not
+// serialise a wave.  An instance (slot o, tile t) lands at
+//     base[t] + #(slots o' < o of this pass whose rect covers t)
+// with base[t] = ranges[t].x + table[chunk][t] + the pass's earlier slots covering t; the second
+// term is a popcount of per-wave ballots of "rect covers tile column tx" and "... row ty" (4 x
+// 64-bit masks per column and per row, in LDS), and base[] advances by the pass's per-tile totals.
+// The (chunk x tile) table and the per-workgroup base[] load shrink with the chunk, not the pass.
+template <int ABL>  // timing ablations (GSR_SCATTER_ABLATE): 1 = no strip test, 2 = no list store
+__global__ __launch_bounds__(kSlots) void k_ordered_scatter(Dims d, GeomArena g, ImageArena im, BinArena bn) {
+    uint32_t sink = 0;
     extern __shared__ uint64_t masks[];  // colm[gx][4], rowm[gy][4], then uint32 tile bases[T]
-    __shared__ uint32_t s_pref[kChunk];
-    __shared__ uint32_t s_sh[kChunk / 64 + 1];
-    __shared__ uint2 s_rect[kChunk];
-    __shared__ uint32_t s_gi[kChunk];
-    __shared__ float4 s_co[kChunk];
-    __shared__ float4 s_pre[kChunk];
-    __shared__ float2 s_m[kChunk];
+    __shared__ uint32_t s_pref[kSlots];
+    __shared__ uint32_t s_sh[kSlots / 64 + 1];
+    __shared__ uint2 s_rect[kSlots];
+    __shared__ uint32_t s_gi[kSlots];
+    __shared__ float4 s_co[kSlots];
+    __shared__ float4 s_pre[kSlots];
+    __shared__ float2 s_m[kSlots];
     if (g.ctrl[kCtrlOverflow]) return;
     const int b = blockIdx.y, c = blockIdx.x;
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     const uint32_t V = g.fstat[kFsWords * b + kFsVisible];
-    if ((uint32_t)c * kChunk >= V) return;
+    if ((uint32_t)c * d.chunk >= V) return;
     uint64_t* colm = masks;
     uint64_t* rowm = masks + 4 * d.gx;
     uint32_t* base = (uint32_t*)(masks + 4 * (d.gx + d.gy));
     // list position of this chunk's first instance in every tile of the frame
     const uint32_t* tbl = g.table + ((int64_t)b * d.nchunk + c) * d.T;
     const uint2* rg = im.ranges + (int64_t)b * d.T;
-    for (int t = tid; t < d.T; t += kChunk) base[t] = rg[t].x + tbl[t];
-    const uint32_t j = (uint32_t)c * kChunk + tid;
-    uint32_t gi = 0, nt = 0;
-    uint2 r = make_uint2(0u, 0u);
-    if (j < V) {
-        gi = g.order[(int64_t)b * d.P + j];
-        const int64_t gid = (int64_t)b * d.P + gi;
-        r = g.rect[gid];
-        nt = ((r.y & 0xFFFF) - (r.x & 0xFFFF)) * ((r.y >> 16) - (r.x >> 16));
-        const float4 co = g.conic[gid];
-        s_co[tid] = co;
-        s_pre[tid] = strip_pre(co);
-        s_m[tid] = g.means2D[gid];
-    }
-    uint32_t total;
-    s_pref[tid] = block_excl_scan<uint32_t, kChunk>(nt, &total, s_sh) + nt;
-    s_rect[tid] = r;
-    s_gi[tid] = gi;
-    const int x0 = r.x & 0xFFFF, y0 = r.x >> 16, x1 = r.y & 0xFFFF, y1 = r.y >> 16;
-    for (int x = 0; x < d.gx; x++) {
-        const uint64_t m = __ballot(nt && x >= x0 && x < x1);
-        if (lane == 0) colm[4 * x + wv] = m;
-    }
-    for (int y = 0; y < d.gy; y++) {
-        const uint64_t m = __ballot(nt && y >= y0 && y < y1);
-        if (lane == 0) rowm[4 * y + wv] = m;
-    }
-    __syncthreads();
-    for (uint32_t q = tid; q < total; q += kChunk) {
-        int lo = 0, hi = kChunk - 1;  // first slot whose inclusive count exceeds q
-#pragma unroll
-        for (int step = 0; step < 8; step++) {
-            const int mid = (lo + hi) >> 1;
-            if (s_pref[mid] > q) hi = mid; else lo = mid + 1;
+    for (int t = tid; t < d.T; t += kSlots) base[t] = rg[t].x + tbl[t];
+    for (int pass = 0; pass < d.chunk / kSlots; pass++) {
+        const uint32_t j0 = (uint32_t)c * d.chunk + (uint32_t)pass * kSlots;
+        if (j0 >= V) break;  // uniform
+        const uint32_t j = j0 + tid;
+        uint32_t gi = 0, nt = 0;
+        uint2 r = make_uint2(0u, 0u);
+        if (j < V) {
+            gi = g.order[(int64_t)b * d.P + j];
+            const int64_t gid = (int64_t)b * d.P + gi;
+            r = g.rect[gid];
+            nt = ((r.y & 0xFFFF) - (r.x & 0xFFFF)) * ((r.y >> 16) - (r.x >> 16));
+            const float4 co = g.conic[gid];
+            s_co[tid] = co;
+            s_pre[tid] = strip_pre(co);
+            s_m[tid] = g.means2D[gid];
         }
-        const int o = lo;
-        const uint32_t k = q - (o ? s_pref[o - 1] : 0u);
-        const uint2 ro = s_rect[o];
-        const int ox0 = ro.x & 0xFFFF, oy0 = ro.x >> 16, ow = (ro.y & 0xFFFF) - ox0;
-        // k / ow in float: exact, the quotient's fraction is >= 0.5/ow from an integer
-        const int dy = (int)(((float)k + 0.5f) * __builtin_amdgcn_rcpf((float)ow));
-        const int ty = oy0 + dy, tx = ox0 + (int)k - dy * ow;
-        const int t = ty * d.gx + tx;
-        const int w_o = o >> 6, l_o = o & 63;
-        uint32_t lr = 0;
-        for (int w = 0; w < w_o; w++) lr += (uint32_t)__popcll(colm[4 * tx + w] & rowm[4 * ty + w]);
-        const uint64_t below = l_o ? (~0ull >> (64 - l_o)) : 0ull;
-        lr += (uint32_t)__popcll(colm[4 * tx + w_o] & rowm[4 * ty + w_o] & below);
-        bn.point_list[base[t] + lr] = s_gi[o] | (strip_mask(s_co[o], s_pre[o], s_m[o], tx, ty) << 28);
+        uint32_t total;
+        s_pref[tid] = block_excl_scan<uint32_t, kSlots>(nt, &total, s_sh) + nt;  // (barriers inside)
+        s_rect[tid] = r;
+        s_gi[tid] = gi;
+        const int x0 = r.x & 0xFFFF, y0 = r.x >> 16, x1 = r.y & 0xFFFF, y1 = r.y >> 16;
+        for (int x = 0; x < d.gx; x++) {
+            const uint64_t m = __ballot(nt && x >= x0 && x < x1);
+            if (lane == 0) colm[4 * x + wv] = m;
+        }
+        for (int y = 0; y < d.gy; y++) {
+            const uint64_t m = __ballot(nt && y >= y0 && y < y1);
+            if (lane == 0) rowm[4 * y + wv] = m;
+        }
+        __syncthreads();
+        for (uint32_t q = tid; q < total; q += kSlots) {
+            int lo = 0, hi = kSlots - 1;  // first slot whose inclusive count exceeds q
+#pragma unroll
+            for (int step = 0; step < 8; step++) {
+                const int mid = (lo + hi) >> 1;
+                if (s_pref[mid] > q) hi = mid; else lo = mid + 1;
+            }
+            const int o = lo;
+            const uint32_t k = q - (o ? s_pref[o - 1] : 0u);
+            const uint2 ro = s_rect[o];
+            const int ox0 = ro.x & 0xFFFF, oy0 = ro.x >> 16, ow = (ro.y & 0xFFFF) - ox0;
+            // k / ow in float: exact, the quotient's fraction is >= 0.5/ow from an integer
+            const int dy = (int)(((float)k + 0.5f) * __builtin_amdgcn_rcpf((float)ow));
+            const int ty = oy0 + dy, tx = ox0 + (int)k - dy * ow;
+            const int t = ty * d.gx + tx;
+            const int w_o = o >> 6, l_o = o & 63;
+            uint32_t lr = 0;
+            for (int w = 0; w < w_o; w++) lr += (uint32_t)__popcll(colm[4 * tx + w] & rowm[4 * ty + w]);
+            const uint64_t below = l_o ? (~0ull >> (64 - l_o)) : 0ull;
+            lr += (uint32_t)__popcll(colm[4 * tx + w_o] & rowm[4 * ty + w_o] & below);
+            const uint32_t sm = (ABL & 1) ? 0xFu : strip_mask(s_co[o], s_pre[o], s_m[o], tx, ty);
+            if (ABL & 2) sink += base[t] + lr + sm;
+            else bn.point_list[base[t] + lr] = s_gi[o] | (sm << 28);
+        }
+        if ((pass + 1) * kSlots < d.chunk && j0 + kSlots < V) {  // uniform: advance base[] past this pass
+            __syncthreads();
+            for (int t = tid; t < d.T; t += kSlots) {
+                const int tx = t % d.gx, ty = t / d.gx;
+                uint32_t n = 0;
+#pragma unroll
+                for (int w = 0; w < kSlots / 64; w++) n += (uint32_t)__popcll(colm[4 * tx + w] & rowm[4 * ty + w]);
+                base[t] += n;
+            }
+            __syncthreads();
+        }
     }
+    if ((ABL & 2) && sink == 0xDEADBEEFu) bn.point_list[0] = sink;
 }
 
 void launch_ordered_scatter(const Dims& d, const GeomArena& g, const ImageArena& im,
@@ -673,9 +698,16 @@ void launch_ordered_scatter(const Dims& d, const GeomArena& g, const ImageArena&
     static size_t attr = 0;
     if (lds > 65536 && attr < lds) {
         attr = lds;
-        hipFuncSetAttribute((const void*)k_ordered_scatter, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        for (const void* f : {(const void*)k_ordered_scatter<0>, (const void*)k_ordered_scatter<1>,
+                              (const void*)k_ordered_scatter<2>, (const void*)k_ordered_scatter<3>})
+            hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     }
-    hipLaunchKernelGGL(k_ordered_scatter, dim3(d.nchunk, d.B), dim3(kChunk), lds, s, d, g, im, b);
+    static const int abl = [] { const char* e = getenv("GSR_SCATTER_ABLATE"); return e ? atoi(e) : 0; }();
+    const dim3 gr(d.nchunk, d.B), bl(kSlots);
+    if (abl == 1) hipLaunchKernelGGL(k_ordered_scatter<1>, gr, bl, lds, s, d, g, im, b);
+    else if (abl == 2) hipLaunchKernelGGL(k_ordered_scatter<2>, gr, bl, lds, s, d, g, im, b);
+    else if (abl == 3) hipLaunchKernelGGL(k_ordered_scatter<3>, gr, bl, lds, s, d, g, im, b);
+    else hipLaunchKernelGGL(k_ordered_scatter<0>, gr, bl, lds, s, d, g, im, b);
 }
 
 // ---------------------------------------------------------------- 6. strip work list

@@ -17,7 +17,7 @@ constexpr int kScanBlock = 256;       // Gaussians per preprocess / binning work
 constexpr int kSortSmallCap = 2048;   // keys per segment sorted by the 256-thread LDS sort
 constexpr int kSortLargeCap = 8192;   // keys per segment sorted by the 1024-thread LDS sort
 constexpr int kTinyBucket = 64;       // depth buckets up to this size are ranked in place
-constexpr int kChunk = 256;           // depth-ordered Gaussians per instance-count table row
+constexpr int kSlots = 256;           // k_ordered_scatter: Gaussians per pass (one per thread)
 constexpr int kRenderBatch = 64;      // Gaussians staged in LDS per render_bwd round
 constexpr int kStrips = 4;            // 16x4 pixel strips per 16x16 tile (one render wave each)
 
@@ -93,7 +93,8 @@ struct BinArena {
 struct Dims {
     int B, P, W, H, gx, gy, T, nblk;  // nblk: scan blocks per frame
     int NB;                           // depth buckets per frame (power of two)
-    int nchunk;                       // kChunk-Gaussian rows of the count table per frame
+    int chunk;                        // depth-ordered Gaussians per instance-count table row
+    int nchunk;                       // rows of the count table per frame
 };
 
 inline Dims make_dims(int B, int P, int W, int H) {
@@ -106,7 +107,10 @@ inline Dims make_dims(int B, int P, int W, int H) {
     int nb = 64;
     while (nb < P / 8 && nb < (1 << 20)) nb <<= 1;
     d.NB = nb;
-    d.nchunk = (P + kChunk - 1) / kChunk;
+    // count-table rows: kSlots Gaussians (one scatter pass) up to 1024 tiles; beyond, the dense
+    // (row x tile) table and each row's base[] load outweigh the extra passes (1024-Gaussian rows)
+    d.chunk = d.T > 1024 ? 4 * kSlots : kSlots;
+    d.nchunk = (P + d.chunk - 1) / d.chunk;
     return d;
 }
 
