@@ -13,8 +13,8 @@
 //
 // Kernels (all B frames per launch):
 //   k_lbs_rodrigues  B*J threads      axis-angle -> R, pose feature R - I
-//   k_lbs_blend      3V x B/8         v_shaped = template + shapedirs.betas, v_posed = v_shaped +
-//                                     posedirs.feature: the bases are streamed once per 8 frames
+//   k_lbs_blend      3V/64 x B/16 WGs v_shaped = template + shapedirs.betas, v_posed = v_shaped +
+//                                     posedirs.feature: the bases are streamed once per 16 frames
 //                                     (HBM-bound: 4*(NB + 9(J-1)) bytes per vertex coordinate)
 //   k_lbs_joints     J x B workgroups J_regressor . v_shaped (+ joints_offset)
 //   k_lbs_chain      B waves          the kinematic chain (J sequential 4x4 products) in LDS
@@ -30,7 +30,8 @@
 
 namespace gsr {
 
-constexpr int kLbsFrames = 8;  // frames per k_lbs_blend thread (accumulators per thread)
+constexpr int kLbsFrames = 16;  // frames per k_lbs_blend workgroup (accumulators per thread)
+constexpr int kLbsSplit = 4;    // k_lbs_blend waves per workgroup, each an interleaved slice of k
 
 struct Parents {
     int8_t p[GSR_LBS_MAX_JOINTS];
@@ -72,18 +73,51 @@ __global__ void k_lbs_rodrigues(int B, int J, const float* __restrict__ pose, in
     }
 }
 
+// acc[f] += sum over this wave's k-slice (k = w mod kLbsSplit, ascending) of coef[k][f] * base[k][m],
+// kLbsBatch loads of the k-major base issued before their FMAs (enough bytes in flight to stream
+// from HBM with ~4 waves per SIMD).
+constexpr int kLbsBatch = 16;
+__device__ __forceinline__ void lbs_stream(const float* __restrict__ base, int M, int m, int K, int w,
+                                           const float* coef, float (&acc)[kLbsFrames]) {
+    for (int k0 = w; k0 < K; k0 += kLbsSplit * kLbsBatch) {
+        float v[kLbsBatch];
+#pragma unroll
+        for (int u = 0; u < kLbsBatch; u++) {
+            const int k = k0 + u * kLbsSplit;
+            v[u] = k < K ? base[(int64_t)k * M + m] : 0.f;
+        }
+#pragma unroll
+        for (int u = 0; u < kLbsBatch; u++) {
+            const int k = k0 + u * kLbsSplit;
+            if (k >= K) break;
+            const float4* c = reinterpret_cast<const float4*>(&coef[k * kLbsFrames]);
+#pragma unroll
+            for (int q = 0; q < kLbsFrames / 4; q++) {
+                const float4 cq = c[q];
+                acc[4 * q] = fmaf(cq.x, v[u], acc[4 * q]); acc[4 * q + 1] = fmaf(cq.y, v[u], acc[4 * q + 1]);
+                acc[4 * q + 2] = fmaf(cq.z, v[u], acc[4 * q + 2]); acc[4 * q + 3] = fmaf(cq.w, v[u], acc[4 * q + 3]);
+            }
+        }
+    }
+}
+
 // v_shaped = v_template + blend_shapes(betas, shapedirs); v_posed = pose_offsets + v_shaped
-// (lbs.py:186,201,210 / :305,314).  One thread per vertex coordinate m of kLbsFrames frames; the
-// frame coefficients sit in LDS and the k-major bases are read coalesced, once per frame group.
-__global__ __launch_bounds__(256) void k_lbs_blend(int B, int M, int NB, int NP,
-                                                   const float* __restrict__ vt, int64_t vt_stride,
-                                                   const float* __restrict__ betas,
-                                                   const float* __restrict__ sd_t,
-                                                   const float* __restrict__ feat,
-                                                   const float* __restrict__ pd,
-                                                   float* __restrict__ v_shaped,
-                                                   float* __restrict__ v_posed) {
-    extern __shared__ float coef[];  // [(NB + NP)][kLbsFrames]
+// (lbs.py:186,201,210 / :305,314): a [3V x K] x [K x B] product streamed from HBM.  A workgroup
+// owns 64 vertex coordinates (lane = coordinate) of kLbsFrames frames; its kLbsSplit waves take
+// interleaved slices of k (k = w mod kLbsSplit), so each coordinate's K-long stream has 4 waves of
+// loads in flight instead of one serial chain, and the slice sums are added in slice order through
+// LDS (deterministic).  The frame coefficients sit in LDS (broadcast reads); the k-major bases are
+// read coalesced, once per frame group.
+__global__ __launch_bounds__(64 * kLbsSplit) void k_lbs_blend(int B, int M, int NB, int NP,
+                                                              const float* __restrict__ vt, int64_t vt_stride,
+                                                              const float* __restrict__ betas,
+                                                              const float* __restrict__ sd_t,
+                                                              const float* __restrict__ feat,
+                                                              const float* __restrict__ pd,
+                                                              float* __restrict__ v_shaped,
+                                                              float* __restrict__ v_posed) {
+    extern __shared__ float4 lds4[];  // coef [(NB + NP)][kLbsFrames], then the slice reduction
+    float* coef = reinterpret_cast<float*>(lds4);
     const int b0 = blockIdx.y * kLbsFrames;
     const int nk = NB + NP;
     for (int idx = threadIdx.x; idx < nk * kLbsFrames; idx += blockDim.x) {
@@ -94,46 +128,66 @@ __global__ __launch_bounds__(256) void k_lbs_blend(int B, int M, int NB, int NP,
         coef[idx] = v;
     }
     __syncthreads();
-    const int m = blockIdx.x * blockDim.x + threadIdx.x;
-    if (m >= M) return;
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int m = blockIdx.x * 64 + lane;
+    const bool ok = m < M;
     const int nf = min(kLbsFrames, B - b0);
-    float acc[kLbsFrames];
+    float as[kLbsFrames], ap[kLbsFrames];
 #pragma unroll
-    for (int f = 0; f < kLbsFrames; f++) acc[f] = 0.f;
-    for (int k = 0; k < NB; k++) {
-        const float s = sd_t[(int64_t)k * M + m];
-        const float4 c0 = *reinterpret_cast<const float4*>(&coef[k * kLbsFrames]);
-        const float4 c1 = *reinterpret_cast<const float4*>(&coef[k * kLbsFrames + 4]);
-        acc[0] = fmaf(c0.x, s, acc[0]); acc[1] = fmaf(c0.y, s, acc[1]);
-        acc[2] = fmaf(c0.z, s, acc[2]); acc[3] = fmaf(c0.w, s, acc[3]);
-        acc[4] = fmaf(c1.x, s, acc[4]); acc[5] = fmaf(c1.y, s, acc[5]);
-        acc[6] = fmaf(c1.z, s, acc[6]); acc[7] = fmaf(c1.w, s, acc[7]);
+    for (int f = 0; f < kLbsFrames; f++) { as[f] = 0.f; ap[f] = 0.f; }
+    if (ok) {
+        lbs_stream(sd_t, M, m, NB, w, coef, as);
+        lbs_stream(pd, M, m, NP, w, coef + NB * kLbsFrames, ap);
     }
+    // slice reduction through LDS: red[w][f][lane]
+    float* red = coef;
+    __syncthreads();  // coefficients no longer needed
+#pragma unroll
+    for (int f = 0; f < kLbsFrames; f++) red[(w * kLbsFrames + f) * 64 + lane] = as[f];
+    __syncthreads();
     float vs[kLbsFrames];
 #pragma unroll
-    for (int f = 0; f < kLbsFrames; f++) {
-        const int b = b0 + f;
-        vs[f] = 0.f;
-        if (f < nf) {
-            const float tv = vt[(int64_t)b * vt_stride + m];
-            vs[f] = NB > 0 ? tv + acc[f] : tv;
-            v_shaped[(int64_t)b * M + m] = vs[f];
-        }
-        acc[f] = 0.f;
-    }
-    for (int k = 0; k < NP; k++) {
-        const float p = pd[(int64_t)k * M + m];
-        const float4 c0 = *reinterpret_cast<const float4*>(&coef[(NB + k) * kLbsFrames]);
-        const float4 c1 = *reinterpret_cast<const float4*>(&coef[(NB + k) * kLbsFrames + 4]);
-        acc[0] = fmaf(c0.x, p, acc[0]); acc[1] = fmaf(c0.y, p, acc[1]);
-        acc[2] = fmaf(c0.z, p, acc[2]); acc[3] = fmaf(c0.w, p, acc[3]);
-        acc[4] = fmaf(c1.x, p, acc[4]); acc[5] = fmaf(c1.y, p, acc[5]);
-        acc[6] = fmaf(c1.z, p, acc[6]); acc[7] = fmaf(c1.w, p, acc[7]);
-    }
-    if (!v_posed) return;  // blend_shapes + joints only (gsr_blend_joints)
+    for (int f = 0; f < kLbsFrames; f++) vs[f] = 0.f;
+    if (w == 0) {
 #pragma unroll
-    for (int f = 0; f < kLbsFrames; f++)
-        if (f < nf) v_posed[(int64_t)(b0 + f) * M + m] = acc[f] + vs[f];
+        for (int f = 0; f < kLbsFrames; f++) {
+            float acc = red[f * 64 + lane];
+            for (int u = 1; u < kLbsSplit; u++) acc += red[(u * kLbsFrames + f) * 64 + lane];
+            const int b = b0 + f;
+            if (ok && f < nf) {
+                const float tv = vt[(int64_t)b * vt_stride + m];
+                vs[f] = NB > 0 ? tv + acc : tv;
+                v_shaped[(int64_t)b * M + m] = vs[f];
+            }
+        }
+    }
+    if (!v_posed) return;  // blend_shapes + joints only (gsr_blend_joints); uniform
+    __syncthreads();
+#pragma unroll
+    for (int f = 0; f < kLbsFrames; f++) red[(w * kLbsFrames + f) * 64 + lane] = ap[f];
+    __syncthreads();
+    if (w == 0) {
+#pragma unroll
+        for (int f = 0; f < kLbsFrames; f++) {
+            float acc = red[f * 64 + lane];
+            for (int u = 1; u < kLbsSplit; u++) acc += red[(u * kLbsFrames + f) * 64 + lane];
+            if (ok && f < nf) v_posed[(int64_t)(b0 + f) * M + m] = acc + vs[f];
+        }
+    }
+}
+
+static size_t lbs_blend_lds(int NB, int NP) {
+    const size_t coef = sizeof(float) * (size_t)(NB + NP) * kLbsFrames;
+    const size_t red = sizeof(float) * (size_t)kLbsSplit * kLbsFrames * 64;
+    return coef > red ? coef : red;
+}
+
+static void lbs_blend_attr(size_t lds) {
+    static size_t attr = 0;
+    if (lds > 65536 && attr < lds) {
+        attr = lds;
+        hipFuncSetAttribute((const void*)k_lbs_blend, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    }
 }
 
 // vertices2joints (lbs.py:335-352): J[b,j,:] = sum_v J_regressor[j,v] v_shaped[b,v,:], plus
@@ -493,9 +547,10 @@ int gsr_lbs(int B, int V, int J, int NB, const float* v_template, int64_t v_temp
     hipLaunchKernelGGL(k_lbs_rodrigues, dim3((B * J + 255) / 256), dim3(256), 0, s, B, J, pose,
                        pose2rot, a.rot, a.feat);
     if (int rc = hip_check("lbs_rodrigues")) return rc;
-    const size_t lds = sizeof(float) * (size_t)(NB + NP) * kLbsFrames;
+    const size_t lds = lbs_blend_lds(NB, NP);
     if (lds > 160 * 1024) return api_fail(GSR_ERR_ARG, "gsr_lbs: NB + 9(J-1) too large for LDS");
-    hipLaunchKernelGGL(k_lbs_blend, dim3((M + 255) / 256, (B + kLbsFrames - 1) / kLbsFrames), dim3(256),
+    lbs_blend_attr(lds);
+    hipLaunchKernelGGL(k_lbs_blend, dim3((M + 63) / 64, (B + kLbsFrames - 1) / kLbsFrames), dim3(64 * kLbsSplit),
                        lds, s, B, M, NB, NP, v_template, v_template_stride, betas, shapedirs_t,
                        a.feat, posedirs, vs, a.vp);
     if (int rc = hip_check("lbs_blend")) return rc;
@@ -520,11 +575,12 @@ int gsr_blend_joints(int B, int V, int J, int NB, const float* v_template, int64
     if (betas && (NB <= 0 || !shapedirs_t))
         return api_fail(GSR_ERR_ARG, "gsr_blend_joints: betas need NB > 0 and shapedirs");
     if (!betas) NB = 0;
-    const size_t lds = sizeof(float) * (size_t)NB * kLbsFrames;
+    const size_t lds = lbs_blend_lds(NB, 0);
     if (lds > 160 * 1024) return api_fail(GSR_ERR_ARG, "gsr_blend_joints: NB too large for LDS");
+    lbs_blend_attr(lds);
     hipStream_t s = (hipStream_t)stream;
     const int M = V * 3;
-    hipLaunchKernelGGL(k_lbs_blend, dim3((M + 255) / 256, (B + kLbsFrames - 1) / kLbsFrames), dim3(256),
+    hipLaunchKernelGGL(k_lbs_blend, dim3((M + 63) / 64, (B + kLbsFrames - 1) / kLbsFrames), dim3(64 * kLbsSplit),
                        lds, s, B, M, NB, 0, v_template, v_template_stride, betas, shapedirs_t,
                        nullptr, nullptr, v_shaped, nullptr);
     if (int rc = hip_check("blend_shapes")) return rc;
