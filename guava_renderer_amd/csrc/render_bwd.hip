@@ -5,50 +5,65 @@
 //    marked as reaching the strip, from the strip's largest n_contrib instead of the tile list end;
 //  * the 32-channel "accumulated colour behind" recurrence is carried as its dot product with
 //    dL/dpixel (linear, so sum_ch (c - accum_rec_ch) dL_ch == g - accum_dot with g = f . dL);
-//  * per (wave, Gaussian) the 39 per-Gaussian gradient terms are reduced across the 64 pixels of
-//    the wave with a transpose-reduction (40 -> 5 values per lane in 3 halving rounds + a 3-round
-//    all-reduce) and issued as ONE 40-lane atomic instruction, instead of 39 atomics per pixel.
+//  * dL/dcolor of a Gaussian is sum_px w_px dL_px (w = alpha T): a contraction over the strip's 64
+//    pixels, done on the matrix cores for batches of 32 active Gaussians -- each lane parks its
+//    pixel's weight in wave-private LDS, and at the end of a batch 32 v_mfma_f32_32x32x2_f32 (two
+//    pixels per k-step) give the [32 channels x 32 Gaussians] block, issued as 16 atomic
+//    instructions, instead of 32 multiplies and a 32-channel cross-lane reduction per Gaussian;
+//  * the other 7 per-Gaussian terms (mean2D, conic, opacity, inverse depth) are reduced across the
+//    64 pixels with an 8-wide transpose-reduction and issued as ONE 7-lane atomic instruction.
 #include "gsr_internal.h"
 
 namespace gsr {
 
-// Reduce v[40] across the 64 lanes; lane l ends holding the sum of component
-// ((l>>5)&1)*20 + ((l>>4)&1)*10 + ((l>>3)&1)*5 + k in out[k], k < 5.
-__device__ __forceinline__ void wave_transpose_reduce40(float (&v)[40], float (&out)[5]) {
+typedef float floatx16 __attribute__((ext_vector_type(16)));
+
+constexpr int kBwdBatch = 32;      // active Gaussians per colour-gradient MFMA batch
+constexpr int kBwdPitch = 65;      // LDS row pitch (floats) of the [32][64] weight / dL tiles
+constexpr int kBwdLdsWave = kBwdBatch * kBwdPitch;  // floats per wave
+
+// Orders this wave's LDS accesses (rocPRIM's wave_barrier): the LDS executes a wave's DS
+// instructions in order, so a lane then reads what another lane of its wave wrote before.
+__device__ __forceinline__ void wave_lds_order() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// Reduce v[8] across the 64 lanes; lane l ends holding the sum of component
+// ((l>>5)&1)*4 + ((l>>4)&1)*2 + ((l>>3)&1) (complete in every lane of its group of 8).
+__device__ __forceinline__ float wave_transpose_reduce8(const float (&v)[8]) {
     const int lane = threadIdx.x & 63;
-    float a[20];
+    float a[4];
     {
         const bool hi = lane & 32;
 #pragma unroll
-        for (int k = 0; k < 20; k++) {
-            const float keep = hi ? v[k + 20] : v[k];
-            const float send = hi ? v[k] : v[k + 20];
+        for (int k = 0; k < 4; k++) {
+            const float keep = hi ? v[k + 4] : v[k];
+            const float send = hi ? v[k] : v[k + 4];
             a[k] = keep + __shfl_xor(send, 32);
         }
     }
-    float bb[10];
+    float bb[2];
     {
         const bool hi = lane & 16;
 #pragma unroll
-        for (int k = 0; k < 10; k++) {
-            const float keep = hi ? a[k + 10] : a[k];
-            const float send = hi ? a[k] : a[k + 10];
+        for (int k = 0; k < 2; k++) {
+            const float keep = hi ? a[k + 2] : a[k];
+            const float send = hi ? a[k] : a[k + 2];
             bb[k] = keep + __shfl_xor(send, 16);
         }
     }
+    float c;
     {
         const bool hi = lane & 8;
-#pragma unroll
-        for (int k = 0; k < 5; k++) {
-            const float keep = hi ? bb[k + 5] : bb[k];
-            const float send = hi ? bb[k] : bb[k + 5];
-            out[k] = keep + __shfl_xor(send, 8);
-        }
+        const float keep = hi ? bb[1] : bb[0];
+        const float send = hi ? bb[0] : bb[1];
+        c = keep + __shfl_xor(send, 8);
     }
 #pragma unroll
-    for (int off = 4; off > 0; off >>= 1)
-#pragma unroll
-        for (int k = 0; k < 5; k++) out[k] += __shfl_xor(out[k], off);
+    for (int off = 4; off > 0; off >>= 1) c += __shfl_xor(c, off);
+    return c;
 }
 
 // Work: the 16x4 strips of the non-empty tiles, in strip_list order (most survivors first), dealt to
@@ -56,17 +71,20 @@ __device__ __forceinline__ void wave_transpose_reduce40(float (&v)[40], float (&
 // and replays its tile's depth-sorted list back to front from the strip's largest n_contrib,
 // taking only the Gaussians whose strip bit is set in point_list (binning's exact test that the
 // Gaussian reaches alpha >= 1/255 somewhere in the strip; the others cannot be active on any of its
-// pixels).  No LDS and no barriers: render records and feature rows arrive by scalar loads (the
-// Gaussian index is wave-uniform).
+// pixels).  No workgroup barriers: render records and feature rows arrive by scalar loads (the
+// Gaussian index is wave-uniform); the LDS is wave-private.
 constexpr int kBwdQueueOffset = 32;  // words after each forward XCD counter (own cache line)
 
 template <bool EXACT, bool INVD>
 __global__ __launch_bounds__(GSR_TILE_PIX) void k_render_bwd(Dims d, Inputs in, GeomArena g,
                                                              ImageArena im, BinArena bn, Grads gr) {
+    __shared__ float lds_all[(GSR_TILE_PIX / 64) * kBwdLdsWave];
     if (g.ctrl[kCtrlOverflow]) return;
     const uint32_t ne = g.ctrl[kCtrlNonEmpty];
     const uint32_t nitems = (uint32_t)kStrips * ne;
     const int lane = threadIdx.x & 63;
+    float* wl = lds_all + (threadIdx.x >> 6) * kBwdLdsWave;  // this wave's [32][65] tile
+    const int hi = lane >> 5, l32 = lane & 31;
     uint32_t q = __builtin_amdgcn_s_getreg((3 << 11) | 20) & 7u;  // HW_REG_XCC_ID
     uint32_t q_left = 8;
     const int64_t HW = (int64_t)d.H * d.W;
@@ -121,6 +139,44 @@ __global__ __launch_bounds__(GSR_TILE_PIX) void k_render_bwd(Dims d, Inputs in, 
         }
         const float dL_inv = (INVD && inside) ? gr.dL_dinvdepth[pix] : 0.f;
 
+        // MFMA A operands of the colour-gradient contraction: step j covers strip pixels 2j, 2j+1;
+        // lane l holds dL[pixel 2j + (l>>5)][channel l&31].  Transposed through the LDS tile.
+        float adl[kBwdBatch];
+        wave_lds_order();
+#pragma unroll
+        for (int ch = 0; ch < GSR_C; ch++) wl[ch * kBwdPitch + lane] = dL[ch];
+        wave_lds_order();
+#pragma unroll
+        for (int j = 0; j < kBwdBatch; j++) adl[j] = wl[l32 * kBwdPitch + 2 * j + hi];
+        wave_lds_order();
+
+        // the current batch: slot s holds Gaussian gbat[lane s], its weights at wl[s][pixel]
+        int slot = 0;
+        int gbat = 0;
+        auto flush = [&]() {
+            wave_lds_order();
+            floatx16 acc;
+#pragma unroll
+            for (int r = 0; r < 16; r++) acc[r] = 0.f;
+#pragma unroll
+            for (int j = 0; j < kBwdBatch; j++) {
+                const float w = l32 < slot ? wl[l32 * kBwdPitch + 2 * j + hi] : 0.f;
+                acc = __builtin_amdgcn_mfma_f32_32x32x2f32(adl[j], w, acc, 0, 0, 0);
+            }
+            wave_lds_order();
+            // acc[r] at lane l: channel (r&3) + 8(r>>2) + 4(l>>5) of the batch's Gaussian l&31
+            const uint32_t gsel = (uint32_t)__shfl(gbat, l32);
+            if (l32 < slot) {
+                float* dst = gr.dL_dcolors + (gbase + gsel) * GSR_C + 4 * hi;
+#pragma unroll
+                for (int r = 0; r < 16; r++) {
+                    const float val = acc[r];
+                    if (val != 0.f) atomicAdd(dst + (r & 3) + 8 * (r >> 2), val);
+                }
+            }
+            slot = 0;
+        };
+
         float T = T_final;
         float accum_dot = 0.f, last_gdot = 0.f, last_alpha = 0.f;
         float accum_inv = 0.f, last_inv = 0.f;
@@ -149,19 +205,18 @@ __global__ __launch_bounds__(GSR_TILE_PIX) void k_render_bwd(Dims d, Inputs in, 
                     act = !(alpha < 1.0f / 255.0f);
                 }
                 if (!__any(act)) continue;
-                float v[40];
+                float v[8];
 #pragma unroll
-                for (int k = 0; k < 40; k++) v[k] = 0.f;
+                for (int k = 0; k < 8; k++) v[k] = 0.f;
+                float wgt = 0.f;
                 if (act) {
                     const float ca = -2.0f * rc.x, cb = -rc.y, cc = -2.0f * rc.z;  // exact
                     T = T / (1.f - alpha);
-                    const float wgt = alpha * T;
+                    wgt = alpha * T;
                     const float* f = colors + (int64_t)gi * GSR_C;
                     float gdot = 0.f;
 #pragma unroll
                     for (int ch = 0; ch < GSR_C; ch++) gdot = fmaf(f[ch], dL[ch], gdot);
-#pragma unroll
-                    for (int ch = 0; ch < GSR_C; ch++) v[ch] = wgt * dL[ch];
                     accum_dot = last_alpha * last_gdot + (1.f - last_alpha) * accum_dot;
                     last_gdot = gdot;
                     float dL_dalpha = gdot - accum_dot;
@@ -170,7 +225,7 @@ __global__ __launch_bounds__(GSR_TILE_PIX) void k_render_bwd(Dims d, Inputs in, 
                         accum_inv = last_alpha * last_inv + (1.f - last_alpha) * accum_inv;
                         last_inv = invdg;
                         dL_dalpha += (invdg - accum_inv) * dL_inv;
-                        v[38] = wgt * dL_inv;
+                        v[6] = wgt * dL_inv;
                     }
                     dL_dalpha *= T;
                     last_alpha = alpha;
@@ -180,37 +235,35 @@ __global__ __launch_bounds__(GSR_TILE_PIX) void k_render_bwd(Dims d, Inputs in, 
                     const float gdy = G * dy;
                     const float dG_ddelx = -gdx * ca - gdy * cb;
                     const float dG_ddely = -gdy * cc - gdx * cb;
-                    v[32] = dL_dG * dG_ddelx * ddelx_dx;
-                    v[33] = dL_dG * dG_ddely * ddely_dy;
-                    v[34] = -0.5f * gdx * dx * dL_dG;
-                    v[35] = -0.5f * gdx * dy * dL_dG;
-                    v[36] = -0.5f * gdy * dy * dL_dG;
-                    v[37] = G * dL_dalpha;
+                    v[0] = dL_dG * dG_ddelx * ddelx_dx;
+                    v[1] = dL_dG * dG_ddely * ddely_dy;
+                    v[2] = -0.5f * gdx * dx * dL_dG;
+                    v[3] = -0.5f * gdx * dy * dL_dG;
+                    v[4] = -0.5f * gdy * dy * dL_dG;
+                    v[5] = G * dL_dalpha;
                 }
-                float r[5];
-                wave_transpose_reduce40(v, r);
-                const int sub = lane & 7;
-                if (sub < 5) {
-                    const int comp = ((lane >> 5) & 1) * 20 + ((lane >> 4) & 1) * 10 + ((lane >> 3) & 1) * 5 + sub;
-                    float val = r[0];
-                    val = sub == 1 ? r[1] : val;
-                    val = sub == 2 ? r[2] : val;
-                    val = sub == 3 ? r[3] : val;
-                    val = sub == 4 ? r[4] : val;
+                // this Gaussian's weights join the colour-gradient batch
+                wl[slot * kBwdPitch + lane] = wgt;
+                gbat = lane == slot ? (int)gi : gbat;
+                slot++;
+                const float r = wave_transpose_reduce8(v);
+                const int comp = ((lane >> 5) & 1) * 4 + ((lane >> 4) & 1) * 2 + ((lane >> 3) & 1);
+                if ((lane & 7) == 0 && r != 0.f) {
                     const int64_t gg = gbase + gi;
                     float* dst = nullptr;
-                    if (comp < 32) dst = gr.dL_dcolors + gg * GSR_C + comp;
-                    else if (comp == 32) dst = gr.dL_dmean2D + gg * 3;
-                    else if (comp == 33) dst = gr.dL_dmean2D + gg * 3 + 1;
-                    else if (comp == 34) dst = gr.dL_dconic + gg * 4;
-                    else if (comp == 35) dst = gr.dL_dconic + gg * 4 + 1;
-                    else if (comp == 36) dst = gr.dL_dconic + gg * 4 + 3;
-                    else if (comp == 37) dst = gr.dL_dopacity + gg;
-                    else if (comp == 38 && INVD) dst = gr.dL_dinvdepth_g + gg;
-                    if (dst && val != 0.f) atomicAdd(dst, val);
+                    if (comp == 0) dst = gr.dL_dmean2D + gg * 3;
+                    else if (comp == 1) dst = gr.dL_dmean2D + gg * 3 + 1;
+                    else if (comp == 2) dst = gr.dL_dconic + gg * 4;
+                    else if (comp == 3) dst = gr.dL_dconic + gg * 4 + 1;
+                    else if (comp == 4) dst = gr.dL_dconic + gg * 4 + 3;
+                    else if (comp == 5) dst = gr.dL_dopacity + gg;
+                    else if (comp == 6 && INVD) dst = gr.dL_dinvdepth_g + gg;
+                    if (dst) atomicAdd(dst, r);
                 }
+                if (slot == kBwdBatch) flush();
             }
         }
+        if (slot) flush();
     }
 }
 

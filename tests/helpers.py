@@ -31,7 +31,8 @@ def geom_layout(P, W, H):
     nblk = (P + 255) // 256
     T = ((W + 15) // 16) * ((H + 15) // 16)
     NB = _nb(P)
-    nchunk = (P + 255) // 256
+    chunk = 1024 if T > 1024 else 256  # make_dims: count-table rows
+    nchunk = (P + chunk - 1) // chunk
     return _carve([("ctrl", np.uint32, 9216 + 8), ("depth", np.float32, P), ("invdepth", np.float32, P),
                    ("radii", np.int32, P), ("means2D", np.float32, 2 * P), ("cov3D", np.float32, 6 * P),
                    ("conic", np.float32, 4 * P), ("rect", np.uint32, 2 * P), ("rrec", np.float32, 8 * P),
@@ -44,7 +45,8 @@ def image_layout(W, H):
     T = ((W + 15) // 16) * ((H + 15) // 16)
     return _carve([("final_T", np.float32, W * H), ("n_contrib", np.uint32, W * H),
                    ("ranges", np.uint32, 2 * T), ("tile_count", np.uint32, T), ("work_list", np.uint32, T),
-                   ("lpt_hist", np.uint32, 34)])
+                   ("lpt_hist", np.uint32, 34), ("strip_cnt", np.uint32, 4 * T),
+                   ("strip_list", np.uint32, 4 * T), ("strip_hist", np.uint32, 129)])
 
 
 def bin_layout(R):
