@@ -112,6 +112,34 @@ def test_render_counters_match_oracle(kind, P, W, H):
     assert cnt["strip_pairs_blended"] <= 2 * cnt["mfma_ksteps"] <= cnt["strip_pairs_blended"] + cnt["gaussians_staged"]
 
 
+def test_strip_work_list():
+    """k_strip_count / k_strip_place: survivors per 16x4 strip equal the popcount of that strip's
+    bit over the tile's list, and the strip work list holds every strip of every non-empty tile
+    exactly once, in non-increasing survivor order up to the 4-buckets-per-octave granularity."""
+    _lib().set_exact_exp(True)
+    d = make_scene("avatar", 20000, 200, 136, seed=3)
+    _, _, _, gs = gpu_forward(d)
+    T = gs["ranges"].size // 2
+    rg = gs["ranges"].reshape(T, 2)
+    cnt = gs["strip_cnt"].reshape(T, 4)
+    for t in range(T):
+        m = gs["smask"][rg[t, 0]:rg[t, 1]]
+        np.testing.assert_array_equal(cnt[t], [(m >> s & 1).sum() for s in range(4)])
+    nonempty = np.nonzero(gs["tile_count"])[0]
+    n = 4 * len(nonempty)
+    lst = gs["strip_list"][:n]
+    assert sorted(lst.tolist()) == sorted((4 * nonempty[:, None] + np.arange(4)).reshape(-1).tolist())
+
+    def bucket(c):
+        if c == 0:
+            return 128
+        e = int(c).bit_length() - 1
+        sub = (c >> (e - 2)) & 3 if e >= 2 else (c << (2 - e)) & 3
+        return 127 - (4 * e + sub)
+    b = [bucket(int(cnt[x >> 2, x & 3])) for x in lst]
+    assert all(b[i] <= b[i + 1] for i in range(n - 1))
+
+
 def test_refine_epilogue_matches_conv():
     """The fused StyleUNet conv_body_first + leaky ReLU (styleunet.py:110,178) equals torch's conv2d
     on the full render within 1e-5 of scale (the conv is applied to each Gaussian's features before
