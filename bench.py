@@ -122,11 +122,17 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None
+    # one process per GPU (RCCL = the "nccl" backend).  GSR_DIST_BACKEND=gloo rehearses the N>1
+    # path with several ranks on one GPU (device = LOCAL_RANK modulo the visible devices).
+    backend = os.environ.get("GSR_DIST_BACKEND", "nccl")
+    dev = torch.device("cuda", local % max(torch.cuda.device_count(), 1))
     if world > 1:
         import torch.distributed as dist
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    dev = torch.device("cuda", local)
+        torch.cuda.set_device(dev)
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(backend)
     torch.cuda.set_device(dev)
 
     from guava_renderer_amd import _lib, parallel, scenes
@@ -249,7 +255,7 @@ def main():
     R_after, ovf = rast.status()
     assert not ovf, "capacity overflow inside the timed region"
     if dist is not None:
-        tt = torch.tensor([el], dtype=torch.float64, device=dev)
+        tt = torch.tensor([el], dtype=torch.float64, device=dev if backend == "nccl" else "cpu")
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         el = float(tt.item())
 
