@@ -11,7 +11,10 @@
 //    pixels per k-step) give the [32 channels x 32 Gaussians] block, issued as 16 atomic
 //    instructions, instead of 32 multiplies and a 32-channel cross-lane reduction per Gaussian;
 //  * the other 7 per-Gaussian terms (mean2D, conic, opacity, inverse depth) are reduced across the
-//    64 pixels with an 8-wide transpose-reduction and issued as ONE 7-lane atomic instruction.
+//    64 pixels with an 8-wide transpose-reduction, parked in LDS and issued with the batch, so no
+//    atomic sits in vmcnt ahead of the next survivor's loads;
+//  * one survivor of look-ahead: the next render record is loaded (vector loads, in-order vmcnt)
+//    while the current survivor runs.
 #include "gsr_internal.h"
 
 namespace gsr {
@@ -20,7 +23,8 @@ typedef float floatx16 __attribute__((ext_vector_type(16)));
 
 constexpr int kBwdBatch = 32;      // active Gaussians per colour-gradient MFMA batch
 constexpr int kBwdPitch = 65;      // LDS row pitch (floats) of the [32][64] weight / dL tiles
-constexpr int kBwdLdsWave = kBwdBatch * kBwdPitch;  // floats per wave
+constexpr int kBwdComps = 8;      // per-Gaussian non-colour gradient terms parked per batch slot
+constexpr int kBwdLdsWave = kBwdBatch * kBwdPitch + kBwdBatch * kBwdComps;  // floats per wave
 
 // Orders this wave's LDS accesses (rocPRIM's wave_barrier): the LDS executes a wave's DS
 // instructions in order, so a lane then reads what another lane of its wave wrote before.
@@ -76,7 +80,7 @@ __device__ __forceinline__ float wave_transpose_reduce8(const float (&v)[8]) {
 constexpr int kBwdQueueOffset = 32;  // words after each forward XCD counter (own cache line)
 
 template <bool EXACT, bool INVD>
-__global__ __launch_bounds__(GSR_TILE_PIX) void k_render_bwd(Dims d, Inputs in, GeomArena g,
+__global__ __launch_bounds__(GSR_TILE_PIX) __attribute__((amdgpu_waves_per_eu(3))) void k_render_bwd(Dims d, Inputs in, GeomArena g,
                                                              ImageArena im, BinArena bn, Grads gr) {
     __shared__ float lds_all[(GSR_TILE_PIX / 64) * kBwdLdsWave];
     if (g.ctrl[kCtrlOverflow]) return;
@@ -84,6 +88,9 @@ __global__ __launch_bounds__(GSR_TILE_PIX) void k_render_bwd(Dims d, Inputs in, 
     const uint32_t nitems = (uint32_t)kStrips * ne;
     const int lane = threadIdx.x & 63;
     float* wl = lds_all + (threadIdx.x >> 6) * kBwdLdsWave;  // this wave's [32][65] tile
+    float* cl = wl + kBwdBatch * kBwdPitch;                    // and its [32][8] term slots
+    uint32_t vzero;  // a VGPR zero: indexes the uniform record loads so they stay vector loads
+    asm volatile("v_mov_b32 %0, 0" : "=v"(vzero));
     const int hi = lane >> 5, l32 = lane & 31;
     uint32_t q = __builtin_amdgcn_s_getreg((3 << 11) | 20) & 7u;  // HW_REG_XCC_ID
     uint32_t q_left = 8;
@@ -167,34 +174,68 @@ __global__ __launch_bounds__(GSR_TILE_PIX) void k_render_bwd(Dims d, Inputs in, 
             // acc[r] at lane l: channel (r&3) + 8(r>>2) + 4(l>>5) of the batch's Gaussian l&31
             const uint32_t gsel = (uint32_t)__shfl(gbat, l32);
             if (l32 < slot) {
-                float* dst = gr.dL_dcolors + (gbase + gsel) * GSR_C + 4 * hi;
+                const int64_t gg = gbase + gsel;
+                float* dst = gr.dL_dcolors + gg * GSR_C + 4 * hi;
 #pragma unroll
                 for (int r = 0; r < 16; r++) {
                     const float val = acc[r];
                     if (val != 0.f) atomicAdd(dst + (r & 3) + 8 * (r >> 2), val);
                 }
+                // the parked terms: lane l takes terms 4(l>>5) .. +3 of slot l&31
+#pragma unroll
+                for (int u = 0; u < 4; u++) {
+                    const int comp = 4 * hi + u;
+                    const float val = cl[l32 * kBwdComps + comp];
+                    float* dc = nullptr;
+                    if (comp == 0) dc = gr.dL_dmean2D + gg * 3;
+                    else if (comp == 1) dc = gr.dL_dmean2D + gg * 3 + 1;
+                    else if (comp == 2) dc = gr.dL_dconic + gg * 4;
+                    else if (comp == 3) dc = gr.dL_dconic + gg * 4 + 1;
+                    else if (comp == 4) dc = gr.dL_dconic + gg * 4 + 3;
+                    else if (comp == 5) dc = gr.dL_dopacity + gg;
+                    else if (comp == 6 && INVD) dc = gr.dL_dinvdepth_g + gg;
+                    if (dc && val != 0.f) atomicAdd(dc, val);
+                }
             }
+            wave_lds_order();
             slot = 0;
         };
 
         float T = T_final;
         float accum_dot = 0.f, last_gdot = 0.f, last_alpha = 0.f;
         float accum_inv = 0.f, last_inv = 0.f;
-        // chunks of 64 list positions, last chunk first; the next (lower) chunk is prefetched
-        int base = (int)((ns - 1) & ~63u);
+        // survivor stream, back to front: chunks of 64 list positions, last chunk first (the next
+        // lower chunk prefetched), the strip's survivors of a chunk from its highest bit down
+        int base = (int)((ns - 1) & ~63u) + 64;
         uint32_t cidx = 0;
-        uint32_t nidx = base + lane < (int)ns ? plist[base + lane] : 0u;
-        for (; base >= 0; base -= 64) {
-            cidx = nidx;
-            if (base >= 64) nidx = plist[base - 64 + lane];
-            uint64_t mask = __ballot(base + lane < (int)ns && (cidx & smask_bit) != 0u);
-            while (mask) {
-                const int i = 63 - (int)__builtin_clzll(mask);
-                mask &= ~(1ull << i);
-                const uint32_t gi = __builtin_amdgcn_readlane(cidx, i) & kIndexMask;
-                const uint32_t contributor = (uint32_t)(base + i);  // 0-based list position
-                const float4 ra = rrec[2 * gi];       // x, y, opacity, 1/depth
-                const float4 rc = rrec[2 * gi + 1];   // -a/2, -b, -c/2
+        uint32_t nidx = base - 64 + lane < (int)ns ? plist[base - 64 + lane] : 0u;
+        uint64_t mask = 0;
+        auto next_survivor = [&](uint32_t& gi_o, uint32_t& contrib_o) -> bool {
+            while (mask == 0) {
+                base -= 64;
+                if (base < 0) return false;
+                cidx = nidx;
+                if (base >= 64) nidx = plist[base - 64 + lane];
+                mask = __ballot(base + lane < (int)ns && (cidx & smask_bit) != 0u);
+            }
+            const int i = 63 - (int)__builtin_clzll(mask);
+            mask &= ~(1ull << i);
+            gi_o = __builtin_amdgcn_readlane(cidx, i) & kIndexMask;
+            contrib_o = (uint32_t)(base + i);  // 0-based list position
+            return true;
+        };
+        // one survivor of look-ahead: its render record is in flight while the current one runs
+        uint32_t gi = 0, contributor = 0;
+        bool have = next_survivor(gi, contributor);
+        float4 ra = make_float4(0.f, 0.f, 0.f, 0.f), rc = ra;
+        if (have) { ra = rrec[2 * gi + vzero]; rc = rrec[2 * gi + 1 + vzero]; }
+        while (have) {
+            uint32_t gi_n = 0, contributor_n = 0;
+            const bool have_n = next_survivor(gi_n, contributor_n);
+            float4 ra_n = ra, rc_n = rc;
+            if (have_n) { ra_n = rrec[2 * gi_n + vzero]; rc_n = rrec[2 * gi_n + 1 + vzero]; }
+            {
+                // ra: x, y, opacity, 1/depth; rc: -a/2, -b, -c/2
                 const float dx = ra.x - pfx, dy = ra.y - pfy;
                 const float power = blend_power(rc.x, rc.y, rc.z, dx, dy);
                 bool act = inside && contributor < last_contributor && !(power > 0.0f);
@@ -204,64 +245,56 @@ __global__ __launch_bounds__(GSR_TILE_PIX) void k_render_bwd(Dims d, Inputs in, 
                     alpha = fminf(0.99f, ra.z * G);
                     act = !(alpha < 1.0f / 255.0f);
                 }
-                if (!__any(act)) continue;
-                float v[8];
+                if (__any(act)) {
+                    float v[8];
 #pragma unroll
-                for (int k = 0; k < 8; k++) v[k] = 0.f;
-                float wgt = 0.f;
-                if (act) {
-                    const float ca = -2.0f * rc.x, cb = -rc.y, cc = -2.0f * rc.z;  // exact
-                    T = T / (1.f - alpha);
-                    wgt = alpha * T;
-                    const float* f = colors + (int64_t)gi * GSR_C;
-                    float gdot = 0.f;
+                    for (int k = 0; k < 8; k++) v[k] = 0.f;
+                    float wgt = 0.f;
+                    if (act) {
+                        const float ca = -2.0f * rc.x, cb = -rc.y, cc = -2.0f * rc.z;  // exact
+                        T = T / (1.f - alpha);
+                        wgt = alpha * T;
+                        const float* f = colors + (int64_t)gi * GSR_C;
+                        float gdot = 0.f;
 #pragma unroll
-                    for (int ch = 0; ch < GSR_C; ch++) gdot = fmaf(f[ch], dL[ch], gdot);
-                    accum_dot = last_alpha * last_gdot + (1.f - last_alpha) * accum_dot;
-                    last_gdot = gdot;
-                    float dL_dalpha = gdot - accum_dot;
-                    if (INVD) {
-                        const float invdg = ra.w;
-                        accum_inv = last_alpha * last_inv + (1.f - last_alpha) * accum_inv;
-                        last_inv = invdg;
-                        dL_dalpha += (invdg - accum_inv) * dL_inv;
-                        v[6] = wgt * dL_inv;
+                        for (int ch = 0; ch < GSR_C; ch++) gdot = fmaf(f[ch], dL[ch], gdot);
+                        accum_dot = last_alpha * last_gdot + (1.f - last_alpha) * accum_dot;
+                        last_gdot = gdot;
+                        float dL_dalpha = gdot - accum_dot;
+                        if (INVD) {
+                            const float invdg = ra.w;
+                            accum_inv = last_alpha * last_inv + (1.f - last_alpha) * accum_inv;
+                            last_inv = invdg;
+                            dL_dalpha += (invdg - accum_inv) * dL_inv;
+                            v[6] = wgt * dL_inv;
+                        }
+                        dL_dalpha *= T;
+                        last_alpha = alpha;
+                        dL_dalpha += (-T_final / (1.f - alpha)) * bg_dot;
+                        const float dL_dG = ra.z * dL_dalpha;
+                        const float gdx = G * dx;
+                        const float gdy = G * dy;
+                        const float dG_ddelx = -gdx * ca - gdy * cb;
+                        const float dG_ddely = -gdy * cc - gdx * cb;
+                        v[0] = dL_dG * dG_ddelx * ddelx_dx;
+                        v[1] = dL_dG * dG_ddely * ddely_dy;
+                        v[2] = -0.5f * gdx * dx * dL_dG;
+                        v[3] = -0.5f * gdx * dy * dL_dG;
+                        v[4] = -0.5f * gdy * dy * dL_dG;
+                        v[5] = G * dL_dalpha;
                     }
-                    dL_dalpha *= T;
-                    last_alpha = alpha;
-                    dL_dalpha += (-T_final / (1.f - alpha)) * bg_dot;
-                    const float dL_dG = ra.z * dL_dalpha;
-                    const float gdx = G * dx;
-                    const float gdy = G * dy;
-                    const float dG_ddelx = -gdx * ca - gdy * cb;
-                    const float dG_ddely = -gdy * cc - gdx * cb;
-                    v[0] = dL_dG * dG_ddelx * ddelx_dx;
-                    v[1] = dL_dG * dG_ddely * ddely_dy;
-                    v[2] = -0.5f * gdx * dx * dL_dG;
-                    v[3] = -0.5f * gdx * dy * dL_dG;
-                    v[4] = -0.5f * gdy * dy * dL_dG;
-                    v[5] = G * dL_dalpha;
+                    // this Gaussian joins the batch: its weights and its 7 reduced terms are parked
+                    // in LDS, all of its atomics go out with the batch (none between two flushes)
+                    wl[slot * kBwdPitch + lane] = wgt;
+                    gbat = lane == slot ? (int)gi : gbat;
+                    const float r = wave_transpose_reduce8(v);
+                    if ((lane & 7) == 0)
+                        cl[slot * kBwdComps + ((lane >> 5) & 1) * 4 + ((lane >> 4) & 1) * 2 + ((lane >> 3) & 1)] = r;
+                    slot++;
+                    if (slot == kBwdBatch) flush();
                 }
-                // this Gaussian's weights join the colour-gradient batch
-                wl[slot * kBwdPitch + lane] = wgt;
-                gbat = lane == slot ? (int)gi : gbat;
-                slot++;
-                const float r = wave_transpose_reduce8(v);
-                const int comp = ((lane >> 5) & 1) * 4 + ((lane >> 4) & 1) * 2 + ((lane >> 3) & 1);
-                if ((lane & 7) == 0 && r != 0.f) {
-                    const int64_t gg = gbase + gi;
-                    float* dst = nullptr;
-                    if (comp == 0) dst = gr.dL_dmean2D + gg * 3;
-                    else if (comp == 1) dst = gr.dL_dmean2D + gg * 3 + 1;
-                    else if (comp == 2) dst = gr.dL_dconic + gg * 4;
-                    else if (comp == 3) dst = gr.dL_dconic + gg * 4 + 1;
-                    else if (comp == 4) dst = gr.dL_dconic + gg * 4 + 3;
-                    else if (comp == 5) dst = gr.dL_dopacity + gg;
-                    else if (comp == 6 && INVD) dst = gr.dL_dinvdepth_g + gg;
-                    if (dst) atomicAdd(dst, r);
-                }
-                if (slot == kBwdBatch) flush();
             }
+            gi = gi_n; contributor = contributor_n; ra = ra_n; rc = rc_n; have = have_n;
         }
         if (slot) flush();
     }
