@@ -754,7 +754,16 @@ __global__ __launch_bounds__(256) void k_strip_count(Dims d, ImageArena im, BinA
 }
 
 // Per frame: histogram of its non-empty tiles' strips over the buckets.
-__global__ __launch_bounds__(1024) void k_strip_hist(Dims d, ImageArena im) {
+__device__ __forceinline__ uint32_t tile_strip_max(const ImageArena& im, int64_t tg) {
+    uint32_t m = 0;
+#pragma unroll
+    for (int s = 0; s < kStrips; s++) m = max(m, im.strip_cnt[tg * kStrips + s]);
+    return m;
+}
+
+// Per frame: histogram over the buckets of its non-empty tiles' strips (tile_major = 0) or of the
+// tiles themselves keyed by their longest strip (tile_major = 1).
+__global__ __launch_bounds__(1024) void k_strip_hist(Dims d, ImageArena im, int tile_major) {
     __shared__ uint32_t h[kStripBuckets];
     const int b = blockIdx.x;
     for (int i = threadIdx.x; i < kStripBuckets; i += 1024) h[i] = 0;
@@ -762,16 +771,23 @@ __global__ __launch_bounds__(1024) void k_strip_hist(Dims d, ImageArena im) {
     for (int t = threadIdx.x; t < d.T; t += 1024) {
         const int64_t tg = (int64_t)b * d.T + t;
         if (!im.tile_count[tg]) continue;
+        if (tile_major) {
+            atomicAdd(&h[strip_bucket(tile_strip_max(im, tg))], 1u);
+        } else {
 #pragma unroll
-        for (int s = 0; s < kStrips; s++) atomicAdd(&h[strip_bucket(im.strip_cnt[tg * kStrips + s])], 1u);
+            for (int s = 0; s < kStrips; s++) atomicAdd(&h[strip_bucket(im.strip_cnt[tg * kStrips + s])], 1u);
+        }
     }
     __syncthreads();
     for (int i = threadIdx.x; i < kStripBuckets; i += 1024) im.strip_hist[b * kStripBuckets + i] = h[i];
 }
 
 // Per frame: place its strips into the batch-wide strip list, bucket-major (most survivors first);
-// the order inside a bucket is whatever the LDS atomics give (scheduling only).
-__global__ __launch_bounds__(1024) void k_strip_place(Dims d, ImageArena im) {
+// the order inside a bucket is whatever the LDS atomics give (scheduling only).  tile_major = 1
+// places whole tiles (their 4 strips consecutive) by their longest strip, so the render's
+// tile-affine queues (queue_item) keep a tile's strips -- which read the same Gaussians -- on one
+// XCD and its L2.
+__global__ __launch_bounds__(1024) void k_strip_place(Dims d, ImageArena im, int tile_major) {
     extern __shared__ uint32_t hist[];  // [B][kStripBuckets]
     __shared__ uint32_t cur[kStripBuckets];
     __shared__ uint32_t before[kStripBuckets];
@@ -801,10 +817,16 @@ __global__ __launch_bounds__(1024) void k_strip_place(Dims d, ImageArena im) {
     for (int t = threadIdx.x; t < d.T; t += 1024) {
         const int64_t tg = (int64_t)b * d.T + t;
         if (!im.tile_count[tg]) continue;
+        if (tile_major) {
+            const uint32_t pos = atomicAdd(&cur[strip_bucket(tile_strip_max(im, tg))], 1u);
 #pragma unroll
-        for (int s = 0; s < kStrips; s++) {
-            const uint32_t bk = strip_bucket(im.strip_cnt[tg * kStrips + s]);
-            im.strip_list[atomicAdd(&cur[bk], 1u)] = ((uint32_t)tg << 2) | (uint32_t)s;
+            for (int s = 0; s < kStrips; s++) im.strip_list[kStrips * pos + s] = ((uint32_t)tg << 2) | (uint32_t)s;
+        } else {
+#pragma unroll
+            for (int s = 0; s < kStrips; s++) {
+                const uint32_t bk = strip_bucket(im.strip_cnt[tg * kStrips + s]);
+                im.strip_list[atomicAdd(&cur[bk], 1u)] = ((uint32_t)tg << 2) | (uint32_t)s;
+            }
         }
     }
 }
@@ -815,14 +837,15 @@ void launch_strip_order(const Dims& d, const GeomArena& g, const ImageArena& im,
     if (d.B == 0 || d.T == 0) return;
     const int nt = d.B * d.T;
     hipLaunchKernelGGL(k_strip_count, dim3((nt + 3) / 4), dim3(256), 0, s, d, im, b);
-    hipLaunchKernelGGL(k_strip_hist, dim3(d.B), dim3(1024), 0, s, d, im);
+    const int tile_major = strip_order_tile_major();
+    hipLaunchKernelGGL(k_strip_hist, dim3(d.B), dim3(1024), 0, s, d, im, tile_major);
     const size_t lds = (size_t)d.B * kStripBuckets * 4;
     static size_t attr = 0;
     if (lds > 65536 && attr < lds) {
         attr = lds;
         hipFuncSetAttribute((const void*)k_strip_place, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     }
-    hipLaunchKernelGGL(k_strip_place, dim3(d.B), dim3(1024), lds, s, d, im);
+    hipLaunchKernelGGL(k_strip_place, dim3(d.B), dim3(1024), lds, s, d, im, tile_major);
 }
 
 }  // namespace gsr

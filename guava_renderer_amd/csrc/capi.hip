@@ -89,6 +89,12 @@ namespace gsr {
 static void env_tuning(Inputs& in) {
     static const uint32_t prio = [] { const char* e = getenv("GSR_PRIO_ITEMS"); return e ? (uint32_t)atoi(e) : 0u; }();
     in.prio_items = prio;
+    in.xcd_map = (uint32_t)strip_order_tile_major();
+}
+
+int strip_order_tile_major() {
+    static const int v = [] { const char* e = getenv("GSR_STRIP_ORDER"); return (e && !strcmp(e, "strip")) ? 0 : 1; }();
+    return v;
 }
 
 int persistent_grid(int per_cu) {

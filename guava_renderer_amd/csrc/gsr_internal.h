@@ -139,6 +139,7 @@ struct Inputs {
     float scale_mod;
     int prefiltered, antialiasing;
     uint32_t prio_items;  // render_fwd: work items (longest first) that run at raised issue priority
+    uint32_t xcd_map;     // render work-queue mapping (queue_item): 1 = tile-affine (strip order tile-major)
 };
 
 struct Outputs {
@@ -177,6 +178,28 @@ int api_fail(int status, const char* msg);
 
 // Workgroups for a persistent (work-queue) launch: CUs of the current device x per_cu.
 int persistent_grid(int per_cu);
+// GSR_STRIP_ORDER: "strip" orders the render work by each strip's survivors; "tile" (default) by
+// tile (its longest strip), the 4 strips consecutive and dealt to one XCD queue (L2 reuse).
+int strip_order_tile_major();
+
+// Render work items (render_fwd / render_bwd): the 4 strips of each of the ne non-empty tiles in
+// strip_list order (items [0, 4 ne)), then nempty whole empty tiles (items [4 ne, 4 ne + nempty)).
+// Eight per-XCD queues; the k-th dequeue of queue q returns:
+//  * map 0: item q + 8k;
+//  * map 1 (tile-affine): queue q owns list tiles q, q+8, q+16, ... with their 4 strips consecutive,
+//    then the empty tiles e = q (mod 8): a tile's strips read the same Gaussians from one L2.
+// 0xFFFFFFFF when queue q is drained.
+__device__ __forceinline__ uint32_t queue_item(uint32_t q, uint32_t k, uint32_t ne, uint32_t nempty,
+                                               uint32_t map) {
+    if (map == 0) {
+        const uint32_t item = q + 8u * k;
+        return item < 4u * ne + nempty ? item : 0xFFFFFFFFu;
+    }
+    const uint32_t ntq = ne > q ? (ne - q + 7u) >> 3 : 0u;  // tiles owned by queue q
+    if (k < 4u * ntq) return 4u * (q + 8u * (k >> 2)) + (k & 3u);
+    const uint32_t e = q + 8u * (k - 4u * ntq);
+    return e < nempty ? 4u * ne + e : 0xFFFFFFFFu;
+}
 
 // ---- launchers (all asynchronous on `stream`) ----
 void launch_preprocess(const Dims& d, const Inputs& in, const GeomArena& g, const Outputs& o,

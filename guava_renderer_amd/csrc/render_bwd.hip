@@ -85,7 +85,6 @@ __global__ __launch_bounds__(GSR_TILE_PIX) __attribute__((amdgpu_waves_per_eu(3)
     __shared__ float lds_all[(GSR_TILE_PIX / 64) * kBwdLdsWave];
     if (g.ctrl[kCtrlOverflow]) return;
     const uint32_t ne = g.ctrl[kCtrlNonEmpty];
-    const uint32_t nitems = (uint32_t)kStrips * ne;
     const int lane = threadIdx.x & 63;
     float* wl = lds_all + (threadIdx.x >> 6) * kBwdLdsWave;  // this wave's [32][65] tile
     float* cl = wl + kBwdBatch * kBwdPitch;                    // and its [32][8] term slots
@@ -104,8 +103,8 @@ __global__ __launch_bounds__(GSR_TILE_PIX) __attribute__((amdgpu_waves_per_eu(3)
             uint32_t k = 0;
             if (lane == 0) k = atomicAdd(&g.ctrl[kCtrlXcdQueue + kCtrlXcdStride * q + kBwdQueueOffset], 1u);
             k = __builtin_amdgcn_readfirstlane(k);
-            item = q + 8u * k;
-            if (item < nitems) break;
+            item = queue_item(q, k, ne, 0u, in.xcd_map);
+            if (item != 0xFFFFFFFFu) break;
             q = (q + 1) & 7u;
             q_left--;
         }

@@ -197,8 +197,8 @@ __device__ __forceinline__ void render_fwd_body(const Dims& d, const Inputs& in,
             uint32_t k = 0;
             if (lane == 0) k = atomicAdd(&g.ctrl[kCtrlXcdQueue + kCtrlXcdStride * q], 1u);
             k = __builtin_amdgcn_readfirstlane(k);
-            item = q + 8u * k;
-            if (item < nitems) break;
+            item = queue_item(q, k, ne, nitems - nstrip, in.xcd_map);
+            if (item != 0xFFFFFFFFu) break;
             q = (q + 1) & 7u;
             q_left--;
         }

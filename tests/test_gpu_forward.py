@@ -115,7 +115,8 @@ def test_render_counters_match_oracle(kind, P, W, H):
 def test_strip_work_list():
     """k_strip_count / k_strip_place: survivors per 16x4 strip equal the popcount of that strip's
     bit over the tile's list, and the strip work list holds every strip of every non-empty tile
-    exactly once, in non-increasing survivor order up to the 4-buckets-per-octave granularity."""
+    exactly once, tile-major (GSR_STRIP_ORDER default): a tile's 4 strips consecutive, tiles in
+    non-increasing order of their longest strip up to the 4-buckets-per-octave granularity."""
     _lib().set_exact_exp(True)
     d = make_scene("avatar", 20000, 200, 136, seed=3)
     _, _, _, gs = gpu_forward(d)
@@ -136,8 +137,10 @@ def test_strip_work_list():
         e = int(c).bit_length() - 1
         sub = (c >> (e - 2)) & 3 if e >= 2 else (c << (2 - e)) & 3
         return 127 - (4 * e + sub)
-    b = [bucket(int(cnt[x >> 2, x & 3])) for x in lst]
-    assert all(b[i] <= b[i + 1] for i in range(n - 1))
+    groups = lst.reshape(-1, 4)
+    assert (groups >> 2 == (groups[:, :1] >> 2)).all() and ((groups & 3) == np.arange(4)).all()
+    b = [bucket(int(cnt[x >> 2].max())) for x in groups[:, 0]]
+    assert all(b[i] <= b[i + 1] for i in range(len(b) - 1))
 
 
 def test_refine_epilogue_matches_conv():
