@@ -19,7 +19,7 @@
 //   4. k_tile_scan/place   per frame: tile counts -> ranges; longest-first render work list
 //   5. k_ordered_scatter   per chunk: load-balanced expansion of the instances over the workgroup,
 //                          stable rank = tile base + chunk base + earlier slots covering the tile
-//                          (popcount of row/column ballots), plus the exact 16x4 strip mask
+//                          (popcount of row/column ballots), plus the exact 4-bit strip mask
 // Traffic per instance: 4 B point_list + 1 B strip mask written once; per Gaussian a few words.
 #include "gsr_internal.h"
 
@@ -563,7 +563,7 @@ __device__ __forceinline__ float4 strip_pre(float4 co) {
 }
 
 // Strip mask of one (Gaussian, tile) instance: bit s is set unless no pixel centre of the tile's
-// s-th 16x4 strip can give alpha = min(0.99, o*exp(-Q/2)) >= 1/255, i.e. unless Q > 2 ln(255 o)
+// s-th strip (strip_origin, kStripW x kStripH) can give alpha = min(0.99, o*exp(-Q/2)) >= 1/255, i.e. unless Q > 2 ln(255 o)
 // on the whole strip.  A cleared bit only ever removes pairs the blend skips anyway (alpha < 1/255,
 // forward.cu:362-363), so culling with it is decision-preserving; the slack (1e-4 of the form's
 // term magnitudes + 1e-3 relative) covers float rounding of both this test and the blend's power.
@@ -574,13 +574,15 @@ __device__ __forceinline__ uint32_t strip_mask(float4 co, float4 pre, float2 m, 
     if (mode == 2u) return (1u << kStrips) - 1u;
     const float a = co.x, b = co.y, c = co.z;
     const float K = pre.x;
-    const float dxl = m.x - (float)(tx * GSR_BX + GSR_BX - 1), dxh = m.x - (float)(tx * GSR_BX);
-    const float mx = fmaxf(fabsf(dxl), fabsf(dxh));
     uint32_t bits = 0;
 #pragma unroll
     for (int s = 0; s < kStrips; s++) {
-        const float y0 = (float)(ty * GSR_BY + s * (GSR_BY / kStrips));
-        const float dyl = m.y - (y0 + (float)(GSR_BY / kStrips - 1)), dyh = m.y - y0;
+        int sx0, sy0;
+        strip_origin(tx, ty, s, sx0, sy0);
+        const float x0 = (float)sx0, y0 = (float)sy0;
+        const float dxl = m.x - (x0 + (float)(kStripW - 1)), dxh = m.x - x0;
+        const float mx = fmaxf(fabsf(dxl), fabsf(dxh));
+        const float dyl = m.y - (y0 + (float)(kStripH - 1)), dyh = m.y - y0;
         const float my = fmaxf(fabsf(dyl), fabsf(dyh));
         const float slack = 1e-4f * (a * mx * mx + 2.f * fabsf(b) * mx * my + c * my * my) + 1e-3f * K + 1e-3f;
         const float q = rect_qmin(a, b, c, pre.y, pre.z, dxl, dxh, dyl, dyh);
@@ -711,7 +713,7 @@ void launch_ordered_scatter(const Dims& d, const GeomArena& g, const ImageArena&
 }
 
 // ---------------------------------------------------------------- 6. strip work list
-// The render kernels' unit of work is one 16x4 strip, and its cost is the number of list entries
+// The render kernels' unit of work is one 64-pixel strip (8x8), and its cost is the number of list entries
 // whose strip bit is set (before early termination).  The tile-level longest-first list above
 // orders by list length in octaves, which lets strips of 10x the mean work start late and set the
 // kernel's length; this orders the strips themselves, 4 buckets per octave of survivors.

@@ -19,7 +19,19 @@ constexpr int kSortLargeCap = 8192;   // keys per segment sorted by the 1024-thr
 constexpr int kTinyBucket = 64;       // depth buckets up to this size are ranked in place
 constexpr int kSlots = 256;           // k_ordered_scatter: Gaussians per pass (one per thread)
 constexpr int kRenderBatch = 64;      // Gaussians staged in LDS per render_bwd round
-constexpr int kStrips = 4;            // 16x4 pixel strips per 16x16 tile (one render wave each)
+constexpr int kStrips = 4;            // 64-pixel strips per 16x16 tile (one render wave each)
+#ifndef GSR_STRIP_W
+#define GSR_STRIP_W 8
+#endif
+constexpr int kStripW = GSR_STRIP_W;        // strip width: 8 (8x8 strips, 2x2 per tile) or 16 (16x4)
+constexpr int kStripH = 64 / kStripW;
+constexpr int kStripsX = GSR_BX / kStripW;  // strips per tile row
+static_assert(kStripsX * (GSR_BY / kStripH) == kStrips, "4 strips of 64 pixels per tile");
+// pixel origin of strip s of tile (tx, ty); lane l of its wave owns pixel (x0 + l % kStripW, y0 + l / kStripW)
+__host__ __device__ __forceinline__ void strip_origin(int tx, int ty, int s, int& x0, int& y0) {
+    x0 = tx * GSR_BX + (s % kStripsX) * kStripW;
+    y0 = ty * GSR_BY + (s / kStripsX) * kStripH;
+}
 
 // control words (uint32) at the head of the geometry arena
 enum Ctrl : int {
@@ -87,7 +99,7 @@ struct ImageArena {
 struct BinArena {
     uint32_t* point_list;  // per tile, depth-sorted: Gaussian index (within its frame, bits 0..27) |
                            // strip mask << 28, bit s set <=> the Gaussian can reach alpha >= 1/255
-                           // somewhere in the tile's 16x4 pixel strip s (render_fwd's wave unit)
+                           // somewhere in the tile's pixel strip s (strip_origin; render_fwd's wave unit)
 };
 
 struct Dims {

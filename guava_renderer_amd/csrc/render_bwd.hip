@@ -1,7 +1,7 @@
 // render_bwd.hip -- back-to-front gradient replay (backward.cu:452-638 of the reference).
 //
 // Differences in structure (same math):
-//  * one wave per 16x4 strip from persistent per-XCD queues, replaying only the Gaussians binning
+//  * one wave per 8x8 strip from persistent per-XCD queues, replaying only the Gaussians binning
 //    marked as reaching the strip, from the strip's largest n_contrib instead of the tile list end;
 //  * the 32-channel "accumulated colour behind" recurrence is carried as its dot product with
 //    dL/dpixel (linear, so sum_ch (c - accum_rec_ch) dL_ch == g - accum_dot with g = f . dL);
@@ -70,7 +70,7 @@ __device__ __forceinline__ float wave_transpose_reduce8(const float (&v)[8]) {
     return c;
 }
 
-// Work: the 16x4 strips of the non-empty tiles, in strip_list order (most survivors first), dealt to
+// Work: the 8x8 strips of the non-empty tiles, in strip_list order (most survivors first), dealt to
 // per-XCD queues exactly like render_fwd (separate counters).  One wave owns a strip (lane = pixel)
 // and replays its tile's depth-sorted list back to front from the strip's largest n_contrib,
 // taking only the Gaussians whose strip bit is set in point_list (binning's exact test that the
@@ -115,8 +115,10 @@ __global__ __launch_bounds__(GSR_TILE_PIX) __attribute__((amdgpu_waves_per_eu(3)
         const int b = tile_g / d.T;
         const int t = tile_g - b * d.T;
         const int tx = t % d.gx, ty = t / d.gx;
-        const int px = tx * GSR_BX + (lane & 15);
-        const int py = ty * GSR_BY + strip * 4 + (lane >> 4);
+        int sx0, sy0;
+        strip_origin(tx, ty, strip, sx0, sy0);
+        const int px = sx0 + lane % kStripW;
+        const int py = sy0 + lane / kStripW;
         const bool inside = px < d.W && py < d.H;
         const int64_t pix = b * HW + (int64_t)py * d.W + px;
         const float pfx = (float)px, pfy = (float)py;

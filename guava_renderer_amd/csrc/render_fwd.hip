@@ -2,7 +2,7 @@
 // the reference).
 //
 // Structure (gfx950):
-//  * The unit of work is one 16x4 pixel strip of a 16x16 tile, owned by ONE wave (lane = pixel).
+//  * The unit of work is one 64-pixel strip (8x8, strip_origin) of a 16x16 tile, owned by ONE wave (lane = pixel).
 //    Waves dequeue strips independently from k_tile_scan's longest-first tile list (4 strips per
 //    entry), so there is no workgroup barrier anywhere: a wave whose pixels all finished moves on
 //    at once, and every XCD gets work.
@@ -59,7 +59,7 @@ __device__ __forceinline__ float take_step(float alpha, float inv_depth, uint32_
     return w;
 }
 
-// Epilogue of one 16x4 strip: final_T, n_contrib, inverse depth (lane = pixel) and the 32
+// Epilogue of one strip: final_T, n_contrib, inverse depth (lane = pixel) and the 32
 // channel-major colour rows C + T*bg from the MFMA accumulators.  acc_n[r] at lane l holds channel
 // (r&3)+8*(r>>2)+4*(l>>5) of strip pixel 32n + (l&31), whose transmittance lives in lane 32n + (l&31).
 // REFINE (gsr_forward_batch_refine): the features were pre-contracted by gsr_refine_prepare, so
@@ -68,12 +68,12 @@ __device__ __forceinline__ float take_step(float alpha, float inv_depth, uint32_
 // nowhere.  No extra registers: the blend loop is the same kernel.
 template <bool EMPTY, bool REFINE>
 __device__ __forceinline__ void store_strip(const Dims& d, const ImageArena& im, const Outputs& o,
-                                            const float* bg, int b, int tx, int sy0, int lane,
+                                            const float* bg, int b, int sx0, int sy0, int lane,
                                             const floatx16& acc0, const floatx16& acc1, float T,
                                             float invd, uint32_t last) {
     const int64_t HW = (int64_t)d.H * d.W;
-    const int px = tx * GSR_BX + (lane & 15);
-    const int py = sy0 + (lane >> 4);
+    const int px = sx0 + lane % kStripW;
+    const int py = sy0 + lane / kStripW;
     if (px < d.W && py < d.H) {
         const int64_t pix = b * HW + (int64_t)py * d.W + px;
         im.final_T[pix] = T;
@@ -87,9 +87,9 @@ __device__ __forceinline__ void store_strip(const Dims& d, const ImageArena& im,
     const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
         o.out_color + (int64_t)b * GSR_C * HW, 0, (int)((int64_t)GSR_C * HW * 4), 0x00020000);
     const int j = lane & 31;
-    const int qx = tx * GSR_BX + (j & 15);
-    const int qy0 = sy0 + (j >> 4);
-    const int qy1 = qy0 + 2;
+    const int qx = sx0 + j % kStripW;
+    const int qy0 = sy0 + j / kStripW;
+    const int qy1 = qy0 + 32 / kStripW;  // the upper 32 pixels of the strip
     const int hi = lane >> 5;
     const int hoff = hi * 4 * (int)HW;  // channels +4 for the upper half-wave
     const int v0 = (qx < d.W && qy0 < d.H) ? (hoff + qy0 * d.W + qx) * 4 : 0x7FFFFFF0;
@@ -208,9 +208,12 @@ __device__ __forceinline__ void render_fwd_body(const Dims& d, const Inputs& in,
             const int b = tile_g / d.T;
             const int t = tile_g - b * d.T;
             const floatx16 unused = {};
-            for (int sp = 0; sp < kStrips; sp++)
-                store_strip<true, REFINE>(d, im, o, in.bg + in.s_bg * b, b, t % d.gx, (t / d.gx) * GSR_BY + sp * 4,
-                                  lane, unused, unused, 1.0f, 0.f, 0u);
+            for (int sp = 0; sp < kStrips; sp++) {
+                int ex0, ey0;
+                strip_origin(t % d.gx, t / d.gx, sp, ex0, ey0);
+                store_strip<true, REFINE>(d, im, o, in.bg + in.s_bg * b, b, ex0, ey0, lane, unused, unused,
+                                          1.0f, 0.f, 0u);
+            }
             continue;
         }
         // the longest strips bound the kernel's latency: give them issue priority on their SIMD
@@ -223,8 +226,10 @@ __device__ __forceinline__ void render_fwd_body(const Dims& d, const Inputs& in,
         const int b = tile_g / d.T;
         const int t = tile_g - b * d.T;
         const int tx = t % d.gx, ty = t / d.gx;
-        const int px = tx * GSR_BX + (lane & 15);
-        const int py = ty * GSR_BY + strip * 4 + (lane >> 4);
+        int sx0, sy0;
+        strip_origin(tx, ty, strip, sx0, sy0);
+        const int px = sx0 + lane % kStripW;
+        const int py = sy0 + lane / kStripW;
         const float pfx = (float)px, pfy = (float)py;
         bool done = !(px < d.W && py < d.H);
         float T = 1.0f, invd = 0.f;
@@ -372,7 +377,7 @@ __device__ __forceinline__ void render_fwd_body(const Dims& d, const Inputs& in,
             rec[2] = (uint32_t)n_steps;
             rec[3] = __builtin_amdgcn_s_getreg((3 << 11) | 20) & 7u;
         }
-        store_strip<false, REFINE>(d, im, o, in.bg + in.s_bg * b, b, tx, ty * GSR_BY + strip * 4, lane, acc0, acc1, T,
+        store_strip<false, REFINE>(d, im, o, in.bg + in.s_bg * b, b, sx0, sy0, lane, acc0, acc1, T,
                            invd, last);
     }
 }

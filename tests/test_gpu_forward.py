@@ -113,7 +113,7 @@ def test_render_counters_match_oracle(kind, P, W, H):
 
 
 def test_strip_work_list():
-    """k_strip_count / k_strip_place: survivors per 16x4 strip equal the popcount of that strip's
+    """k_strip_count / k_strip_place: survivors per 64-pixel strip equal the popcount of that strip's
     bit over the tile's list, and the strip work list holds every strip of every non-empty tile
     exactly once, tile-major (GSR_STRIP_ORDER default): a tile's 4 strips consecutive, tiles in
     non-increasing order of their longest strip up to the 4-buckets-per-octave granularity."""
