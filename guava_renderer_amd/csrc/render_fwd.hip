@@ -239,7 +239,10 @@ __device__ __forceinline__ void render_fwd_body(const Dims& d, const Inputs& in,
         const int n = (int)(range.y - range.x);
         const uint32_t* __restrict__ plist = bn.point_list + range.x;
         const float4* __restrict__ rrec = g.rrec + (int64_t)b * d.P * 2;
-        const float* __restrict__ colors = in.colors + in.s_colors * b;
+        // feature rows through a buffer resource: 32-bit byte offsets, the base in SGPRs
+        const __amdgpu_buffer_rsrc_t frs = __builtin_amdgcn_make_buffer_rsrc(
+            const_cast<float*>(in.colors + in.s_colors * b), 0, (int)min((int64_t)d.P * GSR_C * 4, (int64_t)0x7FFFFFFF),
+            0x00020000);
 
         floatx16 acc0, acc1;
 #pragma unroll
@@ -287,7 +290,8 @@ __device__ __forceinline__ void render_fwd_body(const Dims& d, const Inputs& in,
             S##pa = pa_; S##pb = pb_;                                                               \
             S##a0 = rrec[2 * ga_]; S##a1 = rrec[2 * ga_ + 1];                                       \
             S##b0 = rrec[2 * gb_]; S##b1 = rrec[2 * gb_ + 1];                                       \
-            S##f = ABL == 2 ? 0.f : colors[(int64_t)(hi ? gb_ : ga_) * GSR_C + ch];                 \
+            S##f = ABL == 2 ? 0.f : __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(           \
+                frs, (int)(((hi ? gb_ : ga_) * GSR_C + ch) * 4), 0, 0));                            \
         }
         // stage 2: the pixel-local alphas of slot S (a missing survivor has alpha 0)
 #define GSR_ALPHA(S)                                                                                \
