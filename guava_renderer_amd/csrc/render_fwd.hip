@@ -414,7 +414,10 @@ void launch_render_fwd(const Dims& d, const Inputs& in, const GeomArena& g, cons
     static const int ablate = [] { const char* e = getenv("GSR_RENDER_ABLATE"); return e ? atoi(e) : 0; }();
     const int nwaves = d.B * d.T * kStrips;  // upper bound of the work items
     if (nwaves == 0) return;
-    const int grid = min((nwaves + 3) / 4, persistent_grid(8));
+    // workgroups per CU: resident capacity (4 waves/SIMD at the kernel's register count) by default,
+    // so no render workgroup waits in the dispatcher ahead of another stream's kernels
+    static const int wg_per_cu = [] { const char* e = getenv("GSR_RENDER_WG_PER_CU"); return e ? atoi(e) : 4; }();
+    const int grid = min((nwaves + 3) / 4, persistent_grid(wg_per_cu));
     const dim3 gr(grid), bl(GSR_TILE_PIX);
 #define GSR_LAUNCH(E, S, L) hipLaunchKernelGGL((k_render_fwd<E, S, L>), gr, bl, 0, s, d, in, g, im, b, o)
     if (o.stats) { if (exact) GSR_LAUNCH(true, true, false); else GSR_LAUNCH(false, true, false); }
