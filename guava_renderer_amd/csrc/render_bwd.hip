@@ -34,39 +34,38 @@ __device__ __forceinline__ void wave_lds_order() {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
+template <int CTRL>
+__device__ __forceinline__ float dpp(float x) {
+    return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), CTRL, 0xF, 0xF, false));
+}
+
 // Reduce v[8] across the 64 lanes; lane l ends holding the sum of component
-// ((l>>5)&1)*4 + ((l>>4)&1)*2 + ((l>>3)&1) (complete in every lane of its group of 8).
+// ((l>>5)&1)*4 + ((l>>4)&1)*2 + ((l>>3)&1) (complete in every lane of its group of 8).  VALU only:
+// v_permlane32_swap / v_permlane16_swap halve across the wave halves and rows, DPP row_ror:8 across
+// the half-rows, then quad_perm and row_half_mirror finish inside each group of 8 -- no LDS
+// round trip (ds_bpermute) in the per-Gaussian chain.
 __device__ __forceinline__ float wave_transpose_reduce8(const float (&v)[8]) {
     const int lane = threadIdx.x & 63;
     float a[4];
-    {
-        const bool hi = lane & 32;
 #pragma unroll
-        for (int k = 0; k < 4; k++) {
-            const float keep = hi ? v[k + 4] : v[k];
-            const float send = hi ? v[k] : v[k + 4];
-            a[k] = keep + __shfl_xor(send, 32);
-        }
+    for (int k = 0; k < 4; k++) {  // lanes 0-31 keep component k, lanes 32-63 component k+4
+        const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(v[k]), __float_as_uint(v[k + 4]),
+                                                         false, false);
+        a[k] = __uint_as_float(sw[0]) + __uint_as_float(sw[1]);
     }
     float bb[2];
-    {
-        const bool hi = lane & 16;
 #pragma unroll
-        for (int k = 0; k < 2; k++) {
-            const float keep = hi ? a[k + 2] : a[k];
-            const float send = hi ? a[k] : a[k + 2];
-            bb[k] = keep + __shfl_xor(send, 16);
-        }
+    for (int k = 0; k < 2; k++) {  // even rows keep a[k], odd rows a[k+2]
+        const auto sw = __builtin_amdgcn_permlane16_swap(__float_as_uint(a[k]), __float_as_uint(a[k + 2]),
+                                                         false, false);
+        bb[k] = __uint_as_float(sw[0]) + __uint_as_float(sw[1]);
     }
-    float c;
-    {
-        const bool hi = lane & 8;
-        const float keep = hi ? bb[1] : bb[0];
-        const float send = hi ? bb[0] : bb[1];
-        c = keep + __shfl_xor(send, 8);
-    }
-#pragma unroll
-    for (int off = 4; off > 0; off >>= 1) c += __shfl_xor(c, off);
+    const float c0 = bb[0] + dpp<0x128>(bb[0]);  // row_ror:8 = the other half-row
+    const float c1 = bb[1] + dpp<0x128>(bb[1]);
+    float c = (lane & 8) ? c1 : c0;
+    c += dpp<0xB1>(c);   // quad_perm [1,0,3,2]
+    c += dpp<0x4E>(c);   // quad_perm [2,3,0,1]
+    c += dpp<0x141>(c);  // row_half_mirror: the other quad of the group of 8
     return c;
 }
 
