@@ -29,6 +29,8 @@
 namespace gsr {
 
 typedef float floatx16 __attribute__((ext_vector_type(16)));
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef unsigned uint4x __attribute__((ext_vector_type(4)));
 
 // The blend step of forward.cu:349-381 split in two (both halves are branch-free):
 //  * alpha_of: the pixel-local alpha of one Gaussian, independent of the pixel's transmittance, with
@@ -321,6 +323,13 @@ __device__ __forceinline__ void render_fwd_body(const Dims& d, const Inputs& in,
             if (ABL == 1) {  /* timing ablation: VALU stand-in for the MFMAs */                  \
                 acc0[0] = fmaf(f_, __uint_as_float(sw_[0]), acc0[0]);                               \
                 acc1[0] = fmaf(f_, __uint_as_float(sw_[1]), acc1[0]);                               \
+            } else if (ABL == 4) {  /* timing ablation: bf16 32x32x16 MFMAs in place of the f32 ones */ \
+                const unsigned fb_ = __float_as_uint(f_);                                           \
+                const bf16x8 a_ = __builtin_bit_cast(bf16x8, (uint4x)(fb_, fb_ >> 16, fb_, 0u));    \
+                const bf16x8 b0_ = __builtin_bit_cast(bf16x8, (uint4x)(sw_[0], sw_[0] >> 16, sw_[0], 0u)); \
+                const bf16x8 b1_ = __builtin_bit_cast(bf16x8, (uint4x)(sw_[1], sw_[1] >> 16, sw_[1], 0u)); \
+                acc0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a_, b0_, acc0, 0, 0, 0);               \
+                acc1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a_, b1_, acc1, 0, 0, 0);               \
             } else {                                                                                \
                 const float fa_ = ABL == 2 ? 1.0f : f_;  /* timing ablation: no feature operand */  \
                 acc0 = __builtin_amdgcn_mfma_f32_32x32x2f32(fa_, __uint_as_float(sw_[0]), acc0, 0, 0, 0); \
@@ -393,6 +402,7 @@ __global__ __launch_bounds__(GSR_TILE_PIX) void k_render_fwd(Dims d, Inputs in, 
 }
 
 // Timing ablations of the production kernel (GSR_RENDER_ABLATE=1: VALU stand-in for the MFMAs,
+// 4: bf16 32x32x16 MFMAs on dummy operands in place of the f32 ones,
 // 2: no feature loads).  Wrong images by construction; for attributing render_fwd time only.
 template <int ABL>
 __global__ __launch_bounds__(GSR_TILE_PIX) void k_render_fwd_ablate(Dims d, Inputs in, GeomArena g,
@@ -428,6 +438,7 @@ void launch_render_fwd(const Dims& d, const Inputs& in, const GeomArena& g, cons
     }
     else if (ablate == 1) hipLaunchKernelGGL((k_render_fwd_ablate<1>), gr, bl, 0, s, d, in, g, im, b, o);
     else if (ablate == 2) hipLaunchKernelGGL((k_render_fwd_ablate<2>), gr, bl, 0, s, d, in, g, im, b, o);
+    else if (ablate == 4) hipLaunchKernelGGL((k_render_fwd_ablate<4>), gr, bl, 0, s, d, in, g, im, b, o);
     else { if (exact) GSR_LAUNCH(true, false, false); else GSR_LAUNCH(false, false, false); }
 #undef GSR_LAUNCH
 }
