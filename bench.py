@@ -31,6 +31,7 @@ sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 F32_MFMA_PEAK_TFLOPS = 157.3  # dense f32-input MFMA peak (MI355X_MICROARCH.md)
+BF16_MFMA_PEAK_TFLOPS = 2500.0  # dense bf16 MFMA peak (MI355X_MICROARCH.md, no sparsity)
 C = 32
 
 
@@ -52,6 +53,9 @@ def _args():
                     help="fuse the refiner's first 1x1 conv 32->16 + leaky ReLU into the render "
                          "epilogue (inference output: 16 refiner features + 4 raw channels)")
     ap.add_argument("--fast-exp", action="store_true", help="hardware exp (not bit-exact)")
+    ap.add_argument("--exact-accum", action="store_true",
+                    help="f32 MFMA colour accumulation, bit-identical to the oracle (default: split-bf16 "
+                         "MFMA accumulation, colour within the north_star's 1e-4 L_inf, include/gsr.h)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--stages", action="store_true", help="also time every stage (extra events)")
@@ -142,6 +146,7 @@ def main():
     from guava_renderer_amd import _lib, parallel, scenes
     from guava_renderer_amd.batch import BatchRasterizer, profile_enable, profile_read, render_counters
     _lib.set_exact_exp(not a.fast_exp)
+    _lib.set_split_bf16(not a.exact_accum)
 
     wl = _workload(a.config)
     P, W, H, B = wl["P"], wl["W"], wl["H"], a.batch
@@ -326,6 +331,7 @@ def main():
                    "frames_per_step_per_gpu": B, "global_batch": B * world,
                    "parallelism": f"frame-sharded x{world}", "batches_in_flight": n_inflight,
                    "exp": "hw" if a.fast_exp else "exact-poly",
+                   "colour_accum": "f32 mfma (bit-exact)" if a.exact_accum else "split-bf16 mfma (<=1e-4)",
                    "instances_per_step": R_total, "visible_gaussians_per_frame": P_vis / B},
         "roofline": {"bound": "hbm", "kernel": "render_fwd",
                      "achieved": round(achieved, 1) if achieved else None,
@@ -337,12 +343,16 @@ def main():
                           "achieved_GBs": round(_path_alg_bytes(P, W, H) * fps / 1e9, 1),
                           "frac": round(_path_alg_bytes(P, W, H) * fps / 1e9 / HBM_PEAK_GBS, 4)},
     }
-    # per-frame work of the render kernel and its matrix-core utilisation (f32 MFMA, dense peak)
+    # per-frame work of the render kernel and its matrix-core utilisation (dense peak of the MFMA used)
     ksteps = work["mfma_ksteps"]
-    mfma_flops = ksteps * 2 * (2 * 32 * 32 * 2)  # two v_mfma_f32_32x32x2f32 per wave k-step
+    if a.exact_accum:
+        mfma_flops = ksteps * 2 * (2 * 32 * 32 * 2)  # two v_mfma_f32_32x32x2f32 per wave k-step
+    else:  # two v_mfma_f32_32x32x16_bf16 per wave k-step (8 of 16 k-slots carry split products)
+        mfma_flops = ksteps * 2 * (2 * 32 * 32 * 16)
     out["render_work_per_frame"] = {k: round(v / B, 1) for k, v in work.items()}
     out["render_mfma"] = {"issued_tflops": round(mfma_flops / (render_ms * 1e-3) / 1e12, 2) if render_ms else None,
-                          "peak_tflops": F32_MFMA_PEAK_TFLOPS,
+                          "peak_tflops": F32_MFMA_PEAK_TFLOPS if a.exact_accum else BF16_MFMA_PEAK_TFLOPS,
+                          "instruction": "v_mfma_f32_32x32x2_f32" if a.exact_accum else "v_mfma_f32_32x32x16_bf16",
                           "useful_frac": round(work["pairs_contributing"] / max(64 * work["strip_pairs_blended"], 1), 4)}
     if deform_ms is not None:
         out["deform_ms_per_step"] = round(deform_ms, 4)

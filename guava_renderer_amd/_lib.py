@@ -9,7 +9,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "lib", "libgsr.so")
 
 # every symbol declared in include/*.h
-EXPORTS = ("gsr_version", "gsr_last_error", "gsr_set_exact_exp", "gsr_geometry_bytes",
+EXPORTS = ("gsr_version", "gsr_last_error", "gsr_set_exact_exp", "gsr_set_split_bf16", "gsr_geometry_bytes",
            "gsr_image_bytes", "gsr_binning_bytes", "gsr_mark_visible", "gsr_forward",
            "gsr_backward", "gsr_batch_workspace_bytes", "gsr_forward_batch",
            "gsr_backward_batch", "gsr_batch_status", "gsr_profile_enable", "gsr_profile_read",
@@ -63,6 +63,8 @@ def load(path=None):
     L.gsr_last_error.restype = ctypes.c_char_p
     L.gsr_set_exact_exp.argtypes = [_i]
     L.gsr_set_exact_exp.restype = _i
+    L.gsr_set_split_bf16.argtypes = [_i]
+    L.gsr_set_split_bf16.restype = _i
     L.gsr_geometry_bytes.argtypes = [_i, _i, _i]
     L.gsr_geometry_bytes.restype = _sz
     L.gsr_image_bytes.argtypes = [_i, _i]
@@ -135,3 +137,8 @@ def check(rc, what):
 
 def set_exact_exp(on=True):
     return load().gsr_set_exact_exp(1 if on else 0)
+
+
+def set_split_bf16(on=True):
+    """Split-bf16 MFMA colour accumulation (tolerance mode, include/gsr.h); returns the previous setting."""
+    return load().gsr_set_split_bf16(1 if on else 0)

@@ -17,6 +17,7 @@ namespace {
 
 thread_local std::string g_err;
 int g_exact_exp = 1;
+int g_split_bf16 = 0;
 uint64_t* g_render_counters = nullptr;  // gsr_render_counters
 uint32_t* g_timeline = nullptr;         // gsr_render_timeline
 uint32_t g_timeline_cap = 0;
@@ -181,7 +182,7 @@ int run_binning_and_render(const Dims& d, const Inputs& in, const GeomArena& g, 
         launch_strip_order(d, g, im, bn, s);
     }
     STAGE(debug, s, "ordered_scatter");
-    { StageTimer st_(6, s); launch_render_fwd(d, in, g, im, bn, o, g_exact_exp != 0, s); }
+    { StageTimer st_(6, s); launch_render_fwd(d, in, g, im, bn, o, g_exact_exp != 0, g_split_bf16 != 0, s); }
     STAGE(debug, s, "render_fwd");
     return 0;
 }
@@ -198,6 +199,12 @@ const char* gsr_last_error(void) { return g_err.c_str(); }
 int gsr_set_exact_exp(int on) {
     int prev = g_exact_exp;
     g_exact_exp = on ? 1 : 0;
+    return prev;
+}
+
+int gsr_set_split_bf16(int on) {
+    int prev = g_split_bf16;
+    g_split_bf16 = on ? 1 : 0;
     return prev;
 }
 

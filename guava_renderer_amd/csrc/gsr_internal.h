@@ -229,7 +229,7 @@ void launch_strip_order(const Dims& d, const GeomArena& g, const ImageArena& im,
 void launch_ordered_scatter(const Dims& d, const GeomArena& g, const ImageArena& im,
                             const BinArena& b, hipStream_t s);
 void launch_render_fwd(const Dims& d, const Inputs& in, const GeomArena& g, const ImageArena& im,
-                       const BinArena& b, const Outputs& o, bool exact, hipStream_t s);
+                       const BinArena& b, const Outputs& o, bool exact, bool split, hipStream_t s);
 void launch_render_bwd(const Dims& d, const Inputs& in, const GeomArena& g, const ImageArena& im,
                        const BinArena& b, const Grads& gr, bool exact, hipStream_t s);
 void launch_preprocess_bwd(const Dims& d, const Inputs& in, const GeomArena& g, const Grads& gr,

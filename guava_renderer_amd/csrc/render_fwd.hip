@@ -61,6 +61,29 @@ __device__ __forceinline__ float take_step(float alpha, float inv_depth, uint32_
     return w;
 }
 
+// Split-bf16 accumulation (gsr_set_split_bf16): f = f_hi + f_lo with f_hi = bf16_rne(f),
+// f_lo = bf16_rne(f - f_hi); the four bf16 products f_hi.w_hi + f_lo.w_hi + f_hi.w_lo + f_lo.w_lo
+// are exact in f32, so the only loss is the split residual (|f - f_hi - f_lo| <= 2^-17 |f|, the same
+// for w): <= 3e-5 relative per product, summed under sum(w) <= 1.  One v_mfma_f32_32x32x16_bf16
+// (8 passes) replaces the 16-pass f32 MFMA per pixel half.
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+typedef float float2x __attribute__((ext_vector_type(2)));
+// v_cvt_pk_bf16_f32 (round to nearest even) of (x, y), x in the low half
+__device__ __forceinline__ unsigned cvt_pk_bf16(float x, float y) {
+    return __builtin_bit_cast(unsigned, __builtin_convertvector((float2x){x, y}, bf16x2));
+}
+// (hi, lo) packed low|high: hi = bf16(f), lo = bf16(f - hi)
+__device__ __forceinline__ unsigned split_hl(float f) {
+    const float hf = __uint_as_float(cvt_pk_bf16(f, f) << 16);
+    return cvt_pk_bf16(hf, f - hf);
+}
+// (hi, hi) and (lo, lo)
+__device__ __forceinline__ void split_hh_ll(float w, unsigned& hh, unsigned& ll) {
+    hh = cvt_pk_bf16(w, w);
+    const float r = w - __uint_as_float(hh << 16);
+    ll = cvt_pk_bf16(r, r);
+}
+
 // Epilogue of one strip: final_T, n_contrib, inverse depth (lane = pixel) and the 32
 // channel-major colour rows C + T*bg from the MFMA accumulators.  acc_n[r] at lane l holds channel
 // (r&3)+8*(r>>2)+4*(l>>5) of strip pixel 32n + (l&31), whose transmittance lives in lane 32n + (l&31).
@@ -179,7 +202,7 @@ void launch_refine_prepare(int n, const float* in, const float* w, int n_out, in
 // in three rotating register slots: the records and feature operand of step s+3 are loaded while
 // step s+1's alphas (the exp-heavy, transmittance-independent part) are computed and step s's
 // serial blend and MFMA accumulation run.
-template <bool EXACT, bool STATS, bool TL, bool REFINE, int ABL = 0>
+template <bool EXACT, bool STATS, bool TL, bool REFINE, int ABL = 0, bool SPLIT = false>
 __device__ __forceinline__ void render_fwd_body(const Dims& d, const Inputs& in, const GeomArena& g,
                                                 const ImageArena& im, const BinArena& bn,
                                                 const Outputs& o) {
@@ -247,6 +270,7 @@ __device__ __forceinline__ void render_fwd_body(const Dims& d, const Inputs& in,
             0x00020000);
 
         floatx16 acc0, acc1;
+        uint4x sa_ = {0u, 0u, 0u, 0u}, sb0_ = {0u, 0u, 0u, 0u}, sb1_ = {0u, 0u, 0u, 0u};  // SPLIT operands, k 4..7 stay 0
 #pragma unroll
         for (int r = 0; r < 16; r++) { acc0[r] = 0.f; acc1[r] = 0.f; }
         uint64_t n_surv = 0, n_steps = 0, n_contrib_pairs = 0, n_staged = 0;
@@ -302,6 +326,7 @@ __device__ __forceinline__ void render_fwd_body(const Dims& d, const Inputs& in,
             S##bl = S##hb ? alpha_of<EXACT>(S##b0, S##b1, pfx, pfy) : 0.f;                          \
             S##ai = S##a0.w;                                                                        \
             S##bi = S##b0.w;                                                                        \
+            if (SPLIT) S##fp = split_hl(S##f);                                                      \
         }
         // stage 3: the serial blend of slot S and its accumulation on the matrix cores
 #define GSR_TAKE(S)                                                                                 \
@@ -330,6 +355,17 @@ __device__ __forceinline__ void render_fwd_body(const Dims& d, const Inputs& in,
                 const bf16x8 b1_ = __builtin_bit_cast(bf16x8, (uint4x)(sw_[1], sw_[1] >> 16, sw_[1], 0u)); \
                 acc0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a_, b0_, acc0, 0, 0, 0);               \
                 acc1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a_, b1_, acc1, 0, 0, 0);               \
+            } else if (SPLIT) {  /* k 0..3 of each half: f_hi.w_hi + f_lo.w_hi + f_hi.w_lo + f_lo.w_lo */ \
+                const unsigned fp_ = (S##v && (!hi || S##hb)) ? S##fp : 0u;                         \
+                sa_.x = fp_; sa_.y = fp_;                                                           \
+                unsigned h0_, l0_, h1_, l1_;                                                        \
+                split_hh_ll(__uint_as_float(sw_[0]), h0_, l0_);                                     \
+                split_hh_ll(__uint_as_float(sw_[1]), h1_, l1_);                                     \
+                sb0_.x = h0_; sb0_.y = l0_; sb1_.x = h1_; sb1_.y = l1_;                             \
+                acc0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, sa_),     \
+                                                               __builtin_bit_cast(bf16x8, sb0_), acc0, 0, 0, 0); \
+                acc1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, sa_),     \
+                                                               __builtin_bit_cast(bf16x8, sb1_), acc1, 0, 0, 0); \
             } else {                                                                                \
                 const float fa_ = ABL == 2 ? 1.0f : f_;  /* timing ablation: no feature operand */  \
                 acc0 = __builtin_amdgcn_mfma_f32_32x32x2f32(fa_, __uint_as_float(sw_[0]), acc0, 0, 0, 0); \
@@ -337,7 +373,7 @@ __device__ __forceinline__ void render_fwd_body(const Dims& d, const Inputs& in,
             }                                                                                       \
         }
 #define GSR_SLOT(S) bool S##v, S##hb; int S##pa, S##pb; float4 S##a0, S##a1, S##b0, S##b1; \
-        float S##f, S##al, S##bl, S##ai, S##bi;
+        float S##f, S##al, S##bl, S##ai, S##bi; unsigned S##fp = 0;
         GSR_SLOT(A)
         GSR_SLOT(B)
         GSR_SLOT(C)
@@ -395,10 +431,10 @@ __device__ __forceinline__ void render_fwd_body(const Dims& d, const Inputs& in,
     }
 }
 
-template <bool EXACT, bool STATS, bool TL>
+template <bool EXACT, bool STATS, bool TL, bool SPLIT = false>
 __global__ __launch_bounds__(GSR_TILE_PIX) void k_render_fwd(Dims d, Inputs in, GeomArena g,
                                                              ImageArena im, BinArena bn, Outputs o) {
-    render_fwd_body<EXACT, STATS, TL, false>(d, in, g, im, bn, o);
+    render_fwd_body<EXACT, STATS, TL, false, 0, SPLIT>(d, in, g, im, bn, o);
 }
 
 // Timing ablations of the production kernel (GSR_RENDER_ABLATE=1: VALU stand-in for the MFMAs,
@@ -420,7 +456,7 @@ __global__ __launch_bounds__(GSR_TILE_PIX) __attribute__((amdgpu_waves_per_eu(4)
 }
 
 void launch_render_fwd(const Dims& d, const Inputs& in, const GeomArena& g, const ImageArena& im,
-                       const BinArena& b, const Outputs& o, bool exact, hipStream_t s) {
+                       const BinArena& b, const Outputs& o, bool exact, bool split, hipStream_t s) {
     static const int ablate = [] { const char* e = getenv("GSR_RENDER_ABLATE"); return e ? atoi(e) : 0; }();
     const int nwaves = d.B * d.T * kStrips;  // upper bound of the work items
     if (nwaves == 0) return;
@@ -439,6 +475,10 @@ void launch_render_fwd(const Dims& d, const Inputs& in, const GeomArena& g, cons
     else if (ablate == 1) hipLaunchKernelGGL((k_render_fwd_ablate<1>), gr, bl, 0, s, d, in, g, im, b, o);
     else if (ablate == 2) hipLaunchKernelGGL((k_render_fwd_ablate<2>), gr, bl, 0, s, d, in, g, im, b, o);
     else if (ablate == 4) hipLaunchKernelGGL((k_render_fwd_ablate<4>), gr, bl, 0, s, d, in, g, im, b, o);
+    else if (split) {
+        if (exact) hipLaunchKernelGGL((k_render_fwd<true, false, false, true>), gr, bl, 0, s, d, in, g, im, b, o);
+        else hipLaunchKernelGGL((k_render_fwd<false, false, false, true>), gr, bl, 0, s, d, in, g, im, b, o);
+    }
     else { if (exact) GSR_LAUNCH(true, false, false); else GSR_LAUNCH(false, false, false); }
 #undef GSR_LAUNCH
 }

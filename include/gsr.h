@@ -55,6 +55,13 @@ const char* gsr_last_error(void);
  * 0 = hardware v_exp_f32.  Returns the previous setting. */
 int gsr_set_exact_exp(int on);
 
+/* Colour accumulation of the forward blend: 0 = f32 MFMA, bit-identical to the reference's
+ * fmaf chain (default); 1 = split-bf16 MFMA (f = f_hi + f_lo, four exact bf16 products per
+ * feature x weight, f32 accumulation): <= 3e-5 relative per product, colour L-inf within the
+ * north_star's 1e-4; final_T, n_contrib and inverse depth stay bit-exact.  Returns the previous
+ * setting.  No reference counterpart (forward.cu:371-372 accumulates in f32). */
+int gsr_set_split_bf16(int on);
+
 /* Scratch sizes used by gsr_forward (the three resizer requests).  Unlike the reference's
  * GeometryState, the geometry arena also holds the per-frame depth sort and the (depth chunk x tile)
  * instance-count table, so it depends on the image size too.  Images are limited to 16384 tiles

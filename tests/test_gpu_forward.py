@@ -77,6 +77,31 @@ def test_forward_fast_exp_tolerance():
         L.set_exact_exp(True)
 
 
+@pytest.mark.parametrize("kind,P,W,H", [("random", 10000, 256, 256), ("avatar", 20000, 200, 136)])
+def test_forward_split_bf16_tolerance(kind, P, W, H):
+    """gsr_set_split_bf16(1): the colour accumulation runs as four exact bf16 products per
+    feature x weight on v_mfma_f32_32x32x16_bf16.  Everything the blend decides on VALU stays
+    bit-exact (radii, lists, n_contrib, final_T, inverse depth); the 32 channels are within the
+    north_star's 1e-4 L_inf of the oracle (bound: 3e-5 relative per product, sum of weights <= 1)."""
+    L = _lib()
+    L.set_exact_exp(True)
+    prev = L.set_split_bf16(True)
+    try:
+        d = make_scene(kind, P, W, H, seed=12)
+        g_col, g_radii, g_inv, gs = gpu_forward(d)
+        o_col, o_radii, o_inv, os_ = oracle_forward(d, exact=True)
+        np.testing.assert_array_equal(g_radii, o_radii)
+        np.testing.assert_array_equal(gs["point_list"][:gs["R"]], os_["point_list"])
+        np.testing.assert_array_equal(gs["n_contrib"], os_["n_contrib"])
+        np.testing.assert_array_equal(gs["final_T"], os_["final_T"])
+        np.testing.assert_array_equal(g_inv, o_inv)
+        err = np.abs(g_col - o_col)
+        assert err.max() <= 1e-4, err.max()
+        assert err.max() > 0.0  # the mode really ran (f32 accumulation is bit-exact)
+    finally:
+        L.set_split_bf16(bool(prev))
+
+
 def test_forward_precomputed_cov3D():
     _lib().set_exact_exp(True)
     import oracle

@@ -19,10 +19,11 @@ from helpers import decode, image_layout, oracle_forward
 pytestmark = pytest.mark.gpu
 
 
-def _batch_render(sc, cams, colors=None):
+def _batch_render(sc, cams, colors=None, split_bf16=False):
     from guava_renderer_amd import _lib
     from guava_renderer_amd.batch import BatchRasterizer
     _lib.set_exact_exp(True)
+    _lib.set_split_bf16(split_bf16)
     dev = torch.device("cuda")
     t = lambda x: torch.tensor(np.ascontiguousarray(x), device=dev)  # noqa: E731
     B = len(cams)
@@ -36,6 +37,7 @@ def _batch_render(sc, cams, colors=None):
                                 t(sc["opacities"]), t(sc["scales"]), t(sc["rotations"]), views, projs, tanf,
                                 torch.zeros((B, 32), device=dev))
     torch.cuda.synchronize()
+    _lib.set_split_bf16(False)
     R, ovf = r.status()
     assert not ovf
     return r, col.cpu().numpy(), inv.cpu().numpy(), radii.cpu().numpy()
@@ -54,6 +56,24 @@ def test_full_size_frame_bit_exact(P, W, gpt):
     np.testing.assert_array_equal(radii[0], o_radii)
     np.testing.assert_array_equal(col[0], o_col)
     np.testing.assert_array_equal(inv[0].reshape(o_inv.shape), o_inv)
+
+
+def test_full_size_frame_split_bf16():
+    """The bench's colour-accumulation mode at config-2 size: colour within the north_star's 1e-4
+    L_inf of the oracle, inverse depth and radii bit-exact."""
+    from guava_renderer_amd import scenes
+    sc = scenes.avatar_cloud(100000, seed=0)
+    cam = scenes.frame_cameras(2, 512, 512, seed=1000)[1]
+    _, col, inv, radii = _batch_render(sc, [cam], split_bf16=True)
+    import oracle
+    oracle.set_threads(8)
+    d = dict(sc, **cam, bg=np.zeros(32, np.float32))
+    o_col, o_radii, o_inv, _ = oracle_forward(d, exact=True)
+    np.testing.assert_array_equal(radii[0], o_radii)
+    np.testing.assert_array_equal(inv[0].reshape(o_inv.shape), o_inv)
+    err = np.abs(col[0] - o_col)
+    print("split-bf16 colour L_inf vs oracle:", err.max(), "RGB:", err[:3].max())
+    assert err.max() <= 1e-4, err.max()
 
 
 def test_full_batch_invariants():
