@@ -82,6 +82,7 @@ struct GeomArena {
     uint32_t* big;        // worklist of buckets longer than kTinyBucket: frame * NB + bucket
     uint32_t* order;      // per frame, visible Gaussians in (depth, index) order
     uint32_t* table;      // [B][nchunk][T] instance counts per (depth chunk, tile), scanned per tile
+    uint32_t* fsplit;     // [P][32] features pre-split for the split-bf16 blend: bf16 (hi | lo << 16)
 };
 
 struct ImageArena {

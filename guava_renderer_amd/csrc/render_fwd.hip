@@ -84,6 +84,14 @@ __device__ __forceinline__ void split_hh_ll(float w, unsigned& hh, unsigned& ll)
     ll = cvt_pk_bf16(r, r);
 }
 
+// The split of a batch-shared feature table, once per launch (P x 32 words; render_fwd then loads
+// the packed word in place of the f32 feature).
+__global__ __launch_bounds__(256) void k_split_features(int n, const float* __restrict__ f,
+                                                        uint32_t* __restrict__ out) {
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i < n) out[i] = split_hl(f[i]);
+}
+
 // Epilogue of one strip: final_T, n_contrib, inverse depth (lane = pixel) and the 32
 // channel-major colour rows C + T*bg from the MFMA accumulators.  acc_n[r] at lane l holds channel
 // (r&3)+8*(r>>2)+4*(l>>5) of strip pixel 32n + (l&31), whose transmittance lives in lane 32n + (l&31).
@@ -202,7 +210,7 @@ void launch_refine_prepare(int n, const float* in, const float* w, int n_out, in
 // in three rotating register slots: the records and feature operand of step s+3 are loaded while
 // step s+1's alphas (the exp-heavy, transmittance-independent part) are computed and step s's
 // serial blend and MFMA accumulation run.
-template <bool EXACT, bool STATS, bool TL, bool REFINE, int ABL = 0, bool SPLIT = false>
+template <bool EXACT, bool STATS, bool TL, bool REFINE, int ABL = 0, int SPLIT = 0>
 __device__ __forceinline__ void render_fwd_body(const Dims& d, const Inputs& in, const GeomArena& g,
                                                 const ImageArena& im, const BinArena& bn,
                                                 const Outputs& o) {
@@ -265,9 +273,10 @@ __device__ __forceinline__ void render_fwd_body(const Dims& d, const Inputs& in,
         const uint32_t* __restrict__ plist = bn.point_list + range.x;
         const float4* __restrict__ rrec = g.rrec + (int64_t)b * d.P * 2;
         // feature rows through a buffer resource: 32-bit byte offsets, the base in SGPRs
+        // (SPLIT == 2: the pre-split (hi, lo) words of k_split_features, shared by every frame)
         const __amdgpu_buffer_rsrc_t frs = __builtin_amdgcn_make_buffer_rsrc(
-            const_cast<float*>(in.colors + in.s_colors * b), 0, (int)min((int64_t)d.P * GSR_C * 4, (int64_t)0x7FFFFFFF),
-            0x00020000);
+            SPLIT == 2 ? (void*)g.fsplit : (void*)(in.colors + in.s_colors * b), 0,
+            (int)min((int64_t)d.P * GSR_C * 4, (int64_t)0x7FFFFFFF), 0x00020000);
 
         floatx16 acc0, acc1;
         uint4x sa_ = {0u, 0u, 0u, 0u}, sb0_ = {0u, 0u, 0u, 0u}, sb1_ = {0u, 0u, 0u, 0u};  // SPLIT operands, k 4..7 stay 0
@@ -326,7 +335,7 @@ __device__ __forceinline__ void render_fwd_body(const Dims& d, const Inputs& in,
             S##bl = S##hb ? alpha_of<EXACT>(S##b0, S##b1, pfx, pfy) : 0.f;                          \
             S##ai = S##a0.w;                                                                        \
             S##bi = S##b0.w;                                                                        \
-            if (SPLIT) S##fp = split_hl(S##f);                                                      \
+            if (SPLIT) S##fp = SPLIT == 2 ? __float_as_uint(S##f) : split_hl(S##f);                 \
         }
         // stage 3: the serial blend of slot S and its accumulation on the matrix cores
 #define GSR_TAKE(S)                                                                                 \
@@ -431,7 +440,7 @@ __device__ __forceinline__ void render_fwd_body(const Dims& d, const Inputs& in,
     }
 }
 
-template <bool EXACT, bool STATS, bool TL, bool SPLIT = false>
+template <bool EXACT, bool STATS, bool TL, int SPLIT = 0>
 __global__ __launch_bounds__(GSR_TILE_PIX) void k_render_fwd(Dims d, Inputs in, GeomArena g,
                                                              ImageArena im, BinArena bn, Outputs o) {
     render_fwd_body<EXACT, STATS, TL, false, 0, SPLIT>(d, in, g, im, bn, o);
@@ -475,9 +484,15 @@ void launch_render_fwd(const Dims& d, const Inputs& in, const GeomArena& g, cons
     else if (ablate == 1) hipLaunchKernelGGL((k_render_fwd_ablate<1>), gr, bl, 0, s, d, in, g, im, b, o);
     else if (ablate == 2) hipLaunchKernelGGL((k_render_fwd_ablate<2>), gr, bl, 0, s, d, in, g, im, b, o);
     else if (ablate == 4) hipLaunchKernelGGL((k_render_fwd_ablate<4>), gr, bl, 0, s, d, in, g, im, b, o);
+    else if (split && in.s_colors == 0) {  // one feature set for the batch: split it once
+        hipLaunchKernelGGL(k_split_features, dim3((d.P * GSR_C + 255) / 256), dim3(256), 0, s,
+                           d.P * GSR_C, in.colors, g.fsplit);
+        if (exact) hipLaunchKernelGGL((k_render_fwd<true, false, false, 2>), gr, bl, 0, s, d, in, g, im, b, o);
+        else hipLaunchKernelGGL((k_render_fwd<false, false, false, 2>), gr, bl, 0, s, d, in, g, im, b, o);
+    }
     else if (split) {
-        if (exact) hipLaunchKernelGGL((k_render_fwd<true, false, false, true>), gr, bl, 0, s, d, in, g, im, b, o);
-        else hipLaunchKernelGGL((k_render_fwd<false, false, false, true>), gr, bl, 0, s, d, in, g, im, b, o);
+        if (exact) hipLaunchKernelGGL((k_render_fwd<true, false, false, 1>), gr, bl, 0, s, d, in, g, im, b, o);
+        else hipLaunchKernelGGL((k_render_fwd<false, false, false, 1>), gr, bl, 0, s, d, in, g, im, b, o);
     }
     else { if (exact) GSR_LAUNCH(true, false, false); else GSR_LAUNCH(false, false, false); }
 #undef GSR_LAUNCH
