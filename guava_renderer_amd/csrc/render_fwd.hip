@@ -319,9 +319,23 @@ __device__ __forceinline__ void render_fwd_body(const Dims& d, const Inputs& in,
         {                                                                                           \
             uint32_t ga_ = 0, gb_ = 0;                                                              \
             int pa_ = 0, pb_ = 0;                                                                   \
-            S##v = GSR_NEXT(ga_, pa_);                                                              \
-            S##hb = S##v && GSR_NEXT(gb_, pb_);                                                     \
-            if (!S##hb) { gb_ = ga_; pb_ = pa_; }                                                   \
+            if (__builtin_expect(__builtin_popcountll(mask) >= 2, 1)) {                             \
+                /* common case: both survivors from the chunk in hand, no loop, no refill test */   \
+                const int i0_ = (int)__builtin_ctzll(mask);                                         \
+                mask &= mask - 1;                                                                   \
+                const int i1_ = (int)__builtin_ctzll(mask);                                         \
+                mask &= mask - 1;                                                                   \
+                ga_ = __builtin_amdgcn_readlane(cidx, i0_) & kIndexMask;                            \
+                gb_ = __builtin_amdgcn_readlane(cidx, i1_) & kIndexMask;                            \
+                pa_ = base + i0_ + 1;                                                               \
+                pb_ = base + i1_ + 1;                                                               \
+                S##v = true;                                                                        \
+                S##hb = true;                                                                       \
+            } else {                                                                                \
+                S##v = GSR_NEXT(ga_, pa_);                                                          \
+                S##hb = S##v && GSR_NEXT(gb_, pb_);                                                 \
+                if (!S##hb) { gb_ = ga_; pb_ = pa_; }                                               \
+            }                                                                                       \
             S##pa = pa_; S##pb = pb_;                                                               \
             S##a0 = rrec[2 * ga_]; S##a1 = rrec[2 * ga_ + 1];                                       \
             S##b0 = rrec[2 * gb_]; S##b1 = rrec[2 * gb_ + 1];                                       \
