@@ -47,7 +47,7 @@ def load(path=None):
     global _lib
     if _lib is not None:
         return _lib
-    path = path or LIB_PATH
+    path = path or os.environ.get("GSR_LIB") or LIB_PATH  # GSR_LIB: A/B builds (tools/gpu_abl.sh)
     # torch-ROCm ships its own libamdhip64 (soname libamdhip64.so.7) and loads it by the
     # unversioned name; load torch first so libgsr.so binds to that same HIP runtime instead of
     # pulling /opt/rocm's copy into the process as a second runtime.

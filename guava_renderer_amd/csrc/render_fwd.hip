@@ -47,13 +47,18 @@ __device__ __forceinline__ float alpha_of(const float4 ga, const float4 gc, floa
     return (power > 0.0f || power < -87.0f) ? 0.0f : alpha;
 }
 
+// With eff = alpha where the pixel takes the Gaussian (alpha >= 1/255, not done) and 0 elsewhere,
+// test_T = T (1 - eff) equals T where nothing is taken, and a live pixel always has T >= 1e-4 (T
+// only drops to a test_T that passed the stop test), so `test_T < 1e-4` alone is the stop test:
+// the same decisions and the same products as forward.cu:352-381 with fewer lane-mask operations.
 __device__ __forceinline__ float take_step(float alpha, float inv_depth, uint32_t pos, float& T, float& invd,
                                            uint32_t& last, bool& done) {
     const bool take = !done && !(alpha < 1.0f / 255.0f);
-    const float test_T = T * (1.0f - alpha);
-    const bool term = take && (test_T < 0.0001f);
+    const float eff = take ? alpha : 0.0f;
+    const float test_T = T * (1.0f - eff);
+    const bool term = test_T < 0.0001f;
     const bool contrib = take && !term;
-    const float w = contrib ? alpha * T : 0.0f;
+    const float w = contrib ? eff * T : 0.0f;
     invd = fmaf(inv_depth, w, invd);
     T = contrib ? test_T : T;
     last = contrib ? pos : last;
@@ -90,6 +95,11 @@ __global__ __launch_bounds__(256) void k_split_features(int n, const float* __re
                                                         uint32_t* __restrict__ out) {
     const int i = blockIdx.x * 256 + threadIdx.x;
     if (i < n) out[i] = split_hl(f[i]);
+}
+
+// one 16-byte half of a render record at a wave-uniform byte offset (SGPR soffset)
+__device__ __forceinline__ float4 rec_load(__amdgpu_buffer_rsrc_t rs, uint32_t off) {
+    return __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rs, 0, (int)off, 0));
 }
 
 // Epilogue of one strip: final_T, n_contrib, inverse depth (lane = pixel) and the 32
@@ -271,7 +281,10 @@ __device__ __forceinline__ void render_fwd_body(const Dims& d, const Inputs& in,
         const uint2 range = im.ranges[tile_g];
         const int n = (int)(range.y - range.x);
         const uint32_t* __restrict__ plist = bn.point_list + range.x;
-        const float4* __restrict__ rrec = g.rrec + (int64_t)b * d.P * 2;
+        // render records through a buffer resource: the byte offset of a (wave-uniform) record is
+        // one SGPR, no 64-bit address arithmetic per survivor
+        const __amdgpu_buffer_rsrc_t rrs = __builtin_amdgcn_make_buffer_rsrc(
+            (void*)(g.rrec + (int64_t)b * d.P * 2), 0, (int)min((int64_t)d.P * 32, (int64_t)0x7FFFFFFF), 0x00020000);
         // feature rows through a buffer resource: 32-bit byte offsets, the base in SGPRs
         // (SPLIT == 2: the pre-split (hi, lo) words of k_split_features, shared by every frame)
         const __amdgpu_buffer_rsrc_t frs = __builtin_amdgcn_make_buffer_rsrc(
@@ -337,8 +350,8 @@ __device__ __forceinline__ void render_fwd_body(const Dims& d, const Inputs& in,
                 if (!S##hb) { gb_ = ga_; pb_ = pa_; }                                               \
             }                                                                                       \
             S##pa = pa_; S##pb = pb_;                                                               \
-            S##a0 = rrec[2 * ga_]; S##a1 = rrec[2 * ga_ + 1];                                       \
-            S##b0 = rrec[2 * gb_]; S##b1 = rrec[2 * gb_ + 1];                                       \
+            S##a0 = rec_load(rrs, ga_ * 32); S##a1 = rec_load(rrs, ga_ * 32 + 16);                  \
+            S##b0 = rec_load(rrs, gb_ * 32); S##b1 = rec_load(rrs, gb_ * 32 + 16);                  \
             S##f = ABL == 2 ? 0.f : __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(           \
                 frs, (int)(((hi ? gb_ : ga_) * GSR_C + ch) * 4), 0, 0));                            \
         }

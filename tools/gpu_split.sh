@@ -4,7 +4,7 @@ set -u
 cd "$GRAFT_REPO_ROOT"
 O=gpurun_out/split
 mkdir -p $O
-timeout -k 10 400 python -u -m pytest tests/test_gpu_forward.py tests/test_gpu_fullsize.py -x -v -s --timeout 120 --timeout-method thread > $O/pytest.log 2>&1; rc=$?; echo "pytest rc=$rc"; tail -4 $O/pytest.log
+timeout -k 10 400 python -u -m pytest tests/test_gpu_forward.py tests/test_gpu_fullsize.py tests/test_gpu_backward.py -x -v -s --timeout 120 --timeout-method thread > $O/pytest.log 2>&1; rc=$?; echo "pytest rc=$rc"; tail -4 $O/pytest.log
 [ $rc -eq 0 ] || exit $rc
 for args in "" "--exact-accum" ""; do
   timeout -k 10 300 python bench.py --steps 20 --warmup 5 --no-cpu-baseline --stages $args > $O/b.json 2>$O/b.err; rc=$?
