@@ -645,13 +645,15 @@ __global__ __launch_bounds__(kSlots) void k_ordered_scatter(Dims d, GeomArena g,
         s_rect[tid] = r;
         s_gi[tid] = gi;
         const int x0 = r.x & 0xFFFF, y0 = r.x >> 16, x1 = r.y & 0xFFFF, y1 = r.y >> 16;
-        for (int x = 0; x < d.gx; x++) {
-            const uint64_t m = __ballot(nt && x >= x0 && x < x1);
-            if (lane == 0) colm[4 * x + wv] = m;
-        }
-        for (int y = 0; y < d.gy; y++) {
-            const uint64_t m = __ballot(nt && y >= y0 && y < y1);
-            if (lane == 0) rowm[4 * y + wv] = m;
+        // this wave's column / row words: bit l of colm[4 x + wv] = lane l's rect covers column x.
+        // Zero them, then every lane ORs its bit into the few columns and rows its rect spans
+        // (ds_or_b64; a wave's LDS operations complete in order) instead of one ballot per column.
+        for (int x = lane; x < d.gx; x += 64) colm[4 * x + wv] = 0ull;
+        for (int y = lane; y < d.gy; y += 64) rowm[4 * y + wv] = 0ull;
+        if (nt) {
+            const unsigned long long bit = 1ull << lane;
+            for (int x = x0; x < x1; x++) atomicOr((unsigned long long*)&colm[4 * x + wv], bit);
+            for (int y = y0; y < y1; y++) atomicOr((unsigned long long*)&rowm[4 * y + wv], bit);
         }
         __syncthreads();
         for (uint32_t q = tid; q < total; q += kSlots) {
