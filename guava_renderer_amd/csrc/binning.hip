@@ -275,6 +275,51 @@ __global__ __launch_bounds__(kScanBlock) void k_bucket_count(Dims d, GeomArena g
     g.bslot[gid] = atomicAdd(&g.bstart[(int64_t)b * (d.NB + 1) + bk], 1u);
 }
 
+// The same arrival slots with the counting done in LDS: a workgroup takes kCountPer x 1024
+// consecutive Gaussians of one frame (neighbours on the avatar, so few distinct depth buckets),
+// counts them in an LDS copy of the frame's bucket table (the local slot from the LDS atomic), then
+// claims each non-empty bucket's range with ONE returning global atomic.  Slots stay unique and
+// dense per bucket; k_bucket_rank orders them.  Scattered returning global atomics run at the
+// memory side (MI355X_MICROARCH.md, global atomics), so this cuts them by the Gaussians per
+// (workgroup, bucket).
+constexpr int kCountThreads = 1024, kCountPer = 8;
+__global__ __launch_bounds__(kCountThreads) void k_bucket_count_lds(Dims d, GeomArena g) {
+    extern __shared__ uint32_t hist[];  // NB
+    if (g.ctrl[kCtrlOverflow]) return;
+    const int b = blockIdx.y;
+    const int i0 = blockIdx.x * kCountThreads * kCountPer;
+    for (int k = threadIdx.x; k < d.NB; k += kCountThreads) hist[k] = 0u;
+    __syncthreads();
+    const uint32_t kmin = ~g.fstat[kFsWords * b + kFsNotKeyMax], kmax = g.fstat[kFsWords * b + kFsKeyMax];
+    const float scale = bucket_scale(kmin, kmax, d.NB);
+    uint32_t bk[kCountPer], ls[kCountPer];
+#pragma unroll
+    for (int p = 0; p < kCountPer; p++) {
+        const int i = i0 + p * kCountThreads + threadIdx.x;
+        bk[p] = 0xFFFFFFFFu;
+        ls[p] = 0u;
+        if (i < d.P) {
+            const int64_t gid = (int64_t)b * d.P + i;
+            if (g.tiles[gid]) {
+                bk[p] = bucket_of(__float_as_uint(g.depth[gid]), kmin, scale, d.NB);
+                ls[p] = atomicAdd(&hist[bk[p]], 1u);
+            }
+        }
+    }
+    __syncthreads();
+    uint32_t* bs = g.bstart + (int64_t)b * (d.NB + 1);
+    for (int k = threadIdx.x; k < d.NB; k += kCountThreads) {
+        const uint32_t c = hist[k];
+        if (c) hist[k] = atomicAdd(&bs[k], c);
+    }
+    __syncthreads();
+#pragma unroll
+    for (int p = 0; p < kCountPer; p++) {
+        const int i = i0 + p * kCountThreads + threadIdx.x;
+        if (bk[p] != 0xFFFFFFFFu) g.bslot[(int64_t)b * d.P + i] = hist[bk[p]] + ls[p];
+    }
+}
+
 // One workgroup per frame: bucket counts -> bucket starts (entry NB = visible count); buckets
 // longer than kTinyBucket go to the segment-sort worklist.
 __global__ __launch_bounds__(1024) void k_bucket_scan(Dims d, GeomArena g) {
@@ -363,7 +408,13 @@ __global__ __launch_bounds__(NT) void k_bucket_sort(Dims d, GeomArena g) {
 
 void launch_depth_sort(const Dims& d, const GeomArena& g, hipStream_t s) {
     if (d.P == 0 || d.B == 0) return;
-    hipLaunchKernelGGL(k_bucket_count, dim3(d.nblk, d.B), dim3(kScanBlock), 0, s, d, g);
+    if ((size_t)d.NB * 4 <= 65536) {
+        const int per_wg = kCountThreads * kCountPer;
+        hipLaunchKernelGGL(k_bucket_count_lds, dim3((d.P + per_wg - 1) / per_wg, d.B), dim3(kCountThreads),
+                           (size_t)d.NB * 4, s, d, g);
+    } else {
+        hipLaunchKernelGGL(k_bucket_count, dim3(d.nblk, d.B), dim3(kScanBlock), 0, s, d, g);
+    }
     hipLaunchKernelGGL(k_bucket_scan, dim3(d.B), dim3(1024), 0, s, d, g);
     hipLaunchKernelGGL(k_bucket_scatter, dim3(d.nblk, d.B), dim3(kScanBlock), 0, s, d, g);
     hipLaunchKernelGGL(k_bucket_rank, dim3(d.nblk, d.B), dim3(kScanBlock), 0, s, d, g);
