@@ -784,12 +784,14 @@ __global__ __launch_bounds__(256) void k_strip_count(Dims d, ImageArena im, BinA
     if (tile_g >= d.B * d.T) return;
     const uint2 r = im.ranges[tile_g];
     uint32_t c[kStrips] = {};
-    for (uint32_t i = r.x + lane; i < r.y; i += 256) {
-        uint32_t e[4];
+    // 16 loads in flight per lane: the longest lists (several thousand entries) bound this kernel
+    // by their serial load round trips
+    for (uint32_t i = r.x + lane; i < r.y; i += 1024) {
+        uint32_t e[16];
 #pragma unroll
-        for (int u = 0; u < 4; u++) e[u] = i + 64u * u < r.y ? bn.point_list[i + 64u * u] : 0u;
+        for (int u = 0; u < 16; u++) e[u] = i + 64u * u < r.y ? bn.point_list[i + 64u * u] : 0u;
 #pragma unroll
-        for (int u = 0; u < 4; u++)
+        for (int u = 0; u < 16; u++)
 #pragma unroll
             for (int s = 0; s < kStrips; s++) c[s] += (e[u] >> (28 + s)) & 1u;
     }
