@@ -15,7 +15,7 @@
 //                          small buckets, LDS segment sort of the few large ones -> order[]
 //   3. k_chunk_count       per 256 depth-ordered Gaussians: tile histogram in LDS from 4 corner
 //                          updates per rect (2-D difference array) -> count table row;
-//      k_column_scan       per tile: exclusive scan down the table -> chunk bases, tile counts
+//      k_column_scan_wide  per tile: exclusive scan down the table -> chunk bases, tile counts
 //   4. k_tile_scan/place   per frame: tile counts -> ranges; longest-first render work list
 //   5. k_ordered_scatter   per chunk: load-balanced expansion of the instances over the workgroup,
 //                          stable rank = tile base + chunk base + earlier slots covering the tile
@@ -467,32 +467,61 @@ __global__ __launch_bounds__(kScanBlock) void k_chunk_count(Dims d, GeomArena g)
     }
 }
 
-// Per (frame, tile): exclusive scan of the counts down the frame's chunks, total -> tile_count.
-__global__ __launch_bounds__(kScanBlock) void k_column_scan(Dims d, GeomArena g, ImageArena im) {
+// Per tile: exclusive scan down the (chunk x tile) count table -> each chunk's base in the tile,
+// and the tile's count.  16 waves per 64 tiles: wave w sums its slice of the rows (lane = tile,
+// 8 loads in flight), the slice totals are scanned across the waves through LDS, and each wave
+// rewrites its slice from its offset (the second read hits L2).  16x the waves of one thread per
+// tile walking all rows serially (measured 75 -> 61 us per 32-frame chunk_count stage).
+constexpr int kColWaves = 16;
+__global__ __launch_bounds__(64 * kColWaves) void k_column_scan_wide(Dims d, GeomArena g, ImageArena im) {
+    __shared__ uint32_t tot[kColWaves][64];
     const int b = blockIdx.y;
-    const int t = blockIdx.x * kScanBlock + threadIdx.x;
-    if (t >= d.T) return;
-    uint32_t acc = 0;
-    if (!g.ctrl[kCtrlOverflow]) {
-        const int nc = (int)((g.fstat[kFsWords * b + kFsVisible] + d.chunk - 1) / d.chunk);
-        uint32_t* col = g.table + (int64_t)b * d.nchunk * d.T + t;
-        int c = 0;
-        for (; c + 4 <= nc; c += 4) {
-            const uint32_t v0 = col[(int64_t)c * d.T], v1 = col[(int64_t)(c + 1) * d.T];
-            const uint32_t v2 = col[(int64_t)(c + 2) * d.T], v3 = col[(int64_t)(c + 3) * d.T];
-            col[(int64_t)c * d.T] = acc;
-            col[(int64_t)(c + 1) * d.T] = acc + v0;
-            col[(int64_t)(c + 2) * d.T] = acc + v0 + v1;
-            col[(int64_t)(c + 3) * d.T] = acc + v0 + v1 + v2;
-            acc += v0 + v1 + v2 + v3;
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int t = blockIdx.x * 64 + lane;
+    const bool ok = t < d.T && !g.ctrl[kCtrlOverflow];
+    const int nc = (int)((g.fstat[kFsWords * b + kFsVisible] + d.chunk - 1) / d.chunk);
+    const int per = (nc + kColWaves - 1) / kColWaves;
+    const int c0 = w * per, c1 = min(nc, c0 + per);
+    uint32_t* col = g.table + (int64_t)b * d.nchunk * d.T + t;
+    uint32_t sum = 0;
+    if (ok) {
+        int c = c0;
+        for (; c + 8 <= c1; c += 8) {
+            uint32_t v[8];
+#pragma unroll
+            for (int u = 0; u < 8; u++) v[u] = col[(int64_t)(c + u) * d.T];
+#pragma unroll
+            for (int u = 0; u < 8; u++) sum += v[u];
         }
-        for (; c < nc; c++) {
+        for (; c < c1; c++) sum += col[(int64_t)c * d.T];
+    }
+    tot[w][lane] = sum;
+    __syncthreads();
+    uint32_t acc = 0, all = 0;
+#pragma unroll
+    for (int u = 0; u < kColWaves; u++) {
+        const uint32_t x = tot[u][lane];
+        acc += u < w ? x : 0u;
+        all += x;
+    }
+    if (ok) {
+        int c = c0;
+        for (; c + 8 <= c1; c += 8) {
+            uint32_t v[8];
+#pragma unroll
+            for (int u = 0; u < 8; u++) v[u] = col[(int64_t)(c + u) * d.T];
+#pragma unroll
+            for (int u = 0; u < 8; u++) { col[(int64_t)(c + u) * d.T] = acc; acc += v[u]; }
+        }
+        for (; c < c1; c++) {
             const uint32_t v = col[(int64_t)c * d.T];
             col[(int64_t)c * d.T] = acc;
             acc += v;
         }
+        if (w == 0) im.tile_count[(int64_t)b * d.T + t] = all;
+    } else if (t < d.T && w == 0) {
+        im.tile_count[(int64_t)b * d.T + t] = 0u;  // overflow: no instances
     }
-    im.tile_count[(int64_t)b * d.T + t] = acc;
 }
 
 void launch_chunk_count(const Dims& d, const GeomArena& g, const ImageArena& im, hipStream_t s) {
@@ -504,8 +533,7 @@ void launch_chunk_count(const Dims& d, const GeomArena& g, const ImageArena& im,
         hipFuncSetAttribute((const void*)k_chunk_count, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     }
     hipLaunchKernelGGL(k_chunk_count, dim3(d.nchunk, d.B), dim3(kScanBlock), lds, s, d, g);
-    hipLaunchKernelGGL(k_column_scan, dim3((d.T + kScanBlock - 1) / kScanBlock, d.B), dim3(kScanBlock), 0, s,
-                       d, g, im);
+    hipLaunchKernelGGL(k_column_scan_wide, dim3((d.T + 63) / 64, d.B), dim3(64 * kColWaves), 0, s, d, g, im);
 }
 
 // ---------------------------------------------------------------- 4. tile ranges

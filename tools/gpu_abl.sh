@@ -10,5 +10,5 @@ GSR_LIB=$PWD/guava_renderer_amd/lib/ab/libgsr_b.so timeout -k 10 300 python -u -
 for v in a b a b a b; do for acc in "" ${ABL_EXACT:-}; do
   GSR_LIB=$PWD/guava_renderer_amd/lib/ab/libgsr_$v.so timeout -k 10 300 python bench.py --steps 20 --warmup 5 --no-cpu-baseline --stages ${ABL_BENCH:-} $acc > $O/b.json 2>$O/b.err; rc=$?
   [ $rc -eq 0 ] || { echo "bench rc=$rc"; tail $O/b.err; exit $rc; }
-  python -c "import json,sys; d=json.loads(open('$O/b.json').read().strip().splitlines()[-1]); s=d['stage_ms_per_step']; print('$v $acc', d['value'], s['render_fwd'], s.get('render_bwd'), s['preprocess'], s['ordered_scatter'], s['depth_sort'])"
+  python -c "import json,sys; d=json.loads(open('$O/b.json').read().strip().splitlines()[-1]); s=d['stage_ms_per_step']; print('$v $acc', d['value'], s['render_fwd'], s.get('render_bwd'), s['preprocess'], s['ordered_scatter'], s['depth_sort'], s['chunk_count'])"
 done; done
