@@ -108,6 +108,11 @@ __device__ __forceinline__ void lbs_stream(const float* __restrict__ base, int M
 // loads in flight instead of one serial chain, and the slice sums are added in slice order through
 // LDS (deterministic).  The frame coefficients sit in LDS (broadcast reads); the k-major bases are
 // read coalesced, once per frame group.
+inline dim3 lbs_blend_grid(int M, int B) {
+    const int nx8 = ((M + 63) / 64 + 7) / 8 * 8;
+    return dim3(nx8 * ((B + kLbsFrames - 1) / kLbsFrames));
+}
+
 __global__ __launch_bounds__(64 * kLbsSplit) void k_lbs_blend(int B, int M, int NB, int NP,
                                                               const float* __restrict__ vt, int64_t vt_stride,
                                                               const float* __restrict__ betas,
@@ -118,7 +123,14 @@ __global__ __launch_bounds__(64 * kLbsSplit) void k_lbs_blend(int B, int M, int 
                                                               float* __restrict__ v_posed) {
     extern __shared__ float4 lds4[];  // coef [(NB + NP)][kLbsFrames], then the slice reduction
     float* coef = reinterpret_cast<float*>(lds4);
-    const int b0 = blockIdx.y * kLbsFrames;
+    // XCD-aware order (1-D grid, lbs_blend_grid): the frame groups of one coordinate block are
+    // dealt to the same XCD back to back, so all but the first read the basis slice from its L2
+    const int ng = (B + kLbsFrames - 1) / kLbsFrames;
+    const int jx = (int)(blockIdx.x >> 3);
+    const int by = jx % ng;
+    const int bx = (jx / ng) * 8 + (int)(blockIdx.x & 7);
+    if (bx * 64 >= M) return;  // padding block (the whole workgroup, before any barrier)
+    const int b0 = by * kLbsFrames;
     const int nk = NB + NP;
     for (int idx = threadIdx.x; idx < nk * kLbsFrames; idx += blockDim.x) {
         const int k = idx / kLbsFrames, f = idx - k * kLbsFrames;
@@ -129,7 +141,7 @@ __global__ __launch_bounds__(64 * kLbsSplit) void k_lbs_blend(int B, int M, int 
     }
     __syncthreads();
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    const int m = blockIdx.x * 64 + lane;
+    const int m = bx * 64 + lane;
     const bool ok = m < M;
     const int nf = min(kLbsFrames, B - b0);
     float as[kLbsFrames], ap[kLbsFrames];
@@ -550,7 +562,7 @@ int gsr_lbs(int B, int V, int J, int NB, const float* v_template, int64_t v_temp
     const size_t lds = lbs_blend_lds(NB, NP);
     if (lds > 160 * 1024) return api_fail(GSR_ERR_ARG, "gsr_lbs: NB + 9(J-1) too large for LDS");
     lbs_blend_attr(lds);
-    hipLaunchKernelGGL(k_lbs_blend, dim3((M + 63) / 64, (B + kLbsFrames - 1) / kLbsFrames), dim3(64 * kLbsSplit),
+    hipLaunchKernelGGL(k_lbs_blend, lbs_blend_grid(M, B), dim3(64 * kLbsSplit),
                        lds, s, B, M, NB, NP, v_template, v_template_stride, betas, shapedirs_t,
                        a.feat, posedirs, vs, a.vp);
     if (int rc = hip_check("lbs_blend")) return rc;
@@ -580,7 +592,7 @@ int gsr_blend_joints(int B, int V, int J, int NB, const float* v_template, int64
     lbs_blend_attr(lds);
     hipStream_t s = (hipStream_t)stream;
     const int M = V * 3;
-    hipLaunchKernelGGL(k_lbs_blend, dim3((M + 63) / 64, (B + kLbsFrames - 1) / kLbsFrames), dim3(64 * kLbsSplit),
+    hipLaunchKernelGGL(k_lbs_blend, lbs_blend_grid(M, B), dim3(64 * kLbsSplit),
                        lds, s, B, M, NB, 0, v_template, v_template_stride, betas, shapedirs_t,
                        nullptr, nullptr, v_shaped, nullptr);
     if (int rc = hip_check("blend_shapes")) return rc;
