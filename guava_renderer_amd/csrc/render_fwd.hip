@@ -91,10 +91,13 @@ __device__ __forceinline__ void split_hh_ll(float w, unsigned& hh, unsigned& ll)
 
 // The split of a batch-shared feature table, once per launch (P x 32 words; render_fwd then loads
 // the packed word in place of the f32 feature).
-__global__ __launch_bounds__(256) void k_split_features(int n, const float* __restrict__ f,
-                                                        uint32_t* __restrict__ out) {
-    const int i = blockIdx.x * 256 + threadIdx.x;
-    if (i < n) out[i] = split_hl(f[i]);
+__global__ __launch_bounds__(256) void k_split_features(int n4, const float4* __restrict__ f,
+                                                        uint4* __restrict__ out) {
+    const int i = blockIdx.x * 256 + threadIdx.x;  // 4 features per thread (rows are 32 floats)
+    if (i < n4) {
+        const float4 v = f[i];
+        out[i] = make_uint4(split_hl(v.x), split_hl(v.y), split_hl(v.z), split_hl(v.w));
+    }
 }
 
 // one 16-byte half of a render record at a wave-uniform byte offset (SGPR soffset)
@@ -512,8 +515,9 @@ void launch_render_fwd(const Dims& d, const Inputs& in, const GeomArena& g, cons
     else if (ablate == 2) hipLaunchKernelGGL((k_render_fwd_ablate<2>), gr, bl, 0, s, d, in, g, im, b, o);
     else if (ablate == 4) hipLaunchKernelGGL((k_render_fwd_ablate<4>), gr, bl, 0, s, d, in, g, im, b, o);
     else if (split && in.s_colors == 0) {  // one feature set for the batch: split it once
-        hipLaunchKernelGGL(k_split_features, dim3((d.P * GSR_C + 255) / 256), dim3(256), 0, s,
-                           d.P * GSR_C, in.colors, g.fsplit);
+        hipLaunchKernelGGL(k_split_features, dim3((d.P * GSR_C / 4 + 255) / 256), dim3(256), 0, s,
+                           d.P * GSR_C / 4, reinterpret_cast<const float4*>(in.colors),
+                           reinterpret_cast<uint4*>(g.fsplit));
         if (exact) hipLaunchKernelGGL((k_render_fwd<true, false, false, 2>), gr, bl, 0, s, d, in, g, im, b, o);
         else hipLaunchKernelGGL((k_render_fwd<false, false, false, 2>), gr, bl, 0, s, d, in, g, im, b, o);
     }
