@@ -118,7 +118,8 @@ inline Dims make_dims(int B, int P, int W, int H) {
     d.T = d.gx * d.gy;
     d.nblk = (P + kScanBlock - 1) / kScanBlock;
     int nb = 64;
-    while (nb < P / 8 && nb < (1 << 20)) nb <<= 1;
+    // <= 16384 buckets: the frame's bucket table fits the LDS of k_bucket_count_lds (64 KB)
+    while (nb < P / 8 && nb < (1 << 14)) nb <<= 1;
     d.NB = nb;
     // count-table rows: kSlots Gaussians (one scatter pass) up to 1024 tiles; beyond, the dense
     // (row x tile) table and each row's base[] load outweigh the extra passes (1024-Gaussian rows)
