@@ -118,8 +118,11 @@ inline Dims make_dims(int B, int P, int W, int H) {
     d.T = d.gx * d.gy;
     d.nblk = (P + kScanBlock - 1) / kScanBlock;
     int nb = 64;
-    // <= 16384 buckets: the frame's bucket table fits the LDS of k_bucket_count_lds (64 KB)
-    while (nb < P / 8 && nb < (1 << 14)) nb <<= 1;
+    // up to 512k Gaussians: <= 16384 buckets, so the frame's bucket table fits the LDS of
+    // k_bucket_count_lds (64 KB; <= 32 keys per bucket on average); beyond, ~8 keys per bucket
+    // (global-atomic counting) so that the buckets stay small enough for in-place ranking
+    const int nb_cap = P <= (1 << 19) ? (1 << 14) : (1 << 20);
+    while (nb < P / 8 && nb < nb_cap) nb <<= 1;
     d.NB = nb;
     // count-table rows: kSlots Gaussians (one scatter pass) up to 1024 tiles; beyond, the dense
     // (row x tile) table and each row's base[] load outweigh the extra passes (1024-Gaussian rows)
