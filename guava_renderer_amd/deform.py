@@ -241,6 +241,14 @@ class EHMDeformer:
             self._ws[key] = torch.empty((n,), dtype=torch.uint8, device=self.dev)
         return self._ws[key]
 
+    def _zeros(self, B, n):
+        """A cached [B, n] zero block (the padding of the coefficient rows)."""
+        zs = self.__dict__.setdefault("_zero_blocks", {})
+        z = zs.get((B, n))
+        if z is None:
+            z = zs[(B, n)] = torch.zeros((B, n), dtype=torch.float32, device=self.dev)
+        return z
+
     def forward(self, body_param_dict, flame_param_dict):
         L = _lib.load()
         st = _stream(self.dev)
@@ -252,11 +260,11 @@ class EHMDeformer:
         o = dict(dtype=torch.float32, device=self.dev)
         # FLAME head (EHM.py:41-75): betas = shape ++ expression; pose = 0 global, 0 neck, jaw, eyes
         Vh, Jh, NBh = fa["J_regressor"].shape[1], fa["J_regressor"].shape[0], fa["shapedirs"].shape[2]
-        betas_h = torch.cat([_f32(fp["shape_params"]), _f32(fp["expression_params"])], 1)
-        if betas_h.shape[1] < NBh:
-            betas_h = torch.cat([betas_h, torch.zeros(B, NBh - betas_h.shape[1], **o)], 1)
-        z3 = torch.zeros(B, 3, **o)
-        pose_h = torch.cat([z3, z3, _f32(fp["jaw_params"]).reshape(B, 3),
+        # each coefficient row is ONE cat (cached zero blocks, no fill launches per frame batch)
+        shp_h, exp_h = _f32(fp["shape_params"]), _f32(fp["expression_params"])
+        pad_h = NBh - shp_h.shape[1] - exp_h.shape[1]
+        betas_h = torch.cat([shp_h, exp_h] + ([self._zeros(B, pad_h)] if pad_h > 0 else []), 1)
+        pose_h = torch.cat([self._zeros(B, 6), _f32(fp["jaw_params"]).reshape(B, 3),
                             _f32(fp["eye_pose_params"]).reshape(B, 6)], 1).contiguous()
         hv = torch.empty((B, Vh, 3), **o)
         hj = torch.empty((B, Jh, 3), **o)
@@ -270,9 +278,8 @@ class EHMDeformer:
         Vb, Jb, NBb = ba["J_regressor"].shape[1], ba["J_regressor"].shape[0], ba["shapedirs"].shape[2]
         n_shape = NBb - bp["exp"].shape[1]  # EHM.py:101-106: pad or cut shape to n_shape, then ++ exp
         shp = _f32(bp["shape"])[:, :n_shape]
-        if shp.shape[1] < n_shape:
-            shp = torch.cat([shp, torch.zeros(B, n_shape - shp.shape[1], **o)], 1)
-        sc = torch.cat([shp, _f32(bp["exp"])], 1).contiguous()
+        pad_b = n_shape - shp.shape[1]
+        sc = torch.cat([shp] + ([self._zeros(B, pad_b)] if pad_b > 0 else []) + [_f32(bp["exp"])], 1).contiguous()
         joff = _f32(bp["joints_offset"]) if bp.get("joints_offset") is not None else None
         vt = torch.empty((B, Vb, 3), **o)
         tj = torch.empty((B, Jb, 3), **o)
@@ -288,10 +295,10 @@ class EHMDeformer:
                                      self.HEAD_REF[0], self.HEAD_REF[1], _ptr(tj), Jb, self.BODY_REF[0],
                                      self.BODY_REF[1], _ptr(vt), _ptr(self.bad), st), "gsr_splice_head")
         # body pose (EHM.py:94-112): global, body, jaw = 0, eyes = 0, hands
-        gp = _f32(bp["global_pose"]).reshape(B, 1, 3) if bp.get("global_pose") is not None else torch.zeros(B, 1, 3, **o)
-        bpose = _f32(bp["body_pose"]).reshape(B, 21, 3) if bp.get("body_pose") is not None else torch.zeros(B, 21, 3, **o)
-        pose = torch.cat([gp, bpose, torch.zeros(B, 3, 3, **o), _f32(bp["left_hand_pose"]).reshape(B, 15, 3),
-                          _f32(bp["right_hand_pose"]).reshape(B, 15, 3)], 1).contiguous()
+        gp = _f32(bp["global_pose"]).reshape(B, 3) if bp.get("global_pose") is not None else self._zeros(B, 3)
+        bpose = _f32(bp["body_pose"]).reshape(B, 63) if bp.get("body_pose") is not None else self._zeros(B, 63)
+        pose = torch.cat([gp, bpose, self._zeros(B, 9), _f32(bp["left_hand_pose"]).reshape(B, 45),
+                          _f32(bp["right_hand_pose"]).reshape(B, 45)], 1).reshape(B, 55, 3).contiguous()
         verts = torch.empty((B, Vb, 3), **o)
         jt2 = torch.empty((B, Jb, 3), **o)
         J = torch.empty((B, Jb, 3), **o)
