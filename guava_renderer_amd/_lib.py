@@ -14,7 +14,7 @@ EXPORTS = ("gsr_version", "gsr_last_error", "gsr_set_exact_exp", "gsr_set_split_
            "gsr_backward", "gsr_batch_workspace_bytes", "gsr_forward_batch",
            "gsr_backward_batch", "gsr_batch_status", "gsr_profile_enable", "gsr_profile_read",
            "gsr_render_counters", "gsr_render_timeline", "gsr_forward_batch_refine",
-           "gsr_refine_prepare",
+           "gsr_refine_prepare", "gsr_batch_status_offset",
            # include/gsr_deform.h
            "gsr_lbs_workspace_bytes", "gsr_lbs", "gsr_blend_joints", "gsr_splice_head",
            "gsr_deform_gaussians",
@@ -40,6 +40,11 @@ class RefineEpilogue(ctypes.Structure):
 
 class GsrError(RuntimeError):
     pass
+
+
+class CapacityError(GsrError):
+    """A batched forward needed more Gaussian-tile instances than its workspace holds (that call's
+    images were filled with NaN)."""
 
 
 def load(path=None):
@@ -83,6 +88,8 @@ def load(path=None):
     L.gsr_backward.restype = _i
     L.gsr_batch_workspace_bytes.argtypes = [_i, _i, _i, _i, _i64]
     L.gsr_batch_workspace_bytes.restype = _sz
+    L.gsr_batch_status_offset.argtypes = [_i, _i, _i, _i, _i64]
+    L.gsr_batch_status_offset.restype = _sz
     L.gsr_forward_batch.argtypes = [_i, _i, _i, _i, _vp, _i64, _vp, _i64, _vp, _i64, _vp, _i64, _vp,
                                     _i64, _f, _vp, _vp, _vp, _vp, _i64, _vp, _i64, _vp, _vp, _vp, _i,
                                     _vp]

@@ -6,6 +6,7 @@ no host synchronisation, so a whole batch can also be captured in a HIP graph.  
 attributes may be shared (stride 0: a [P,k] tensor) or per frame (a [B,P,k] tensor).
 """
 import ctypes
+import weakref
 
 import torch
 
@@ -16,26 +17,72 @@ STAGES = ("preprocess", "scan", "depth_sort", "chunk_count", "tile_scan", "order
           "render_bwd", "preprocess_bwd")
 
 
-def _stride(t, B, per):
-    """Element stride between frames for a [P,per] (shared) or [B,P,per] tensor."""
-    if t.dim() == 3:
-        assert t.shape[0] == B and t.shape[2] == per, t.shape
-        return t.shape[1] * per
-    assert t.dim() == 2 and t.shape[1] == per, t.shape
-    return 0
+def _frame_arg(t, B, P, per, name, device, align16=False):
+    """(tensor, element stride between frames) of a shared [P,per] or per-frame [B,P,per] float32
+    input on `device`.  The frame stride is the tensor's own stride(0) -- 0 for an expanded tensor,
+    whose frames all read one [P,per] table (deform.py's features_color / opacity); rows that are
+    not dense in memory are made contiguous first.  align16: every frame's rows start 16-byte
+    aligned (the render kernels' feature loads)."""
+    if not isinstance(t, torch.Tensor):
+        raise TypeError(f"{name} must be a tensor")
+    if t.device != device:
+        raise ValueError(f"{name} must be on {device} (got {t.device})")
+    if t.dtype != torch.float32:
+        raise TypeError(f"{name} must be float32 (got {t.dtype})")
+    if t.dim() == 2:
+        if tuple(t.shape) != (P, per):
+            raise ValueError(f"{name}: expected [{P},{per}] or [{B},{P},{per}], got {list(t.shape)}")
+        t = t.contiguous()
+        return t, 0
+    if t.dim() != 3 or tuple(t.shape) != (B, P, per):
+        raise ValueError(f"{name}: expected [{P},{per}] or [{B},{P},{per}], got {list(t.shape)}")
+    if t.stride(0) == 0:  # one table for every frame (expand)
+        row = t[0]
+        if not row.is_contiguous():
+            row = row.contiguous()
+        return row, 0
+    dense_rows = t.stride(2) == 1 and (t.stride(1) == per or P == 1)
+    fs = t.stride(0)
+    if not dense_rows or fs < P * per or (align16 and (fs % 4 or t.data_ptr() % 16)):
+        t = t.contiguous()
+        fs = P * per
+    return t, fs
+
+
+def _frame_mat(t, B, n, name, device):
+    """[B,n] float32 per-frame matrix (viewmatrices / projmatrices [B,16], tanfov [B,2])."""
+    if t.device != device or t.dtype != torch.float32:
+        raise ValueError(f"{name} must be float32 on {device}")
+    if t.numel() != B * n:
+        raise ValueError(f"{name}: expected {B}x{n} floats, got shape {list(t.shape)}")
+    return t.contiguous()
 
 
 class BatchRasterizer:
     """Holds the workspace for B frames of P Gaussians at W x H with room for R_capacity
-    Gaussian-tile instances."""
+    Gaussian-tile instances.
+
+    Capacity: a forward whose batch needs more than R_capacity instances renders nothing (its
+    images are NaN) and sets the workspace's sticky overflow word.  No host synchronisation is
+    needed to notice it: after every forward the sticky words are copied asynchronously to pinned
+    memory, and the next forward/backward (or poll()) raises CapacityError once that copy has
+    landed; poll(wait=True) or status() check at once."""
 
     def __init__(self, B, P, W, H, R_capacity=None, device="cuda"):
         self.B, self.P, self.W, self.H = int(B), int(P), int(W), int(H)
         self.device = torch.device(device)
+        if self.device.type == "cuda" and self.device.index is None:
+            self.device = torch.device("cuda", torch.cuda.current_device())
         self.R_capacity = int(R_capacity if R_capacity is not None else 16 * P * B)
         self.L = _lib.load()
         nbytes = self.L.gsr_batch_workspace_bytes(self.B, self.P, self.W, self.H, self.R_capacity)
+        soff = self.L.gsr_batch_status_offset(self.B, self.P, self.W, self.H, self.R_capacity)
         self.workspace = torch.empty((nbytes,), dtype=torch.uint8, device=self.device)
+        self._sticky = self.workspace[soff:soff + 16].view(torch.int32)  # include/gsr.h sticky words
+        self._sticky.zero_()
+        self._overflow = self.workspace[4:8].view(torch.int32).reshape(())  # this call's flag (kCtrlOverflow)
+        self._status_host = torch.zeros(4, dtype=torch.int32, pin_memory=True)
+        self._status_ev = None
         self.out_color = torch.empty((self.B, C, self.H, self.W), dtype=torch.float32, device=self.device)
         self.out_invdepth = torch.empty((self.B, self.H, self.W), dtype=torch.float32, device=self.device)
         self.radii = torch.empty((self.B, self.P), dtype=torch.int32, device=self.device)
@@ -43,40 +90,101 @@ class BatchRasterizer:
     def _stream(self):
         return ctypes.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)
 
+    def _inputs(self, means3D, colors, opacities, scales, rotations, viewmatrices, projmatrices,
+                tanfov, backgrounds):
+        B, P, dev = self.B, self.P, self.device
+        m, sm = _frame_arg(means3D, B, P, 3, "means3D", dev)
+        c, sc = _frame_arg(colors, B, P, C, "colors", dev, align16=True)
+        o, so = _frame_arg(opacities, B, P, 1, "opacities", dev)
+        s, ss = _frame_arg(scales, B, P, 3, "scales", dev)
+        r, sr = _frame_arg(rotations, B, P, 4, "rotations", dev)
+        v = _frame_mat(viewmatrices, B, 16, "viewmatrices", dev)
+        pm = _frame_mat(projmatrices, B, 16, "projmatrices", dev)
+        tf = _frame_mat(tanfov, B, 2, "tanfov", dev)
+        if backgrounds.device != dev or backgrounds.dtype != torch.float32:
+            raise ValueError(f"backgrounds must be float32 on {dev}")
+        if backgrounds.dim() == 2:
+            if tuple(backgrounds.shape) != (B, C):
+                raise ValueError(f"backgrounds: expected [{C}] or [{B},{C}], got {list(backgrounds.shape)}")
+            bg = backgrounds.contiguous() if backgrounds.stride(0) != 0 else backgrounds[0].contiguous()
+            bs = C if backgrounds.stride(0) != 0 else 0
+        elif tuple(backgrounds.shape) == (C,):
+            bg, bs = backgrounds.contiguous(), 0
+        else:
+            raise ValueError(f"backgrounds: expected [{C}] or [{B},{C}], got {list(backgrounds.shape)}")
+        keep = (m, c, o, s, r, v, pm, tf, bg)  # alive until the launches are enqueued
+        args = (B, P, self.W, self.H, m.data_ptr(), sm, c.data_ptr(), sc, o.data_ptr(), so,
+                s.data_ptr(), ss, r.data_ptr(), sr)
+        return keep, args, (v.data_ptr(), pm.data_ptr(), tf.data_ptr(), bg.data_ptr(), bs)
+
+    def _after_forward(self):
+        """Queue the asynchronous copy of the sticky status words (no host synchronisation)."""
+        self._status_host.copy_(self._sticky, non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record(torch.cuda.current_stream(self.device))
+        self._status_ev = ev
+
+    def poll(self, wait=False):
+        """Raise CapacityError if a forward enqueued so far overflowed the capacity.  Without
+        `wait` this only reads the status copy of the forwards that have already completed."""
+        ev = self._status_ev
+        if ev is None:
+            return
+        if wait:
+            ev.synchronize()
+        elif not ev.query():
+            return
+        if int(self._status_host[0]):
+            rmax = int(self._status_host[1]) & 0xFFFFFFFF
+            self._sticky.zero_()
+            self._status_host.zero_()
+            raise _lib.CapacityError(
+                f"batch needed {rmax} Gaussian-tile instances, workspace holds {self.R_capacity} "
+                f"(that forward's images are NaN); allocate a BatchRasterizer with a larger R_capacity")
+
+    def max_instances_seen(self):
+        """Largest batch instance count of the forwards whose status copy has landed."""
+        return int(self._status_host[1]) & 0xFFFFFFFF
+
+    def overflow_flag(self):
+        """0-dim int32 device tensor: 1 if the last forward overflowed (read on the device, e.g. as an
+        optimizer's found_inf), no host synchronisation."""
+        return self._overflow
+
     def forward(self, means3D, colors, opacities, scales, rotations, viewmatrices, projmatrices,
                 tanfov, backgrounds, scale_modifier=1.0, antialiasing=False, refine=None):
         """Render B frames.  refine: optional RefineHead -- the refiner's first 1x1 conv + leaky ReLU
         fused into the render epilogue (include/gsr.h gsr_refine_epilogue); its output is
         refine.out [B,n_out,H,W] and only out_color[:, :refine.keep_channels] is written."""
-        B = self.B
-        bg_stride = backgrounds.shape[-1] if backgrounds.dim() == 2 else 0
-        args = (B, self.P, self.W, self.H,
-                means3D.data_ptr(), _stride(means3D, B, 3), colors.data_ptr(), _stride(colors, B, C),
-                opacities.data_ptr(), _stride(opacities, B, 1), scales.data_ptr(), _stride(scales, B, 3),
-                rotations.data_ptr(), _stride(rotations, B, 4), float(scale_modifier),
-                viewmatrices.data_ptr(), projmatrices.data_ptr(), tanfov.data_ptr(),
-                backgrounds.data_ptr(), bg_stride, self.workspace.data_ptr(), self.R_capacity,
-                self.out_color.data_ptr(), self.out_invdepth.data_ptr(), self.radii.data_ptr(),
-                int(bool(antialiasing)))
+        self.poll()
+        keep, head, (v, pm, tf, bg, bs) = self._inputs(means3D, colors, opacities, scales, rotations,
+                                                       viewmatrices, projmatrices, tanfov, backgrounds)
+        args = head + (float(scale_modifier), v, pm, tf, bg, bs, self.workspace.data_ptr(), self.R_capacity,
+                       self.out_color.data_ptr(), self.out_invdepth.data_ptr(), self.radii.data_ptr(),
+                       int(bool(antialiasing)))
         if refine is None:
             _lib.check(self.L.gsr_forward_batch(*args, self._stream()), "gsr_forward_batch")
         else:
             # composite the pre-contracted rows (include/gsr.h gsr_refine_prepare): features and
             # backgrounds both go through the head's 32 -> keep + n_out map
-            pc = refine.prepare(colors, self._stream())
-            pb = refine.prepare(backgrounds.reshape(-1, C), self._stream(), cache=False)
+            pc = refine.prepare(keep[1], self._stream())
+            bgrows = keep[8].reshape(-1, C)
+            pb = refine.prepare(bgrows, self._stream(), cache=False)
             args = list(args)
             args[6] = pc.data_ptr()
             args[18] = pb.data_ptr()
-            ep = refine.epilogue(B, self.H, self.W)
+            ep = refine.epilogue(self.B, self.H, self.W)
             _lib.check(self.L.gsr_forward_batch_refine(*args, ctypes.byref(ep), self._stream()),
                        "gsr_forward_batch_refine")
+        del keep
+        self._after_forward()
         return self.out_color, self.out_invdepth, self.radii
 
     def backward(self, means3D, colors, opacities, scales, rotations, viewmatrices, projmatrices,
                  tanfov, backgrounds, dL_dcolor, dL_dinvdepth=None, scale_modifier=1.0,
                  antialiasing=False):
-        """Gradients of the last forward, per frame: dict of [B,P,k] tensors."""
+        """Gradients of the last forward, per frame: dict of [B,P,k] tensors (all zero when that
+        forward overflowed the capacity; the overflow is reported by the next forward / poll)."""
         B, P = self.B, self.P
         o = dict(dtype=torch.float32, device=self.device)
         g = dict(mean2D=torch.zeros((B, P, 3), **o), conic=torch.zeros((B, P, 4), **o),
@@ -84,21 +192,25 @@ class BatchRasterizer:
                  invdepth=torch.zeros((B, P, 1), **o) if dL_dinvdepth is not None else None,
                  means3D=torch.zeros((B, P, 3), **o), cov3D=torch.zeros((B, P, 6), **o),
                  scales=torch.zeros((B, P, 3), **o), rotations=torch.zeros((B, P, 4), **o))
-        bg_stride = backgrounds.shape[-1] if backgrounds.dim() == 2 else 0
+        keep, head, (v, pm, tf, bg, bs) = self._inputs(means3D, colors, opacities, scales, rotations,
+                                                       viewmatrices, projmatrices, tanfov, backgrounds)
+        if tuple(dL_dcolor.shape) != (B, C, self.H, self.W):
+            raise ValueError(f"dL_dcolor: expected [{B},{C},{self.H},{self.W}], got {list(dL_dcolor.shape)}")
+        dLc = dL_dcolor.to(torch.float32).contiguous()
+        dLi = None
+        if dL_dinvdepth is not None:
+            if dL_dinvdepth.numel() != B * self.H * self.W:
+                raise ValueError("dL_dinvdepth: expected [B,H,W]")
+            dLi = dL_dinvdepth.to(torch.float32).contiguous()
         rc = self.L.gsr_backward_batch(
-            B, P, self.W, self.H,
-            means3D.data_ptr(), _stride(means3D, B, 3), colors.data_ptr(), _stride(colors, B, C),
-            opacities.data_ptr(), _stride(opacities, B, 1), scales.data_ptr(), _stride(scales, B, 3),
-            rotations.data_ptr(), _stride(rotations, B, 4), float(scale_modifier),
-            viewmatrices.data_ptr(), projmatrices.data_ptr(), tanfov.data_ptr(),
-            backgrounds.data_ptr(), bg_stride, self.workspace.data_ptr(), self.R_capacity,
-            dL_dcolor.contiguous().data_ptr(),
-            dL_dinvdepth.contiguous().data_ptr() if dL_dinvdepth is not None else None,
+            *head, float(scale_modifier), v, pm, tf, bg, bs, self.workspace.data_ptr(), self.R_capacity,
+            dLc.data_ptr(), dLi.data_ptr() if dLi is not None else None,
             g["mean2D"].data_ptr(), g["conic"].data_ptr(), g["opacity"].data_ptr(),
             g["colors"].data_ptr(), g["invdepth"].data_ptr() if g["invdepth"] is not None else None,
             g["means3D"].data_ptr(), g["cov3D"].data_ptr(), g["scales"].data_ptr(),
             g["rotations"].data_ptr(), int(bool(antialiasing)), self._stream())
         _lib.check(rc, "gsr_backward_batch")
+        del keep
         return g
 
     def status(self):
@@ -125,6 +237,7 @@ class RefineHead:
         self.keep_channels = int(keep_channels)
         assert self.keep_channels + self.n_out <= C
         self.out = None
+        self._outs = {}
         self._prep_key, self._prep = None, None
 
     @classmethod
@@ -132,27 +245,44 @@ class RefineHead:
         return cls(conv.weight, conv.bias, negative_slope, keep_channels)
 
     def prepare(self, rows, stream, cache=True):
-        """[..., 32] feature rows -> the pre-contracted rows the refine epilogue composites; cached
-        on the tensor's identity and version (an avatar's features are static across frames)."""
-        key = (rows.data_ptr(), tuple(rows.shape), rows._version)
-        if cache and self._prep_key == key:
-            return self._prep
+        """[..., 32] feature rows -> the pre-contracted rows the refine epilogue composites.  Cached
+        for the same tensor OBJECT at the same version (an avatar's features are static across
+        frames): a different tensor -- even one the allocator placed at the same address -- or an
+        in-place torch update is recomputed.  Writes that bypass torch's version counter (a HIP
+        kernel writing through data_ptr()) need invalidate()."""
+        # identity: the tensor that owns the memory (a view's base) -- alive while the weakref is,
+        # so its address cannot be reused -- plus the view's address, shape and the version counter
+        owner = rows._base if rows._base is not None else rows
+        ident = (rows.data_ptr(), tuple(rows.shape), rows._version)
+        if cache and self._prep_key is not None:
+            ref, key = self._prep_key
+            if ref() is owner and key == ident:
+                return self._prep
         out = torch.empty_like(rows)
         n = rows.numel() // C
         _lib.check(_lib.load().gsr_refine_prepare(n, rows.data_ptr(), self.weight.data_ptr(), self.n_out,
                                                   self.keep_channels, out.data_ptr(), stream),
                    "gsr_refine_prepare")
         if cache:
-            self._prep_key, self._prep = key, out
+            self._prep_key, self._prep = (weakref.ref(owner), ident), out
         return out
 
+    def invalidate(self):
+        """Drop the cached pre-contracted features (after writing them outside torch's tracking)."""
+        self._prep_key, self._prep = None, None
+
     def epilogue(self, B, H, W):
+        """The C-ABI epilogue block; the output tensor is per (stream, shape), so batches in flight
+        on different streams do not share one buffer.  self.out is the one of the last call."""
         shape = (B, self.n_out, H, W)
-        if self.out is None or tuple(self.out.shape) != shape:
-            self.out = torch.empty(shape, dtype=torch.float32, device=self.weight.device)
+        key = (torch.cuda.current_stream(self.weight.device).cuda_stream, shape)
+        out = self._outs.get(key)
+        if out is None:
+            out = self._outs[key] = torch.empty(shape, dtype=torch.float32, device=self.weight.device)
+        self.out = out
         return _lib.RefineEpilogue(self.weight.data_ptr(),
                                    self.bias.data_ptr() if self.bias is not None else None,
-                                   self.n_out, self.slope, self.out.data_ptr(), self.keep_channels)
+                                   self.n_out, self.slope, out.data_ptr(), self.keep_channels)
 
 
 def profile_enable(stages=("render_fwd",)):

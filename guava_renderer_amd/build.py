@@ -25,7 +25,7 @@ FLAGS = ["-O3", "-std=c++17", "-fPIC", "-ffp-contract=off", f"--offload-arch={AR
 
 # per-source extras: no SLP packing in the render kernel (packed f32 VALU beside MFMAs costs more
 # issue slots than the scalar pair, MI355X_MICROARCH.md "price of one filler")
-EXTRA = {"render_fwd.hip": ["-fno-slp-vectorize"]}
+EXTRA = {"render_fwd.hip": ["-fno-slp-vectorize"], "render_bwd.hip": ["-fno-slp-vectorize"]}
 
 
 def _newer(src_paths, dst):

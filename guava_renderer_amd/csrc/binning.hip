@@ -60,7 +60,8 @@ __device__ __forceinline__ TV block_excl_scan(TV v, TV* total, TV* sh /* NT/64 +
 // batch total against the capacity.
 __global__ __launch_bounds__(1024) void k_frame_totals(const uint32_t* __restrict__ bs,
                                                        const uint32_t* __restrict__ bkey, int B, int nblk,
-                                                       uint32_t* ctrl, uint32_t* fstat, int64_t R_cap) {
+                                                       uint32_t* ctrl, uint32_t* fstat, int64_t R_cap,
+                                                       uint32_t* sticky) {
     extern __shared__ uint32_t rf[];  // [B] instances per frame
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     for (int f = wv; f < B; f += 1024 / 64) {
@@ -93,13 +94,18 @@ __global__ __launch_bounds__(1024) void k_frame_totals(const uint32_t* __restric
             base += rf[f];
         }
         ctrl[kCtrlRLo] = (uint32_t)min(base, (uint64_t)0xFFFFFFFFu);
-        ctrl[kCtrlOverflow] = (base > (uint64_t)R_cap || base >= 0xFFFFFFF0ull) ? 1u : 0u;
+        const uint32_t ovf = (base > (uint64_t)R_cap || base >= 0xFFFFFFF0ull) ? 1u : 0u;
+        ctrl[kCtrlOverflow] = ovf;
+        if (sticky) {
+            if (ovf) sticky[kStickyOverflow] = 1u;
+            sticky[kStickyRMax] = max(sticky[kStickyRMax], (uint32_t)min(base, (uint64_t)0xFFFFFFFFu));
+        }
     }
 }
 
 void launch_scan_blocksums(const Dims& d, const GeomArena& g, int64_t R_cap, hipStream_t s) {
     hipLaunchKernelGGL(k_frame_totals, dim3(1), dim3(1024), (size_t)d.B * 4, s, g.blocksums, g.blockkey, d.B,
-                       d.nblk, g.ctrl, g.fstat, R_cap);
+                       d.nblk, g.ctrl, g.fstat, R_cap, g.sticky);
 }
 
 // ---------------------------------------------------------------- segment sort (LDS)

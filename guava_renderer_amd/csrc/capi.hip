@@ -237,7 +237,7 @@ int gsr_forward(gsr_alloc_fn geometryBuffer, gsr_alloc_fn binningBuffer, gsr_all
     (void)D; (void)M; (void)shs; (void)cam_pos;
     hipStream_t s = (hipStream_t)stream;
     if (P < 0 || width <= 0 || height <= 0) return fail(GSR_ERR_ARG, "bad P/width/height");
-    if (P >= kMaxGaussians) return fail(GSR_ERR_ARG, "P must be < 2^28");
+    if (P >= kMaxGaussians) return fail(GSR_ERR_ARG, "P must be < 2^24");
     if ((int64_t)((width + 15) / 16) * ((height + 15) / 16) > kMaxTiles) return fail(GSR_ERR_ARG, "image too large");
     const Dims d = make_dims(1, P, width, height);
     GeomArena g;
@@ -280,7 +280,8 @@ int gsr_forward(gsr_alloc_fn geometryBuffer, gsr_alloc_fn binningBuffer, gsr_all
     HIP_TRY(hipStreamSynchronize(s));
     if (ctrl_h[kCtrlError] & 1u)
         return fail(GSR_ERR_PREFILTERED, "Point is filtered although prefiltered is set. This shouldn't happen!");
-    if (ctrl_h[kCtrlOverflow]) return fail(GSR_ERR_CAPACITY, "instance count exceeds 2^32");
+    if (ctrl_h[kCtrlOverflow] || ctrl_h[kCtrlRLo] > 0x7FFFFFFFu)
+        return fail(GSR_ERR_CAPACITY, "instance count exceeds 2^31 - 1 (num_rendered is an int)");
     const int64_t R = ctrl_h[kCtrlRLo];
     char* bb = binningBuffer(alloc_ctx, carve_bin(nullptr, R, nullptr));
     if (!bb) return fail(GSR_ERR_ALLOC, "binningBuffer allocation failed");
@@ -345,19 +346,27 @@ int gsr_backward(int P, int D, int M, int R, const float* background, int width,
     return 0;
 }
 
-size_t gsr_batch_workspace_bytes(int B, int P, int width, int height, int64_t R_capacity) {
+// Batch workspace: geometry | image | binning arenas, then 256 bytes of sticky status words
+// (kStickyWords, never reset by a call; the host zeroes them when it creates the workspace).
+size_t gsr_batch_status_offset(int B, int P, int width, int height, int64_t R_capacity) {
     const Dims d = make_dims(B, P, width, height);
     return carve_geom(nullptr, d, nullptr) + carve_image(nullptr, d, nullptr) +
            carve_bin(nullptr, R_capacity, nullptr);
+}
+
+size_t gsr_batch_workspace_bytes(int B, int P, int width, int height, int64_t R_capacity) {
+    return gsr_batch_status_offset(B, P, width, height, R_capacity) + 256;
 }
 
 static void carve_workspace(char* ws, const Dims& d, int64_t R_cap, GeomArena* g, ImageArena* im,
                             BinArena* bn) {
     const size_t gsz = carve_geom(nullptr, d, nullptr);
     const size_t isz = carve_image(nullptr, d, nullptr);
+    const size_t bsz = carve_bin(nullptr, R_cap, nullptr);
     carve_geom(ws, d, g);
     carve_image(ws + gsz, d, im);
     carve_bin(ws + gsz + isz, R_cap, bn);
+    g->sticky = reinterpret_cast<uint32_t*>(ws + gsz + isz + bsz);
 }
 
 int gsr_forward_batch(int B, int P, int width, int height, const float* means3D,
@@ -394,7 +403,7 @@ int gsr_forward_batch_refine(int B, int P, int width, int height, const float* m
         return fail(GSR_ERR_ARG, "bad batch arguments");
     if ((int64_t)((width + 15) / 16) * ((height + 15) / 16) > kMaxTiles) return fail(GSR_ERR_ARG, "image too large");
     if (B > kMaxFrames) return fail(GSR_ERR_ARG, "too many frames per batch");
-    if (P >= kMaxGaussians) return fail(GSR_ERR_ARG, "P must be < 2^28");
+    if (P >= kMaxGaussians) return fail(GSR_ERR_ARG, "P must be < 2^24");
     if (!colors) return fail(GSR_ERR_NO_COLORS, "For non-RGB, provide precomputed Gaussian colors!");
     if (((uintptr_t)colors & 15) != 0 || ((colors_stride * 4) & 15) != 0)
         return fail(GSR_ERR_ARG, "colors must be 16-byte aligned per frame");
@@ -459,6 +468,7 @@ int gsr_backward_batch(int B, int P, int width, int height, const float* means3D
                        int antialiasing, void* stream) {
     hipStream_t s = (hipStream_t)stream;
     if (B <= 0 || P <= 0 || !workspace || !tanfov) return fail(GSR_ERR_ARG, "bad batch arguments");
+    if (P >= kMaxGaussians) return fail(GSR_ERR_ARG, "P must be < 2^24");
     const Dims d = make_dims(B, P, width, height);
     GeomArena g;
     ImageArena im;

@@ -83,7 +83,12 @@ struct GeomArena {
     uint32_t* order;      // per frame, visible Gaussians in (depth, index) order
     uint32_t* table;      // [B][nchunk][T] instance counts per (depth chunk, tile), scanned per tile
     uint32_t* fsplit;     // [P][32] features pre-split for the split-bf16 blend: bf16 (hi | lo << 16)
+    // batch path only (else null): status words that survive the per-call ctrl reset --
+    // [kStickyOverflow] set by any overflowing forward, [kStickyRMax] largest batch R seen; cleared
+    // by the host (gsr_batch_status_offset)
+    uint32_t* sticky = nullptr;
 };
+enum Sticky : int { kStickyOverflow = 0, kStickyRMax = 1, kStickyWords = 4 };
 
 struct ImageArena {
     float* final_T;
@@ -135,8 +140,9 @@ inline Dims make_dims(int B, int P, int W, int H) {
 size_t carve_geom(char* base, const Dims& d, GeomArena* g);
 size_t carve_image(char* base, const Dims& d, ImageArena* im);
 size_t carve_bin(char* base, int64_t R, BinArena* b);
-// Upper bound on P (the binning key keeps the Gaussian index in 32 bits with room to spare).
-constexpr int kMaxGaussians = 1 << 28;
+// Upper bound on P: the render kernels address a frame's feature rows (128 B per Gaussian) through
+// a buffer resource with 32-bit byte offsets, so P * 128 must stay below 2^31.
+constexpr int kMaxGaussians = 1 << 24;
 constexpr uint32_t kIndexMask = (1u << 28) - 1u;  // point_list entry -> Gaussian index
 // Upper bound on tiles per frame (the ordered scatter keeps a per-tile counter array in LDS).
 constexpr int kMaxTiles = 16384;

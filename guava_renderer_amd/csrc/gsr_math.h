@@ -143,6 +143,27 @@ __device__ __forceinline__ void get_rect(float px, float py, int r, int gx, int 
     rmax[1] = min((uint32_t)a, (uint32_t)gy);
 }
 
+// ---- split-bf16 operands (render_fwd colour accumulation, render_bwd contractions) ----
+// x = x_hi + x_lo with x_hi = bf16_rne(x), x_lo = bf16_rne(x - x_hi): |x - x_hi - x_lo| <= 2^-17 |x|,
+// and every product of two such halves is exact in f32.
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+typedef float float2x __attribute__((ext_vector_type(2)));
+// v_cvt_pk_bf16_f32 (round to nearest even) of (x, y), x in the low half
+__device__ __forceinline__ unsigned cvt_pk_bf16(float x, float y) {
+    return __builtin_bit_cast(unsigned, __builtin_convertvector((float2x){x, y}, bf16x2));
+}
+// (hi, lo) packed low|high: hi = bf16(f), lo = bf16(f - hi)
+__device__ __forceinline__ unsigned split_hl(float f) {
+    const float hf = __uint_as_float(cvt_pk_bf16(f, f) << 16);
+    return cvt_pk_bf16(hf, f - hf);
+}
+// (hi, hi) and (lo, lo)
+__device__ __forceinline__ void split_hh_ll(float w, unsigned& hh, unsigned& ll) {
+    hh = cvt_pk_bf16(w, w);
+    const float r = w - __uint_as_float(hh << 16);
+    ll = cvt_pk_bf16(r, r);
+}
+
 // Gaussian exponent of the blend (fused form; A=-cx/2, Bb=-cy, Cq=-cz/2 are exact scalings).
 __device__ __forceinline__ float blend_power(float A, float Bb, float Cq, float dx, float dy) {
     return fmaf(dy, fmaf(Cq, dy, Bb * dx), (A * dx) * dx);

@@ -74,21 +74,33 @@ __device__ __forceinline__ float wave_transpose_reduce8(const float (&v)[8]) {
 // and replays its tile's depth-sorted list back to front from the strip's largest n_contrib,
 // taking only the Gaussians whose strip bit is set in point_list (binning's exact test that the
 // Gaussian reaches alpha >= 1/255 somewhere in the strip; the others cannot be active on any of its
-// pixels).  No workgroup barriers: render records and feature rows arrive by scalar loads (the
-// Gaussian index is wave-uniform); the LDS is wave-private.
+// pixels).  No workgroup barriers: the LDS is wave-private.
+//
+// Survivors are processed in batches of 32 (back to front):
+//  * the list is scanned 64 entries at a time and the strip's survivors are appended to a
+//    wave-private LDS ring (slot = rank of the entry among the chunk's survivors), so batches are
+//    full whatever the survivor density;
+//  * a batch's render records and feature rows are loaded lane-distributed (lane s: survivor s)
+//    while the PREVIOUS batch is replayed, so their latency hides behind a whole batch;
+//  * g = f . dL (the colour term of dL/dalpha) for the batch's 32 Gaussians x 64 pixels is one
+//    f32 MFMA contraction over the 32 channels (16 v_mfma_f32_32x32x2_f32 per pixel half, exact
+//    f32 products), one v_permlane32_swap per register puts each pixel's 32 values in its lane;
+//  * the serial replay then needs per survivor only its record fields (v_readlane from the
+//    lane-distributed batch) and the pixel's g from a register.
 constexpr int kBwdQueueOffset = 32;  // words after each forward XCD counter (own cache line)
+constexpr int kBwdRing = 128;        // survivor ring entries per wave (LDS)
 
 template <bool EXACT, bool INVD>
-__global__ __launch_bounds__(GSR_TILE_PIX) __attribute__((amdgpu_waves_per_eu(3))) void k_render_bwd(Dims d, Inputs in, GeomArena g,
-                                                             ImageArena im, BinArena bn, Grads gr) {
-    __shared__ float lds_all[(GSR_TILE_PIX / 64) * kBwdLdsWave];
+__global__ __launch_bounds__(GSR_TILE_PIX) __attribute__((amdgpu_waves_per_eu(2))) void k_render_bwd(
+    Dims d, Inputs in, GeomArena g, ImageArena im, BinArena bn, Grads gr) {
+    __shared__ float lds_all[(GSR_TILE_PIX / 64) * (kBwdLdsWave + 2 * kBwdRing)];
     if (g.ctrl[kCtrlOverflow]) return;
     const uint32_t ne = g.ctrl[kCtrlNonEmpty];
     const int lane = threadIdx.x & 63;
-    float* wl = lds_all + (threadIdx.x >> 6) * kBwdLdsWave;  // this wave's [32][65] tile
-    float* cl = wl + kBwdBatch * kBwdPitch;                    // and its [32][8] term slots
-    uint32_t vzero;  // a VGPR zero: indexes the uniform record loads so they stay vector loads
-    asm volatile("v_mov_b32 %0, 0" : "=v"(vzero));
+    float* wl = lds_all + (threadIdx.x >> 6) * (kBwdLdsWave + 2 * kBwdRing);  // this wave's [32][65] tile
+    float* cl = wl + kBwdBatch * kBwdPitch;                    // its [32][8] term slots
+    uint32_t* ring_g = reinterpret_cast<uint32_t*>(cl + kBwdBatch * kBwdComps);  // survivor ring
+    uint32_t* ring_p = ring_g + kBwdRing;
     const int hi = lane >> 5, l32 = lane & 31;
     uint32_t q = __builtin_amdgcn_s_getreg((3 << 11) | 20) & 7u;  // HW_REG_XCC_ID
     uint32_t q_left = 8;
@@ -146,8 +158,8 @@ __global__ __launch_bounds__(GSR_TILE_PIX) __attribute__((amdgpu_waves_per_eu(3)
         }
         const float dL_inv = (INVD && inside) ? gr.dL_dinvdepth[pix] : 0.f;
 
-        // MFMA A operands of the colour-gradient contraction: step j covers strip pixels 2j, 2j+1;
-        // lane l holds dL[pixel 2j + (l>>5)][channel l&31].  Transposed through the LDS tile.
+        // colour-gradient MFMA A operands: step j covers strip pixels 2j, 2j+1; lane l holds
+        // dL[pixel 2j + (l>>5)][channel l&31].  Transposed through the LDS tile.
         float adl[kBwdBatch];
         wave_lds_order();
 #pragma unroll
@@ -156,25 +168,186 @@ __global__ __launch_bounds__(GSR_TILE_PIX) __attribute__((amdgpu_waves_per_eu(3)
 #pragma unroll
         for (int j = 0; j < kBwdBatch; j++) adl[j] = wl[l32 * kBwdPitch + 2 * j + hi];
         wave_lds_order();
+        // g = f . dL MFMA B operands: k-step k of pixel half h, lane l: dL[channel 16(l>>5) + k]
+        // [pixel 32h + (l&31)] -- one swap per k turns (dL[k], dL[16+k]) into the two halves' operands
+        float bh0[16], bh1[16];
+#pragma unroll
+        for (int k = 0; k < 16; k++) {
+            const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(dL[k]), __float_as_uint(dL[16 + k]),
+                                                             false, false);
+            bh0[k] = __uint_as_float(sw[0]);
+            bh1[k] = __uint_as_float(sw[1]);
+        }
 
-        // the current batch: slot s holds Gaussian gbat[lane s], its weights at wl[s][pixel]
-        int slot = 0;
-        int gbat = 0;
-        auto flush = [&]() {
+        // ---- survivor stream: chunks of 64 list positions, last chunk first (the next lower chunk
+        // prefetched); survivors appended to the ring in back-to-front order
+        int base = (int)((ns - 1) & ~63u) + 64;
+        uint32_t nidx = base - 64 + lane < (int)ns ? plist[base - 64 + lane] : 0u;
+        uint32_t head = 0, tail = 0;  // wave-uniform ring counters
+        bool list_done = false;
+        auto fill = [&](uint32_t want) {
+            while (!list_done && tail - head < want) {
+                base -= 64;
+                if (base < 0) { list_done = true; break; }
+                const uint32_t cidx = nidx;
+                if (base >= 64) nidx = plist[base - 64 + lane];
+                const bool sv = base + lane < (int)ns && (cidx & smask_bit) != 0u;
+                const uint64_t m = __ballot(sv);
+                if (sv) {
+                    // rank among the chunk's survivors counted from the back (higher positions first)
+                    const uint32_t above = lane == 63 ? 0u : (uint32_t)__popcll(m >> (lane + 1));
+                    const uint32_t slot = (tail + above) & (kBwdRing - 1);
+                    ring_g[slot] = cidx & kIndexMask;
+                    ring_p[slot] = (uint32_t)(base + lane);
+                }
+                tail += (uint32_t)__popcll(m);
+            }
+            wave_lds_order();
+        };
+        // a batch, lane-distributed: lane l holds survivor l&31's index / position, its render
+        // record (both halves) and 16 channels 16(l>>5).. of its feature row
+        uint32_t nb = 0, bg_ = 0, bp_ = 0;
+        float4 ra_ = make_float4(0.f, 0.f, 0.f, 0.f), rc_ = ra_;
+        float fr[16];
+        auto pop = [&](uint32_t& nb_o, uint32_t& g_o, uint32_t& p_o, float4& ra_o, float4& rc_o, float (&f_o)[16]) {
+            nb_o = min(tail - head, (uint32_t)kBwdBatch);
+            const uint32_t slot = (head + (uint32_t)l32) & (kBwdRing - 1);
+            const bool valid = (uint32_t)l32 < nb_o;
+            g_o = valid ? ring_g[slot] : 0u;
+            p_o = valid ? ring_p[slot] : 0xFFFFFFFFu;
+            head += nb_o;
+            if (valid) {
+                ra_o = rrec[2 * g_o];
+                rc_o = rrec[2 * g_o + 1];
+                const float4* fsrc = reinterpret_cast<const float4*>(colors + (int64_t)g_o * GSR_C + 16 * hi);
+#pragma unroll
+                for (int u = 0; u < 4; u++) {
+                    const float4 v = fsrc[u];
+                    f_o[4 * u] = v.x; f_o[4 * u + 1] = v.y; f_o[4 * u + 2] = v.z; f_o[4 * u + 3] = v.w;
+                }
+            } else {
+                ra_o = make_float4(0.f, 0.f, 0.f, 0.f);
+                rc_o = ra_o;
+#pragma unroll
+                for (int u = 0; u < 16; u++) f_o[u] = 0.f;
+            }
+        };
+        fill(kBwdBatch);
+        pop(nb, bg_, bp_, ra_, rc_, fr);
+
+        float T = T_final;
+        float accum_dot = 0.f, last_gdot = 0.f, last_alpha = 0.f;
+        float accum_inv = 0.f, last_inv = 0.f;
+        while (nb) {
+            // next batch: survivors into the ring, then its loads in flight during this batch
+            uint32_t nb_n, bg_n, bp_n;
+            float4 ra_n, rc_n;
+            float fr_n[16];
+            fill(kBwdBatch);
+            pop(nb_n, bg_n, bp_n, ra_n, rc_n, fr_n);
+
+            // g[s][px] = sum_ch f_s[ch] dL[ch][px] for the batch (rows s, columns px of each half)
+            floatx16 gd0, gd1;
+#pragma unroll
+            for (int r = 0; r < 16; r++) { gd0[r] = 0.f; gd1[r] = 0.f; }
+#pragma unroll
+            for (int k = 0; k < 16; k++) {
+                gd0 = __builtin_amdgcn_mfma_f32_32x32x2f32(fr[k], bh0[k], gd0, 0, 0, 0);
+                gd1 = __builtin_amdgcn_mfma_f32_32x32x2f32(fr[k], bh1[k], gd1, 0, 0, 0);
+            }
+            // to pixel lanes: gd0[r] = g of slot (r&3) + 8(r>>2), gd1[r] = of slot (r&3) + 8(r>>2) + 4
+#pragma unroll
+            for (int r = 0; r < 16; r++) {
+                const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(gd0[r]), __float_as_uint(gd1[r]),
+                                                                 false, false);
+                gd0[r] = __uint_as_float(sw[0]);
+                gd1[r] = __uint_as_float(sw[1]);
+            }
+
+            // serial replay of the batch, slot by slot (static slots: g lives in registers)
+#pragma unroll
+            for (int s = 0; s < kBwdBatch; s++) {
+                if ((uint32_t)s >= nb) continue;  // (not break: the loop must unroll -- static slots)
+                const float gdot = (s & 4) ? gd1[(s & 3) + 4 * (s >> 3)] : gd0[(s & 3) + 4 * (s >> 3)];
+                const uint32_t contributor = __builtin_amdgcn_readlane(bp_, s);
+                // record: x, y, opacity, 1/depth | -a/2, -b, -c/2
+                const float rx = __uint_as_float(__builtin_amdgcn_readlane(__float_as_uint(ra_.x), s));
+                const float ry = __uint_as_float(__builtin_amdgcn_readlane(__float_as_uint(ra_.y), s));
+                const float ro = __uint_as_float(__builtin_amdgcn_readlane(__float_as_uint(ra_.z), s));
+                const float rinv = __uint_as_float(__builtin_amdgcn_readlane(__float_as_uint(ra_.w), s));
+                const float qa = __uint_as_float(__builtin_amdgcn_readlane(__float_as_uint(rc_.x), s));
+                const float qb = __uint_as_float(__builtin_amdgcn_readlane(__float_as_uint(rc_.y), s));
+                const float qc = __uint_as_float(__builtin_amdgcn_readlane(__float_as_uint(rc_.z), s));
+                const float dx = rx - pfx, dy = ry - pfy;
+                // branch-free: every lane evaluates, `act` selects (the divergent form costs exec
+                // juggling around every step and saves nothing -- both sides run anyway)
+                const float power = blend_power(qa, qb, qc, dx, dy);
+                const float G = blend_exp<EXACT>(power);
+                const float alpha = fminf(0.99f, ro * G);
+                const bool act = inside && contributor < last_contributor && !(power > 0.0f) &&
+                                 !(alpha < 1.0f / 255.0f);
+                const float one_m = 1.f - alpha;
+                const float rinv1m = __builtin_amdgcn_rcpf(one_m);
+                // T / (1 - alpha): reciprocal + one Newton step on the quotient (<= 1 ulp)
+                float Tq = T * rinv1m;
+                Tq = fmaf(fmaf(-Tq, one_m, T), rinv1m, Tq);
+                T = act ? Tq : T;
+                const float wgt = act ? alpha * T : 0.f;
+                const float acc_n = last_alpha * last_gdot + (1.f - last_alpha) * accum_dot;
+                accum_dot = act ? acc_n : accum_dot;
+                last_gdot = act ? gdot : last_gdot;
+                float dL_dalpha = gdot - accum_dot;
+                float v[8];
+                v[7] = 0.f;
+                v[6] = 0.f;
+                if (INVD) {
+                    const float ai_n = last_alpha * last_inv + (1.f - last_alpha) * accum_inv;
+                    accum_inv = act ? ai_n : accum_inv;
+                    last_inv = act ? rinv : last_inv;
+                    dL_dalpha += (rinv - accum_inv) * dL_inv;
+                    v[6] = wgt * dL_inv;
+                }
+                dL_dalpha *= T;
+                last_alpha = act ? alpha : last_alpha;
+                dL_dalpha += (-T_final * rinv1m) * bg_dot;
+                dL_dalpha = act ? dL_dalpha : 0.f;
+                {
+                    const float Ga = act ? G : 0.f;  // inactive lanes: every term exactly 0 (G may be inf)
+                    const float ca = -2.0f * qa, cb = -qb, cc = -2.0f * qc;  // exact
+                    const float dL_dG = ro * dL_dalpha;
+                    const float gdx = Ga * dx;
+                    const float gdy = Ga * dy;
+                    const float dG_ddelx = -gdx * ca - gdy * cb;
+                    const float dG_ddely = -gdy * cc - gdx * cb;
+                    v[0] = dL_dG * dG_ddelx * ddelx_dx;
+                    v[1] = dL_dG * dG_ddely * ddely_dy;
+                    v[2] = -0.5f * gdx * dx * dL_dG;
+                    v[3] = -0.5f * gdx * dy * dL_dG;
+                    v[4] = -0.5f * gdy * dy * dL_dG;
+                    v[5] = Ga * dL_dalpha;
+                }
+                // weights and the 7 reduced terms parked in LDS; the atomics go out with the batch
+                wl[s * kBwdPitch + lane] = wgt;
+                float r = 0.f;
+                if (__any(act)) r = wave_transpose_reduce8(v);
+                if ((lane & 7) == 0)
+                    cl[s * kBwdComps + ((lane >> 5) & 1) * 4 + ((lane >> 4) & 1) * 2 + ((lane >> 3) & 1)] = r;
+            }
+
+            // ---- flush: dL/dcolor = sum_px w dL on the matrix cores, then the batch's atomics
             wave_lds_order();
             floatx16 acc;
 #pragma unroll
             for (int r = 0; r < 16; r++) acc[r] = 0.f;
 #pragma unroll
             for (int j = 0; j < kBwdBatch; j++) {
-                const float w = l32 < slot ? wl[l32 * kBwdPitch + 2 * j + hi] : 0.f;
+                const float w = (uint32_t)l32 < nb ? wl[l32 * kBwdPitch + 2 * j + hi] : 0.f;
                 acc = __builtin_amdgcn_mfma_f32_32x32x2f32(adl[j], w, acc, 0, 0, 0);
             }
             wave_lds_order();
             // acc[r] at lane l: channel (r&3) + 8(r>>2) + 4(l>>5) of the batch's Gaussian l&31
-            const uint32_t gsel = (uint32_t)__shfl(gbat, l32);
-            if (l32 < slot) {
-                const int64_t gg = gbase + gsel;
+            if ((uint32_t)l32 < nb) {
+                const int64_t gg = gbase + bg_;
                 float* dst = gr.dL_dcolors + gg * GSR_C + 4 * hi;
 #pragma unroll
                 for (int r = 0; r < 16; r++) {
@@ -198,105 +371,11 @@ __global__ __launch_bounds__(GSR_TILE_PIX) __attribute__((amdgpu_waves_per_eu(3)
                 }
             }
             wave_lds_order();
-            slot = 0;
-        };
 
-        float T = T_final;
-        float accum_dot = 0.f, last_gdot = 0.f, last_alpha = 0.f;
-        float accum_inv = 0.f, last_inv = 0.f;
-        // survivor stream, back to front: chunks of 64 list positions, last chunk first (the next
-        // lower chunk prefetched), the strip's survivors of a chunk from its highest bit down
-        int base = (int)((ns - 1) & ~63u) + 64;
-        uint32_t cidx = 0;
-        uint32_t nidx = base - 64 + lane < (int)ns ? plist[base - 64 + lane] : 0u;
-        uint64_t mask = 0;
-        auto next_survivor = [&](uint32_t& gi_o, uint32_t& contrib_o) -> bool {
-            while (mask == 0) {
-                base -= 64;
-                if (base < 0) return false;
-                cidx = nidx;
-                if (base >= 64) nidx = plist[base - 64 + lane];
-                mask = __ballot(base + lane < (int)ns && (cidx & smask_bit) != 0u);
-            }
-            const int i = 63 - (int)__builtin_clzll(mask);
-            mask &= ~(1ull << i);
-            gi_o = __builtin_amdgcn_readlane(cidx, i) & kIndexMask;
-            contrib_o = (uint32_t)(base + i);  // 0-based list position
-            return true;
-        };
-        // one survivor of look-ahead: its render record is in flight while the current one runs
-        uint32_t gi = 0, contributor = 0;
-        bool have = next_survivor(gi, contributor);
-        float4 ra = make_float4(0.f, 0.f, 0.f, 0.f), rc = ra;
-        if (have) { ra = rrec[2 * gi + vzero]; rc = rrec[2 * gi + 1 + vzero]; }
-        while (have) {
-            uint32_t gi_n = 0, contributor_n = 0;
-            const bool have_n = next_survivor(gi_n, contributor_n);
-            float4 ra_n = ra, rc_n = rc;
-            if (have_n) { ra_n = rrec[2 * gi_n + vzero]; rc_n = rrec[2 * gi_n + 1 + vzero]; }
-            {
-                // ra: x, y, opacity, 1/depth; rc: -a/2, -b, -c/2
-                const float dx = ra.x - pfx, dy = ra.y - pfy;
-                const float power = blend_power(rc.x, rc.y, rc.z, dx, dy);
-                bool act = inside && contributor < last_contributor && !(power > 0.0f);
-                float G = 0.f, alpha = 0.f;
-                if (act) {
-                    G = blend_exp<EXACT>(power);
-                    alpha = fminf(0.99f, ra.z * G);
-                    act = !(alpha < 1.0f / 255.0f);
-                }
-                if (__any(act)) {
-                    float v[8];
+            nb = nb_n; bg_ = bg_n; bp_ = bp_n; ra_ = ra_n; rc_ = rc_n;
 #pragma unroll
-                    for (int k = 0; k < 8; k++) v[k] = 0.f;
-                    float wgt = 0.f;
-                    if (act) {
-                        const float ca = -2.0f * rc.x, cb = -rc.y, cc = -2.0f * rc.z;  // exact
-                        T = T / (1.f - alpha);
-                        wgt = alpha * T;
-                        const float* f = colors + (int64_t)gi * GSR_C;
-                        float gdot = 0.f;
-#pragma unroll
-                        for (int ch = 0; ch < GSR_C; ch++) gdot = fmaf(f[ch], dL[ch], gdot);
-                        accum_dot = last_alpha * last_gdot + (1.f - last_alpha) * accum_dot;
-                        last_gdot = gdot;
-                        float dL_dalpha = gdot - accum_dot;
-                        if (INVD) {
-                            const float invdg = ra.w;
-                            accum_inv = last_alpha * last_inv + (1.f - last_alpha) * accum_inv;
-                            last_inv = invdg;
-                            dL_dalpha += (invdg - accum_inv) * dL_inv;
-                            v[6] = wgt * dL_inv;
-                        }
-                        dL_dalpha *= T;
-                        last_alpha = alpha;
-                        dL_dalpha += (-T_final / (1.f - alpha)) * bg_dot;
-                        const float dL_dG = ra.z * dL_dalpha;
-                        const float gdx = G * dx;
-                        const float gdy = G * dy;
-                        const float dG_ddelx = -gdx * ca - gdy * cb;
-                        const float dG_ddely = -gdy * cc - gdx * cb;
-                        v[0] = dL_dG * dG_ddelx * ddelx_dx;
-                        v[1] = dL_dG * dG_ddely * ddely_dy;
-                        v[2] = -0.5f * gdx * dx * dL_dG;
-                        v[3] = -0.5f * gdx * dy * dL_dG;
-                        v[4] = -0.5f * gdy * dy * dL_dG;
-                        v[5] = G * dL_dalpha;
-                    }
-                    // this Gaussian joins the batch: its weights and its 7 reduced terms are parked
-                    // in LDS, all of its atomics go out with the batch (none between two flushes)
-                    wl[slot * kBwdPitch + lane] = wgt;
-                    gbat = lane == slot ? (int)gi : gbat;
-                    const float r = wave_transpose_reduce8(v);
-                    if ((lane & 7) == 0)
-                        cl[slot * kBwdComps + ((lane >> 5) & 1) * 4 + ((lane >> 4) & 1) * 2 + ((lane >> 3) & 1)] = r;
-                    slot++;
-                    if (slot == kBwdBatch) flush();
-                }
-            }
-            gi = gi_n; contributor = contributor_n; ra = ra_n; rc = rc_n; have = have_n;
+            for (int u = 0; u < 16; u++) fr[u] = fr_n[u];
         }
-        if (slot) flush();
     }
 }
 
@@ -310,7 +389,7 @@ void launch_render_bwd(const Dims& d, const Inputs& in, const GeomArena& g, cons
     if (nwaves == 0) return;
     hipLaunchKernelGGL(k_zero_bwd_queues, dim3(1), dim3(64), 0, s, g.ctrl);
     const bool invd = gr.dL_dinvdepth != nullptr && gr.dL_dinvdepth_g != nullptr;
-    const dim3 grid(min((nwaves + 3) / 4, persistent_grid(8))), blk(GSR_TILE_PIX);
+    const dim3 grid(min((nwaves + 3) / 4, persistent_grid(2))), blk(GSR_TILE_PIX);
     if (exact) {
         if (invd) hipLaunchKernelGGL((k_render_bwd<true, true>), grid, blk, 0, s, d, in, g, im, b, gr);
         else hipLaunchKernelGGL((k_render_bwd<true, false>), grid, blk, 0, s, d, in, g, im, b, gr);

@@ -71,24 +71,6 @@ __device__ __forceinline__ float take_step(float alpha, float inv_depth, uint32_
 // are exact in f32, so the only loss is the split residual (|f - f_hi - f_lo| <= 2^-17 |f|, the same
 // for w): <= 3e-5 relative per product, summed under sum(w) <= 1.  One v_mfma_f32_32x32x16_bf16
 // (8 passes) replaces the 16-pass f32 MFMA per pixel half.
-typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
-typedef float float2x __attribute__((ext_vector_type(2)));
-// v_cvt_pk_bf16_f32 (round to nearest even) of (x, y), x in the low half
-__device__ __forceinline__ unsigned cvt_pk_bf16(float x, float y) {
-    return __builtin_bit_cast(unsigned, __builtin_convertvector((float2x){x, y}, bf16x2));
-}
-// (hi, lo) packed low|high: hi = bf16(f), lo = bf16(f - hi)
-__device__ __forceinline__ unsigned split_hl(float f) {
-    const float hf = __uint_as_float(cvt_pk_bf16(f, f) << 16);
-    return cvt_pk_bf16(hf, f - hf);
-}
-// (hi, hi) and (lo, lo)
-__device__ __forceinline__ void split_hh_ll(float w, unsigned& hh, unsigned& ll) {
-    hh = cvt_pk_bf16(w, w);
-    const float r = w - __uint_as_float(hh << 16);
-    ll = cvt_pk_bf16(r, r);
-}
-
 // The split of a batch-shared feature table, once per launch (P x 32 words; render_fwd then loads
 // the packed word in place of the f32 feature).
 __global__ __launch_bounds__(256) void k_split_features(int n4, const float4* __restrict__ f,
@@ -214,6 +196,21 @@ void launch_refine_prepare(int n, const float* in, const float* w, int n_out, in
     hipLaunchKernelGGL(k_refine_prepare, dim3((n + 255) / 256), dim3(256), 0, s, n, in, w, n_out, keep, out);
 }
 
+// Capacity overflow (batch path): nothing was binned, so the call's images are filled with NaN --
+// a consumer cannot mistake a stale or partial frame for a render.  Grid-stride over the whole
+// grid, taken only on overflow.
+__device__ __forceinline__ void overflow_fill(const Dims& d, const Outputs& o) {
+    const float qnan = __builtin_nanf("");
+    const int64_t HW = (int64_t)d.H * d.W;
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    const int64_t i0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    for (int64_t i = i0; i < (int64_t)d.B * GSR_C * HW; i += stride) o.out_color[i] = qnan;
+    if (o.out_invdepth)
+        for (int64_t i = i0; i < (int64_t)d.B * HW; i += stride) o.out_invdepth[i] = qnan;
+    if (o.out_refine)
+        for (int64_t i = i0; i < (int64_t)d.B * o.n_out * HW; i += stride) o.out_refine[i] = qnan;
+}
+
 // Work items: the 4 strips of each non-empty tile in strip_list order, most survivors first (items
 // [0, 4*NE)), then each empty tile whole (items [4*NE, 3*NE + B*T)).  Eight queues, one per
 // XCD, take every eighth item (item = x + 8k); a wave dequeues from its own XCD's queue and, once
@@ -227,7 +224,10 @@ template <bool EXACT, bool STATS, bool TL, bool REFINE, int ABL = 0, int SPLIT =
 __device__ __forceinline__ void render_fwd_body(const Dims& d, const Inputs& in, const GeomArena& g,
                                                 const ImageArena& im, const BinArena& bn,
                                                 const Outputs& o) {
-    if (g.ctrl[kCtrlOverflow]) return;
+    if (g.ctrl[kCtrlOverflow]) {  // the lists were not built: every output pixel of the call is NaN
+        overflow_fill(d, o);
+        return;
+    }
     const uint32_t ne = g.ctrl[kCtrlNonEmpty];
     const uint32_t nstrip = (uint32_t)kStrips * ne;
     const uint32_t nitems = nstrip + (uint32_t)(d.B * d.T) - ne;

@@ -1,3 +1,18 @@
+#
+# The Python/autograd surface below follows diff_gaussian_rasterization_32/__init__.py of the
+# reference, which carries this notice:
+#
+# Copyright (C) 2023, Inria
+# GRAPHDECO research group, https://team.inria.fr/graphdeco
+# All rights reserved.
+#
+# This software is free for non-commercial, research and evaluation use
+# under the terms of the LICENSE.md file.
+#
+# For inquiries contact  george.drettakis@inria.fr
+#
+# (LICENSE.md: /root/reference/submodules/diff-gaussian-rasterization-32/LICENSE.md, reproduced in
+# this package as LICENSE.md.)
 """Drop-in replacement of diff_gaussian_rasterization_32 for AMD MI355X (gfx950).
 
 Python/autograd surface identical to the reference package

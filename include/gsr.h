@@ -106,8 +106,9 @@ int gsr_backward(int P, int D, int M, int R, const float* background, int width,
  * viewmatrices/projmatrices: [B,16]; tanfov: [B,2] (x,y); backgrounds: [B,32] with bg_stride.
  * workspace: gsr_batch_workspace_bytes(B,P,W,H,R_capacity) bytes of device memory, reused by
  * gsr_backward_batch.  Outputs: out_color [B,32,H,W], out_invdepth [B,H,W] (or NULL),
- * radii [B,P] (or NULL).  No host synchronisation: call gsr_batch_status() to learn R and
- * whether the capacity overflowed (then nothing was rendered). */
+ * radii [B,P] (or NULL).  P < 2^24.  No host synchronisation: call gsr_batch_status() to learn R
+ * and whether the capacity overflowed (then every output pixel of the call is NaN and the
+ * workspace's sticky overflow word is set, gsr_batch_status_offset). */
 size_t gsr_batch_workspace_bytes(int B, int P, int width, int height, int64_t R_capacity);
 int gsr_forward_batch(int B, int P, int width, int height, const float* means3D,
                       int64_t means_stride, const float* colors, int64_t colors_stride,
@@ -184,6 +185,14 @@ int gsr_render_counters(uint64_t* device_counters);
  * work items in longest-first order (strip items first, 4 per non-empty tile). */
 int gsr_render_timeline(uint32_t* device_records, uint32_t capacity);
 
+/* Byte offset, inside a batch workspace, of its 4 sticky status words (uint32): [0] = 1 once any
+ * gsr_forward_batch* on it overflowed the R capacity (that call's frames are NaN), [1] = the largest
+ * batch instance count R seen.  Calls never reset them (the per-call control words are reset);
+ * the owner zeroes them when it allocates the workspace and after it has read an overflow, and may
+ * copy them to host memory asynchronously after each call to notice an overflow without a
+ * synchronisation.  No reference counterpart (the reference sizes the binning buffer after a
+ * host synchronisation, rasterizer_impl.cu:284-288). */
+size_t gsr_batch_status_offset(int B, int P, int width, int height, int64_t R_capacity);
 /* Synchronises `stream`; writes the batch's instance count and overflow flag. */
 int gsr_batch_status(const char* workspace, int B, int P, int64_t* R_total, int* overflow,
                      void* stream);

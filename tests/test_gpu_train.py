@@ -1,0 +1,213 @@
+"""BASELINE config 4 (the training step) at full size: 100k-Gaussian avatar, 512x512.
+
+* render backward + projection backward of ONE config-2 frame through the drop-in `_C` API, and
+  of a 6-frame batch (BatchRasterizer.backward, the training step's path, per-frame views) for
+  frames 0 and 5, against the CPU oracle's backward (reference backward.cu:147-638 restated):
+  every gradient within 1e-4 of its own max magnitude;
+* SplatTrainer.gradients (fwd -> (1-l) L1 + l (1 - SSIM) on RGB -> bwd, summed over frames; the
+  reference's main/trainer.py:82-102 rasterizer side) against a CPU recomputation: the image
+  gradient from torch autograd of an L1 + conv2d-SSIM loss in float64 on the same rendered frames,
+  then oracle.backward per frame, summed;
+* capacity overflow: NaN frames, CapacityError on the next call, and the trainer skipping the
+  overflowing step on the device (fused Adam found_inf) and growing its workspace.
+"""
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+from helpers import torch_inputs
+
+pytestmark = pytest.mark.gpu
+DEV = torch.device("cuda:0")
+NAMES = ("means2D", "colors", "opacity", "means3D", "cov3D", "sh", "scales", "rotations")
+TOL = 1e-4  # of each gradient's max |oracle| (DESIGN.md numerics contract)
+
+
+def _rel_err(a, b):
+    return float(np.abs(a.reshape(b.shape) - b).max() / max(np.abs(b).max(), 1e-20))
+
+
+def _scene_c2(cams=1, seed=0):
+    from guava_renderer_amd import scenes
+    sc = scenes.avatar_cloud(100000, seed=seed)
+    return sc, scenes.frame_cameras(max(cams, 2), 512, 512, seed=1000)
+
+
+def _oracle_grads(sc, cam, dL, dLinv):
+    import oracle
+    oracle.set_threads(8)
+    bg = np.zeros(32, np.float32)
+    _, _, _, st = oracle.forward(sc["means3D"], sc["colors"], sc["opacities"], sc["scales"], sc["rotations"],
+                                 None, cam["viewmatrix"], cam["projmatrix"], 512, 512, cam["tanfovx"],
+                                 cam["tanfovy"], bg)
+    return oracle.backward(st, sc["means3D"], sc["colors"], sc["opacities"], sc["scales"], sc["rotations"],
+                           None, cam["viewmatrix"], cam["projmatrix"], 512, 512, cam["tanfovx"], cam["tanfovy"],
+                           bg, dL, dLinv)
+
+
+def test_fullsize_backward_single_frame_drop_in():
+    """Config 4 gradients of one frame through _C.rasterize_gaussians(_backward)."""
+    from guava_renderer_amd import _lib
+    from guava_renderer_amd.diff_gaussian_rasterization_32 import _C
+    _lib.set_exact_exp(True)
+    sc, cams = _scene_c2()
+    cam = cams[1]
+    d = dict(sc, **cam, bg=np.zeros(32, np.float32))
+    t = torch_inputs(d)
+    empty = torch.Tensor([])
+    R, color, radii, gb, bb, ib, invd = _C.rasterize_gaussians(
+        t["bg"], t["means3D"], t["colors"], t["opacities"], t["scales"], t["rotations"], 1.0, empty,
+        t["viewmatrix"], t["projmatrix"], cam["tanfovx"], cam["tanfovy"], 512, 512, empty, 0,
+        t["campos"], False, False, False)
+    rng = np.random.default_rng(11)
+    dL = rng.normal(size=(32, 512, 512)).astype(np.float32)
+    dLinv = rng.normal(size=(1, 512, 512)).astype(np.float32)
+    grads = _C.rasterize_gaussians_backward(
+        t["bg"], t["means3D"], radii, t["colors"], t["opacities"], t["scales"], t["rotations"], 1.0, empty,
+        t["viewmatrix"], t["projmatrix"], cam["tanfovx"], cam["tanfovy"], torch.tensor(dL, device=DEV),
+        torch.tensor(dLinv, device=DEV), empty, 0, t["campos"], gb, R, bb, ib, False, False)
+    torch.cuda.synchronize()
+    o = _oracle_grads(sc, cam, dL, dLinv)
+    for name, a, b in zip(NAMES, grads, o):
+        if b.size:
+            err = _rel_err(a.cpu().numpy(), b)
+            assert err <= TOL, f"{name}: {err:.3g}"
+
+
+def test_fullsize_backward_batch6():
+    """BatchRasterizer.backward at the training batch (6 per-frame views): frames 0 and 5 vs the
+    oracle, per-frame gradient tensors."""
+    from guava_renderer_amd import _lib
+    from guava_renderer_amd.batch import BatchRasterizer
+    _lib.set_exact_exp(True)
+    sc, cams = _scene_c2(cams=6)
+    cams = cams[:6]
+    B = 6
+    t = lambda x: torch.tensor(np.ascontiguousarray(x), device=DEV)  # noqa: E731
+    views = t(np.stack([c["viewmatrix"].reshape(16) for c in cams]))
+    projs = t(np.stack([c["projmatrix"].reshape(16) for c in cams]))
+    tanf = t(np.array([[c["tanfovx"], c["tanfovy"]] for c in cams], np.float32))
+    bgs = torch.zeros((B, 32), device=DEV)
+    args = [t(sc[k]) for k in ("means3D", "colors", "opacities", "scales", "rotations")]
+    r = BatchRasterizer(B, 100000, 512, 512, R_capacity=12 * 100000 * B, device=DEV)
+    r.forward(*args, views, projs, tanf, bgs)
+    rng = np.random.default_rng(12)
+    dL = rng.normal(size=(B, 32, 512, 512)).astype(np.float32)
+    dLinv = rng.normal(size=(B, 512, 512)).astype(np.float32)
+    g = r.backward(*args, views, projs, tanf, bgs, t(dL), t(dLinv))
+    torch.cuda.synchronize()
+    assert not r.status()[1]
+    gpu = {k: v.cpu().numpy() for k, v in g.items() if v is not None}
+    for f in (0, 5):
+        o = _oracle_grads(sc, cams[f], dL[f], dLinv[f][None])
+        mine = {"means2D": gpu["mean2D"][f], "colors": gpu["colors"][f], "opacity": gpu["opacity"][f],
+                "means3D": gpu["means3D"][f], "cov3D": gpu["cov3D"][f], "scales": gpu["scales"][f],
+                "rotations": gpu["rotations"][f]}
+        for name, b in zip(NAMES, o):
+            if name in mine:
+                err = _rel_err(mine[name], b)
+                assert err <= TOL, f"frame {f} {name}: {err:.3g}"
+
+
+def _ssim64(img, tgt):
+    g = torch.tensor([np.exp(-(x - 5) ** 2 / (2 * 1.5 ** 2)) for x in range(11)], dtype=torch.float64)
+    g = g / g.sum()
+    ch = img.shape[1]
+    w = (g[:, None] @ g[None, :]).expand(ch, 1, 11, 11).contiguous()
+    mu1 = F.conv2d(img, w, padding=5, groups=ch)
+    mu2 = F.conv2d(tgt, w, padding=5, groups=ch)
+    s1 = F.conv2d(img * img, w, padding=5, groups=ch) - mu1 ** 2
+    s2 = F.conv2d(tgt * tgt, w, padding=5, groups=ch) - mu2 ** 2
+    s12 = F.conv2d(img * tgt, w, padding=5, groups=ch) - mu1 * mu2
+    C1, C2 = 0.01 ** 2, 0.03 ** 2
+    return (((2 * mu1 * mu2 + C1) * (2 * s12 + C2)) / ((mu1 ** 2 + mu2 ** 2 + C1) * (s1 + s2 + C2))).mean()
+
+
+def test_trainer_gradients_match_cpu_recomputation():
+    from guava_renderer_amd import _lib, scenes
+    from guava_renderer_amd.train import SplatTrainer
+    _lib.set_exact_exp(True)
+    _lib.set_split_bf16(False)
+    B, W = 2, 512
+    sc = scenes.avatar_cloud(100000, seed=0)
+    cams = scenes.frame_cameras(B, W, W, seed=1000)
+    t = lambda x: torch.tensor(np.ascontiguousarray(x), device=DEV)  # noqa: E731
+    views = t(np.stack([c["viewmatrix"].reshape(16) for c in cams]))
+    projs = t(np.stack([c["projmatrix"].reshape(16) for c in cams]))
+    tanf = t(np.array([[c["tanfovx"], c["tanfovy"]] for c in cams], np.float32))
+    params = {k: t(sc[k]) for k in ("means3D", "colors", "opacities", "scales", "rotations")}
+    tr = SplatTrainer(params, B, W, W, R_capacity=12 * 100000 * B, device=DEV)
+    target = torch.rand((B, 3, W, W), device=DEV, generator=torch.Generator(device=DEV).manual_seed(3))
+    loss, grads = tr.gradients(views, projs, tanf, target)
+    torch.cuda.synchronize()
+    img = tr.rast.out_color[:, :3].detach().cpu().double().requires_grad_(True)
+    tgt = target.cpu().double()
+    lam = tr.lambda_ssim
+    ref_loss = (1 - lam) * (img - tgt).abs().mean() + lam * (1 - _ssim64(img, tgt))
+    ref_loss.backward()
+    assert abs(loss.item() - ref_loss.item()) <= 1e-5 * abs(ref_loss.item()) + 1e-6
+    dimg = img.grad.float().numpy()
+    acc = None
+    for f in range(B):
+        dL = np.zeros((32, W, W), np.float32)
+        dL[:3] = dimg[f]
+        o = _oracle_grads(sc, cams[f], dL, np.zeros((1, W, W), np.float32))
+        o = {"means3D": o[3], "colors": o[1], "opacities": o[2], "scales": o[6], "rotations": o[7]}
+        acc = o if acc is None else {k: acc[k] + o[k] for k in acc}
+    for k, b in acc.items():
+        err = _rel_err(grads[k].cpu().numpy(), b)
+        assert err <= 2e-4, f"{k}: {err:.3g}"
+
+
+def test_overflow_nan_frames_and_capacity_error():
+    from guava_renderer_amd import _lib, scenes
+    from guava_renderer_amd.batch import BatchRasterizer
+    sc = scenes.avatar_cloud(20000, seed=1)
+    cams = scenes.frame_cameras(2, 256, 256, seed=1000)
+    t = lambda x: torch.tensor(np.ascontiguousarray(x), device=DEV)  # noqa: E731
+    views = t(np.stack([c["viewmatrix"].reshape(16) for c in cams]))
+    projs = t(np.stack([c["projmatrix"].reshape(16) for c in cams]))
+    tanf = t(np.array([[c["tanfovx"], c["tanfovy"]] for c in cams], np.float32))
+    args = [t(sc[k]) for k in ("means3D", "colors", "opacities", "scales", "rotations")]
+    bgs = torch.zeros((2, 32), device=DEV)
+    r = BatchRasterizer(2, 20000, 256, 256, R_capacity=1000, device=DEV)
+    col, inv, _ = r.forward(*args, views, projs, tanf, bgs)
+    torch.cuda.synchronize()
+    assert torch.isnan(col).all() and torch.isnan(inv).all()
+    assert int(r.overflow_flag()) == 1
+    with pytest.raises(_lib.CapacityError):
+        r.poll(wait=True)
+    r.poll(wait=True)  # acknowledged: cleared
+    # a large enough workspace renders the same batch
+    r2 = BatchRasterizer(2, 20000, 256, 256, R_capacity=20 * 20000 * 2, device=DEV)
+    col2, _, _ = r2.forward(*args, views, projs, tanf, bgs)
+    r2.poll(wait=True)
+    assert torch.isfinite(col2).all()
+    assert r2.max_instances_seen() > 1000
+
+
+def test_trainer_skips_overflowing_step():
+    from guava_renderer_amd import scenes
+    from guava_renderer_amd.train import SplatTrainer
+    sc = scenes.avatar_cloud(20000, seed=2)
+    cams = scenes.frame_cameras(2, 256, 256, seed=1000)
+    t = lambda x: torch.tensor(np.ascontiguousarray(x), device=DEV)  # noqa: E731
+    views = t(np.stack([c["viewmatrix"].reshape(16) for c in cams]))
+    projs = t(np.stack([c["projmatrix"].reshape(16) for c in cams]))
+    tanf = t(np.array([[c["tanfovx"], c["tanfovy"]] for c in cams], np.float32))
+    params = {k: t(sc[k]) for k in ("means3D", "colors", "opacities", "scales", "rotations")}
+    tr = SplatTrainer(params, 2, 256, 256, R_capacity=1000, device=DEV)
+    target = torch.rand((2, 3, 256, 256), device=DEV)
+    before = {k: v.detach().clone() for k, v in tr.p.items()}
+    loss = tr.step(views, projs, tanf, target)
+    torch.cuda.synchronize()
+    assert torch.isnan(loss)
+    for k, v in tr.p.items():  # the update was skipped on the device
+        assert torch.equal(v.detach(), before[k]), k
+    with pytest.warns(UserWarning):
+        loss2 = tr.step(views, projs, tanf, target)
+    torch.cuda.synchronize()
+    assert tr.skipped_steps == 1 and tr.rast.R_capacity > 1000
+    assert torch.isfinite(loss2)
+    assert any(not torch.equal(v.detach(), before[k]) for k, v in tr.p.items())
