@@ -136,6 +136,7 @@ class BatchRasterizer:
             return
         if int(self._status_host[0]):
             rmax = int(self._status_host[1]) & 0xFFFFFFFF
+            self.overflow_need = max(getattr(self, "overflow_need", 0), rmax)
             self._sticky.zero_()
             self._status_host.zero_()
             raise _lib.CapacityError(
@@ -143,8 +144,9 @@ class BatchRasterizer:
                 f"(that forward's images are NaN); allocate a BatchRasterizer with a larger R_capacity")
 
     def max_instances_seen(self):
-        """Largest batch instance count of the forwards whose status copy has landed."""
-        return int(self._status_host[1]) & 0xFFFFFFFF
+        """Largest batch instance count of the forwards whose status copy has landed (including
+        the overflowing ones poll() reported)."""
+        return max(int(self._status_host[1]) & 0xFFFFFFFF, getattr(self, "overflow_need", 0))
 
     def overflow_flag(self):
         """0-dim int32 device tensor: 1 if the last forward overflowed (read on the device, e.g. as an

@@ -133,6 +133,7 @@ size_t carve_geom(char* base, const Dims& d, GeomArena* g) {
     a.order = take<uint32_t>(base, off, n);
     a.table = take<uint32_t>(base, off, (size_t)d.B * d.nchunk * d.T);
     a.fsplit = take<uint32_t>(base, off, (size_t)d.P * GSR_C);
+    a.gterm = take<float>(base, off, n * kGtWords);
     if (g) *g = a;
     return align_up(off) + 256;
 }

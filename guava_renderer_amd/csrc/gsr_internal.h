@@ -83,11 +83,15 @@ struct GeomArena {
     uint32_t* order;      // per frame, visible Gaussians in (depth, index) order
     uint32_t* table;      // [B][nchunk][T] instance counts per (depth chunk, tile), scanned per tile
     uint32_t* fsplit;     // [P][32] features pre-split for the split-bf16 blend: bf16 (hi | lo << 16)
+    float* gterm;         // [B*P][8] render_bwd's per-Gaussian screen-space gradient sums (kGt* order),
+                          // consumed by preprocess_bwd
     // batch path only (else null): status words that survive the per-call ctrl reset --
     // [kStickyOverflow] set by any overflowing forward, [kStickyRMax] largest batch R seen; cleared
     // by the host (gsr_batch_status_offset)
     uint32_t* sticky = nullptr;
 };
+// gterm row: dL/dmean2D x, y, dL/dconic x, y, w, dL/dopacity, dL/dinvdepth, (unused)
+enum GTerm : int { kGtM2x = 0, kGtM2y = 1, kGtCx = 2, kGtCy = 3, kGtCw = 4, kGtOp = 5, kGtInv = 6, kGtWords = 8 };
 enum Sticky : int { kStickyOverflow = 0, kStickyRMax = 1, kStickyWords = 4 };
 
 struct ImageArena {

@@ -25,7 +25,17 @@ __global__ __launch_bounds__(kScanBlock) void k_preprocess_bwd(Dims d, Inputs in
     for (int k = 0; k < 6; k++) c3[k] = c3p[k];
     const float* pm = in.means3D + in.s_means * b + 3 * (int64_t)i;
     const float mean[3] = {pm[0], pm[1], pm[2]};
-    const float dcx = gr.dL_dconic[4 * gid], dcy = gr.dL_dconic[4 * gid + 1], dcz = gr.dL_dconic[4 * gid + 3];
+    // render_bwd's sums for this Gaussian (one 32-byte row), also handed to the caller's buffers
+    const float4 gt0 = reinterpret_cast<const float4*>(g.gterm)[2 * gid];
+    const float4 gt1 = reinterpret_cast<const float4*>(g.gterm)[2 * gid + 1];
+    const float dcx = gt0.z, dcy = gt0.w, dcz = gt1.x;
+    gr.dL_dconic[4 * gid] = dcx;
+    gr.dL_dconic[4 * gid + 1] = dcy;
+    gr.dL_dconic[4 * gid + 3] = dcz;
+    gr.dL_dmean2D[3 * gid] = gt0.x;
+    gr.dL_dmean2D[3 * gid + 1] = gt0.y;
+    gr.dL_dopacity[gid] = gt1.y;
+    if (gr.dL_dinvdepth_g) gr.dL_dinvdepth_g[gid] = gt1.z;
 
     // ---- computeCov2DCUDA ----
     float t[3];
@@ -53,7 +63,7 @@ __global__ __launch_bounds__(kScanBlock) void k_preprocess_bwd(Dims d, Inputs in
         c_yy += h_var;
         const float det_cov_plus_h_cov = c_xx * c_yy - c_xy * c_xy;
         const float h_conv = sqrtf(fmaxf(0.000025f, det_cov / det_cov_plus_h_cov));
-        const float dL_dopacity_v = gr.dL_dopacity[gid];
+        const float dL_dopacity_v = gt1.y;
         const float d_h_conv = dL_dopacity_v * in.opac[in.s_opac * b + i];
         gr.dL_dopacity[gid] = dL_dopacity_v * h_conv;
         d_inside_root = (det_cov / det_cov_plus_h_cov) <= 0.000025f ? 0.f : d_h_conv / (2 * h_conv);
@@ -114,7 +124,7 @@ __global__ __launch_bounds__(kScanBlock) void k_preprocess_bwd(Dims d, Inputs in
     const float dL_dty = y_grad_mul * -h_y * tz2 * dL_dJ12;
     float dL_dtz = -h_x * tz2 * dL_dJ00 - h_y * tz2 * dL_dJ11 + (2 * h_x * t[0]) * tz3 * dL_dJ02 +
                    (2 * h_y * t[1]) * tz3 * dL_dJ12;
-    if (gr.dL_dinvdepth_g) dL_dtz -= gr.dL_dinvdepth_g[gid] / (t[2] * t[2]);
+    if (gr.dL_dinvdepth_g) dL_dtz -= gt1.z / (t[2] * t[2]);
     const float dt[3] = {dL_dtx, dL_dty, dL_dtz};
     float dm[3];
     xformvec_t(dt, view, dm);
@@ -125,7 +135,7 @@ __global__ __launch_bounds__(kScanBlock) void k_preprocess_bwd(Dims d, Inputs in
     const float m_w = 1.0f / (mh[3] + 0.0000001f);
     const float mul1 = (proj[0] * mean[0] + proj[4] * mean[1] + proj[8] * mean[2] + proj[12]) * m_w * m_w;
     const float mul2 = (proj[1] * mean[0] + proj[5] * mean[1] + proj[9] * mean[2] + proj[13]) * m_w * m_w;
-    const float d2x = gr.dL_dmean2D[3 * gid], d2y = gr.dL_dmean2D[3 * gid + 1];
+    const float d2x = gt0.x, d2y = gt0.y;
     dm[0] += (proj[0] * m_w - proj[3] * mul1) * d2x + (proj[1] * m_w - proj[3] * mul2) * d2y;
     dm[1] += (proj[4] * m_w - proj[7] * mul1) * d2x + (proj[5] * m_w - proj[7] * mul2) * d2y;
     dm[2] += (proj[8] * m_w - proj[11] * mul1) * d2x + (proj[9] * m_w - proj[11] * mul2) * d2y;

@@ -1,30 +1,40 @@
 // render_bwd.hip -- back-to-front gradient replay (backward.cu:452-638 of the reference).
 //
-// Differences in structure (same math):
-//  * one wave per 8x8 strip from persistent per-XCD queues, replaying only the Gaussians binning
-//    marked as reaching the strip, from the strip's largest n_contrib instead of the tile list end;
+// Same math as the reference, reorganised for the matrix cores and a short per-Gaussian chain:
+//  * one wave per 8x8 strip from persistent per-XCD queues (lane = pixel), replaying only the
+//    Gaussians binning marked as reaching the strip, from the strip's largest n_contrib instead of
+//    the tile list end;
+//  * survivors go in batches of 32: the list is scanned 64 entries at a time and the strip's
+//    survivors are appended to a wave-private LDS ring, so batches are full whatever the survivor
+//    density; a batch's render records and feature rows are loaded while the previous batch is
+//    replayed;
 //  * the 32-channel "accumulated colour behind" recurrence is carried as its dot product with
-//    dL/dpixel (linear, so sum_ch (c - accum_rec_ch) dL_ch == g - accum_dot with g = f . dL);
-//  * dL/dcolor of a Gaussian is sum_px w_px dL_px (w = alpha T): a contraction over the strip's 64
-//    pixels, done on the matrix cores for batches of 32 active Gaussians -- each lane parks its
-//    pixel's weight in wave-private LDS, and at the end of a batch 32 v_mfma_f32_32x32x2_f32 (two
-//    pixels per k-step) give the [32 channels x 32 Gaussians] block, issued as 16 atomic
-//    instructions, instead of 32 multiplies and a 32-channel cross-lane reduction per Gaussian;
-//  * the other 7 per-Gaussian terms (mean2D, conic, opacity, inverse depth) are reduced across the
-//    64 pixels with an 8-wide transpose-reduction, parked in LDS and issued with the batch, so no
-//    atomic sits in vmcnt ahead of the next survivor's loads;
-//  * one survivor of look-ahead: the next render record is loaded (vector loads, in-order vmcnt)
-//    while the current survivor runs.
+//    dL/dpixel (linear: sum_ch (c - accum_rec_ch) dL_ch == g - accum_dot with g = f . dL); g for a
+//    batch's 32 Gaussians x 64 pixels is ONE contraction over the channels on the matrix cores;
+//  * per (pixel, Gaussian) the serial replay keeps only what depends on the pixel's transmittance:
+//    alpha, T, the weight w = alpha T and u = G dL/dalpha, parked in two LDS tiles;
+//  * per batch, dL/dcolor = sum_px w dL is a second matrix-core contraction, and the six other
+//    per-Gaussian terms come from pixel moments of u (dL/dmean2D, dL/dconic and dL/dopacity are
+//    a, b, c, o combinations of sum u, sum u dx, sum u dy, sum u dx^2, sum u dx dy, sum u dy^2 --
+//    see the flush), with dL/dinvdepth = sum w dL/dinvdepth_px; the batch's atomics go out together.
+//
+// Both contractions run on v_mfma_f32_32x32x2_f32 (exact f32 products, f32 accumulation).
+#include <cstdlib>
+
 #include "gsr_internal.h"
 
 namespace gsr {
 
 typedef float floatx16 __attribute__((ext_vector_type(16)));
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef unsigned uint4x __attribute__((ext_vector_type(4)));
 
-constexpr int kBwdBatch = 32;      // active Gaussians per colour-gradient MFMA batch
-constexpr int kBwdPitch = 65;      // LDS row pitch (floats) of the [32][64] weight / dL tiles
-constexpr int kBwdComps = 8;      // per-Gaussian non-colour gradient terms parked per batch slot
-constexpr int kBwdLdsWave = kBwdBatch * kBwdPitch + kBwdBatch * kBwdComps;  // floats per wave
+constexpr int kBwdBatch = 32;   // survivors per batch
+constexpr int kBwdPitch = 65;   // LDS row pitch (floats) of the [32][64] w / u tiles
+constexpr int kBwdRing = 128;   // survivor ring entries per wave
+// per wave: w tile, u tile, batch records [32][8], ring (index, position), dL/dinvdepth row [64]
+constexpr int kBwdLdsWave = 2 * kBwdBatch * kBwdPitch + kBwdBatch * 8 + 2 * kBwdRing + 64;
+constexpr int kBwdQueueOffset = 32;  // words after each forward XCD counter (own cache line)
 
 // Orders this wave's LDS accesses (rocPRIM's wave_barrier): the LDS executes a wave's DS
 // instructions in order, so a lane then reads what another lane of its wave wrote before.
@@ -34,73 +44,31 @@ __device__ __forceinline__ void wave_lds_order() {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-template <int CTRL>
-__device__ __forceinline__ float dpp(float x) {
-    return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), CTRL, 0xF, 0xF, false));
+__device__ __forceinline__ bf16x8 bf8(unsigned a, unsigned b, unsigned c, unsigned d) {
+    return __builtin_bit_cast(bf16x8, (uint4x){a, b, c, d});
 }
 
-// Reduce v[8] across the 64 lanes; lane l ends holding the sum of component
-// ((l>>5)&1)*4 + ((l>>4)&1)*2 + ((l>>3)&1) (complete in every lane of its group of 8).  VALU only:
-// v_permlane32_swap / v_permlane16_swap halve across the wave halves and rows, DPP row_ror:8 across
-// the half-rows, then quad_perm and row_half_mirror finish inside each group of 8 -- no LDS
-// round trip (ds_bpermute) in the per-Gaussian chain.
-__device__ __forceinline__ float wave_transpose_reduce8(const float (&v)[8]) {
-    const int lane = threadIdx.x & 63;
-    float a[4];
-#pragma unroll
-    for (int k = 0; k < 4; k++) {  // lanes 0-31 keep component k, lanes 32-63 component k+4
-        const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(v[k]), __float_as_uint(v[k + 4]),
-                                                         false, false);
-        a[k] = __uint_as_float(sw[0]) + __uint_as_float(sw[1]);
-    }
-    float bb[2];
-#pragma unroll
-    for (int k = 0; k < 2; k++) {  // even rows keep a[k], odd rows a[k+2]
-        const auto sw = __builtin_amdgcn_permlane16_swap(__float_as_uint(a[k]), __float_as_uint(a[k + 2]),
-                                                         false, false);
-        bb[k] = __uint_as_float(sw[0]) + __uint_as_float(sw[1]);
-    }
-    const float c0 = bb[0] + dpp<0x128>(bb[0]);  // row_ror:8 = the other half-row
-    const float c1 = bb[1] + dpp<0x128>(bb[1]);
-    float c = (lane & 8) ? c1 : c0;
-    c += dpp<0xB1>(c);   // quad_perm [1,0,3,2]
-    c += dpp<0x4E>(c);   // quad_perm [2,3,0,1]
-    c += dpp<0x141>(c);  // row_half_mirror: the other quad of the group of 8
-    return c;
+// lane l's value summed with lane l^32's
+__device__ __forceinline__ float add_halves(float x) {
+    const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+    return __uint_as_float(sw[0]) + __uint_as_float(sw[1]);
 }
 
-// Work: the 8x8 strips of the non-empty tiles, in strip_list order (most survivors first), dealt to
-// per-XCD queues exactly like render_fwd (separate counters).  One wave owns a strip (lane = pixel)
-// and replays its tile's depth-sorted list back to front from the strip's largest n_contrib,
-// taking only the Gaussians whose strip bit is set in point_list (binning's exact test that the
-// Gaussian reaches alpha >= 1/255 somewhere in the strip; the others cannot be active on any of its
-// pixels).  No workgroup barriers: the LDS is wave-private.
-//
-// Survivors are processed in batches of 32 (back to front):
-//  * the list is scanned 64 entries at a time and the strip's survivors are appended to a
-//    wave-private LDS ring (slot = rank of the entry among the chunk's survivors), so batches are
-//    full whatever the survivor density;
-//  * a batch's render records and feature rows are loaded lane-distributed (lane s: survivor s)
-//    while the PREVIOUS batch is replayed, so their latency hides behind a whole batch;
-//  * g = f . dL (the colour term of dL/dalpha) for the batch's 32 Gaussians x 64 pixels is one
-//    f32 MFMA contraction over the 32 channels (16 v_mfma_f32_32x32x2_f32 per pixel half, exact
-//    f32 products), one v_permlane32_swap per register puts each pixel's 32 values in its lane;
-//  * the serial replay then needs per survivor only its record fields (v_readlane from the
-//    lane-distributed batch) and the pixel's g from a register.
-constexpr int kBwdQueueOffset = 32;  // words after each forward XCD counter (own cache line)
-constexpr int kBwdRing = 128;        // survivor ring entries per wave (LDS)
-
-template <bool EXACT, bool INVD>
+// ABL (timing ablations only, wrong gradients): 1 = no atomics, 2 = no serial replay, 3 = no
+// flush (colour MFMA, moments, atomics), 4 = no list walk beyond the ring fill (batches empty)
+template <bool EXACT, bool INVD, int ABL = 0>
 __global__ __launch_bounds__(GSR_TILE_PIX) __attribute__((amdgpu_waves_per_eu(2))) void k_render_bwd(
     Dims d, Inputs in, GeomArena g, ImageArena im, BinArena bn, Grads gr) {
-    __shared__ float lds_all[(GSR_TILE_PIX / 64) * (kBwdLdsWave + 2 * kBwdRing)];
+    __shared__ float lds_all[(GSR_TILE_PIX / 64) * kBwdLdsWave];
     if (g.ctrl[kCtrlOverflow]) return;
     const uint32_t ne = g.ctrl[kCtrlNonEmpty];
     const int lane = threadIdx.x & 63;
-    float* wl = lds_all + (threadIdx.x >> 6) * (kBwdLdsWave + 2 * kBwdRing);  // this wave's [32][65] tile
-    float* cl = wl + kBwdBatch * kBwdPitch;                    // its [32][8] term slots
-    uint32_t* ring_g = reinterpret_cast<uint32_t*>(cl + kBwdBatch * kBwdComps);  // survivor ring
+    float* wl = lds_all + (threadIdx.x >> 6) * kBwdLdsWave;  // w tile [slot][pixel]
+    float* ul = wl + kBwdBatch * kBwdPitch;                  // u tile [slot][pixel]
+    float4* rl = reinterpret_cast<float4*>(ul + kBwdBatch * kBwdPitch);  // records [slot][2]
+    uint32_t* ring_g = reinterpret_cast<uint32_t*>(rl + 2 * kBwdBatch);
     uint32_t* ring_p = ring_g + kBwdRing;
+    float* dli_row = reinterpret_cast<float*>(ring_p + kBwdRing);  // dL/dinvdepth per strip pixel
     const int hi = lane >> 5, l32 = lane & 31;
     uint32_t q = __builtin_amdgcn_s_getreg((3 << 11) | 20) & 7u;  // HW_REG_XCC_ID
     uint32_t q_left = 8;
@@ -148,28 +116,33 @@ __global__ __launch_bounds__(GSR_TILE_PIX) __attribute__((amdgpu_waves_per_eu(2)
         for (int off = 32; off > 0; off >>= 1) ns = max(ns, (uint32_t)__shfl_xor(ns, off));
         ns = __builtin_amdgcn_readfirstlane(ns);
         if (ns == 0) continue;
-        float dL[GSR_C];
-        const float* bg = in.bg + in.s_bg * b;
+
+        // ---- per-strip operands
         float bg_dot = 0.f;
+        float dL[GSR_C];
+        {
+            const float* bg = in.bg + in.s_bg * b;
 #pragma unroll
-        for (int ch = 0; ch < GSR_C; ch++) {
-            dL[ch] = inside ? gr.dL_dpix[(b * GSR_C + ch) * HW + (pix - b * HW)] : 0.f;
-            bg_dot += bg[ch] * dL[ch];
+            for (int ch = 0; ch < GSR_C; ch++) {
+                dL[ch] = inside ? gr.dL_dpix[(b * GSR_C + ch) * HW + (pix - b * HW)] : 0.f;
+                bg_dot += bg[ch] * dL[ch];
+            }
         }
         const float dL_inv = (INVD && inside) ? gr.dL_dinvdepth[pix] : 0.f;
-
-        // colour-gradient MFMA A operands: step j covers strip pixels 2j, 2j+1; lane l holds
-        // dL[pixel 2j + (l>>5)][channel l&31].  Transposed through the LDS tile.
+        // colour contraction A operands: step j covers strip pixels 2j, 2j+1; lane l holds
+        // dL[pixel 2j + (l>>5)][channel l&31].  Transposed through the w tile (free until the first
+        // batch).
         float adl[kBwdBatch];
         wave_lds_order();
 #pragma unroll
         for (int ch = 0; ch < GSR_C; ch++) wl[ch * kBwdPitch + lane] = dL[ch];
+        if (INVD) dli_row[lane] = dL_inv;
         wave_lds_order();
 #pragma unroll
         for (int j = 0; j < kBwdBatch; j++) adl[j] = wl[l32 * kBwdPitch + 2 * j + hi];
         wave_lds_order();
-        // g = f . dL MFMA B operands: k-step k of pixel half h, lane l: dL[channel 16(l>>5) + k]
-        // [pixel 32h + (l&31)] -- one swap per k turns (dL[k], dL[16+k]) into the two halves' operands
+        // g = f . dL contraction B operands: k-step k of pixel half h, lane l: dL[channel 16(l>>5) + k]
+        // [pixel 32h + (l&31)] -- one swap per k turns (dL[k], dL[16+k]) into both halves' operands
         float bh0[16], bh1[16];
 #pragma unroll
         for (int k = 0; k < 16; k++) {
@@ -204,12 +177,10 @@ __global__ __launch_bounds__(GSR_TILE_PIX) __attribute__((amdgpu_waves_per_eu(2)
             }
             wave_lds_order();
         };
-        // a batch, lane-distributed: lane l holds survivor l&31's index / position, its render
-        // record (both halves) and 16 channels 16(l>>5).. of its feature row
-        uint32_t nb = 0, bg_ = 0, bp_ = 0;
-        float4 ra_ = make_float4(0.f, 0.f, 0.f, 0.f), rc_ = ra_;
-        float fr[16];
-        auto pop = [&](uint32_t& nb_o, uint32_t& g_o, uint32_t& p_o, float4& ra_o, float4& rc_o, float (&f_o)[16]) {
+        // a batch, lane-distributed: lane l holds survivor l&31's index and list position, its
+        // render record and its feature channels 16h .. 16h + 15 (h = lane half)
+        auto pop = [&](uint32_t& nb_o, uint32_t& g_o, uint32_t& p_o, float4& ra_o, float4& rc_o,
+                       float (&f_o)[16]) {
             nb_o = min(tail - head, (uint32_t)kBwdBatch);
             const uint32_t slot = (head + (uint32_t)l32) & (kBwdRing - 1);
             const bool valid = (uint32_t)l32 < nb_o;
@@ -232,13 +203,24 @@ __global__ __launch_bounds__(GSR_TILE_PIX) __attribute__((amdgpu_waves_per_eu(2)
                 for (int u = 0; u < 16; u++) f_o[u] = 0.f;
             }
         };
+        uint32_t nb, bg_, bp_;
+        float4 ra_, rc_;
+        float fr[16];
         fill(kBwdBatch);
         pop(nb, bg_, bp_, ra_, rc_, fr);
 
+        // strip-centred pixel offsets (exact in f32): the moments use lx = x - cx, ly = y - cy
+        const float cx = (float)sx0 + 3.5f, cy = (float)sy0 + 3.5f;
         float T = T_final;
         float accum_dot = 0.f, last_gdot = 0.f, last_alpha = 0.f;
         float accum_inv = 0.f, last_inv = 0.f;
         while (nb) {
+            // this batch's records to LDS (read back as wave-uniform values per slot), the list
+            // position in the record's spare word
+            if (lane < kBwdBatch) {
+                rl[2 * lane] = ra_;
+                rl[2 * lane + 1] = make_float4(rc_.x, rc_.y, rc_.z, __uint_as_float(bp_));
+            }
             // next batch: survivors into the ring, then its loads in flight during this batch
             uint32_t nb_n, bg_n, bp_n;
             float4 ra_n, rc_n;
@@ -246,7 +228,7 @@ __global__ __launch_bounds__(GSR_TILE_PIX) __attribute__((amdgpu_waves_per_eu(2)
             fill(kBwdBatch);
             pop(nb_n, bg_n, bp_n, ra_n, rc_n, fr_n);
 
-            // g[s][px] = sum_ch f_s[ch] dL[ch][px] for the batch (rows s, columns px of each half)
+            // g[s][px] = sum_ch f_s[ch] dL[ch][px]: f32 MFMA, A = f (row s), B = dL (column px)
             floatx16 gd0, gd1;
 #pragma unroll
             for (int r = 0; r < 16; r++) { gd0[r] = 0.f; gd1[r] = 0.f; }
@@ -263,27 +245,21 @@ __global__ __launch_bounds__(GSR_TILE_PIX) __attribute__((amdgpu_waves_per_eu(2)
                 gd0[r] = __uint_as_float(sw[0]);
                 gd1[r] = __uint_as_float(sw[1]);
             }
+            wave_lds_order();
 
-            // serial replay of the batch, slot by slot (static slots: g lives in registers)
+            // ---- serial replay of the batch, slot by slot (static slots: g lives in registers)
+            uint32_t amask = 0;  // slots with an active pixel (the others add nothing)
 #pragma unroll
             for (int s = 0; s < kBwdBatch; s++) {
-                if ((uint32_t)s >= nb) continue;  // (not break: the loop must unroll -- static slots)
+                if ((uint32_t)s >= nb || ABL == 2) continue;  // (not break: the loop must unroll -- static slots)
                 const float gdot = (s & 4) ? gd1[(s & 3) + 4 * (s >> 3)] : gd0[(s & 3) + 4 * (s >> 3)];
-                const uint32_t contributor = __builtin_amdgcn_readlane(bp_, s);
-                // record: x, y, opacity, 1/depth | -a/2, -b, -c/2
-                const float rx = __uint_as_float(__builtin_amdgcn_readlane(__float_as_uint(ra_.x), s));
-                const float ry = __uint_as_float(__builtin_amdgcn_readlane(__float_as_uint(ra_.y), s));
-                const float ro = __uint_as_float(__builtin_amdgcn_readlane(__float_as_uint(ra_.z), s));
-                const float rinv = __uint_as_float(__builtin_amdgcn_readlane(__float_as_uint(ra_.w), s));
-                const float qa = __uint_as_float(__builtin_amdgcn_readlane(__float_as_uint(rc_.x), s));
-                const float qb = __uint_as_float(__builtin_amdgcn_readlane(__float_as_uint(rc_.y), s));
-                const float qc = __uint_as_float(__builtin_amdgcn_readlane(__float_as_uint(rc_.z), s));
-                const float dx = rx - pfx, dy = ry - pfy;
-                // branch-free: every lane evaluates, `act` selects (the divergent form costs exec
-                // juggling around every step and saves nothing -- both sides run anyway)
-                const float power = blend_power(qa, qb, qc, dx, dy);
+                const float4 ra = rl[2 * s], rc = rl[2 * s + 1];  // x, y, opacity, 1/depth | -a/2, -b, -c/2, pos
+                const uint32_t contributor = __float_as_uint(rc.w);
+                const float dx = ra.x - pfx, dy = ra.y - pfy;
+                // branch-free: every lane evaluates, `act` selects
+                const float power = blend_power(rc.x, rc.y, rc.z, dx, dy);
                 const float G = blend_exp<EXACT>(power);
-                const float alpha = fminf(0.99f, ro * G);
+                const float alpha = fminf(0.99f, ra.z * G);
                 const bool act = inside && contributor < last_contributor && !(power > 0.0f) &&
                                  !(alpha < 1.0f / 255.0f);
                 const float one_m = 1.f - alpha;
@@ -297,77 +273,121 @@ __global__ __launch_bounds__(GSR_TILE_PIX) __attribute__((amdgpu_waves_per_eu(2)
                 accum_dot = act ? acc_n : accum_dot;
                 last_gdot = act ? gdot : last_gdot;
                 float dL_dalpha = gdot - accum_dot;
-                float v[8];
-                v[7] = 0.f;
-                v[6] = 0.f;
                 if (INVD) {
                     const float ai_n = last_alpha * last_inv + (1.f - last_alpha) * accum_inv;
                     accum_inv = act ? ai_n : accum_inv;
-                    last_inv = act ? rinv : last_inv;
-                    dL_dalpha += (rinv - accum_inv) * dL_inv;
-                    v[6] = wgt * dL_inv;
+                    last_inv = act ? ra.w : last_inv;
+                    dL_dalpha += (ra.w - accum_inv) * dL_inv;
                 }
                 dL_dalpha *= T;
                 last_alpha = act ? alpha : last_alpha;
                 dL_dalpha += (-T_final * rinv1m) * bg_dot;
-                dL_dalpha = act ? dL_dalpha : 0.f;
-                {
-                    const float Ga = act ? G : 0.f;  // inactive lanes: every term exactly 0 (G may be inf)
-                    const float ca = -2.0f * qa, cb = -qb, cc = -2.0f * qc;  // exact
-                    const float dL_dG = ro * dL_dalpha;
-                    const float gdx = Ga * dx;
-                    const float gdy = Ga * dy;
-                    const float dG_ddelx = -gdx * ca - gdy * cb;
-                    const float dG_ddely = -gdy * cc - gdx * cb;
-                    v[0] = dL_dG * dG_ddelx * ddelx_dx;
-                    v[1] = dL_dG * dG_ddely * ddely_dy;
-                    v[2] = -0.5f * gdx * dx * dL_dG;
-                    v[3] = -0.5f * gdx * dy * dL_dG;
-                    v[4] = -0.5f * gdy * dy * dL_dG;
-                    v[5] = Ga * dL_dalpha;
-                }
-                // weights and the 7 reduced terms parked in LDS; the atomics go out with the batch
+                // u = G dL/dalpha (0 where the pixel does not take the Gaussian; G may be inf there)
+                const float u = act ? G * dL_dalpha : 0.f;
+                amask |= __any(act) ? (1u << s) : 0u;
                 wl[s * kBwdPitch + lane] = wgt;
-                float r = 0.f;
-                if (__any(act)) r = wave_transpose_reduce8(v);
-                if ((lane & 7) == 0)
-                    cl[s * kBwdComps + ((lane >> 5) & 1) * 4 + ((lane >> 4) & 1) * 2 + ((lane >> 3) & 1)] = r;
+                ul[s * kBwdPitch + lane] = u;
+                __builtin_amdgcn_sched_barrier(0);  // slot by slot: no register build-up across slots
             }
-
-            // ---- flush: dL/dcolor = sum_px w dL on the matrix cores, then the batch's atomics
             wave_lds_order();
+
+            // ---- flush: dL/dcolor[s][ch] = sum_px w[s][px] dL[px][ch] on the matrix cores (slot rows,
+            // channel columns: each register's atomics cover two whole 128-byte feature rows)
+            if (ABL == 3) { nb = nb_n; bg_ = bg_n; bp_ = bp_n; ra_ = ra_n; rc_ = rc_n;
+#pragma unroll
+                for (int u = 0; u < 16; u++) fr[u] = fr_n[u] + gd0[u] + gd1[u];
+                continue; }
             floatx16 acc;
 #pragma unroll
             for (int r = 0; r < 16; r++) acc[r] = 0.f;
 #pragma unroll
             for (int j = 0; j < kBwdBatch; j++) {
-                const float w = (uint32_t)l32 < nb ? wl[l32 * kBwdPitch + 2 * j + hi] : 0.f;
-                acc = __builtin_amdgcn_mfma_f32_32x32x2f32(adl[j], w, acc, 0, 0, 0);
+                const float w = wl[l32 * kBwdPitch + 2 * j + hi];
+                acc = __builtin_amdgcn_mfma_f32_32x32x2f32(w, adl[j], acc, 0, 0, 0);
             }
+            // pixel moments of u for slot l&31 over this lane half's 32 pixels (strip rows 4h..4h+3):
+            // lx = (i % 8) - 3.5, ly = (i / 8) - 3.5 + 4h
+            float S0 = 0.f, Sx = 0.f, Sy = 0.f, Sxx = 0.f, Sxy = 0.f, Syy = 0.f, Si = 0.f;
+#pragma unroll 1
+            for (int row = 0; row < 4; row++) {  // one strip row (8 pixels) at a time
+                const float ly = (float)row - 3.5f;
+                const float* urow = ul + l32 * kBwdPitch + 32 * hi + 8 * row;
+                const float* wrow = wl + l32 * kBwdPitch + 32 * hi + 8 * row;
+                float r0 = 0.f, rx = 0.f, rxx = 0.f, ri = 0.f;
+#pragma unroll
+                for (int c = 0; c < 8; c++) {
+                    const float lx = (float)c - 3.5f;
+                    const float uu = urow[c];
+                    r0 += uu;
+                    rx = fmaf(uu, lx, rx);
+                    rxx = fmaf(uu, lx * lx, rxx);
+                    if (INVD) ri = fmaf(wrow[c], dli_row[32 * hi + 8 * row + c], ri);
+                }
+                S0 += r0;
+                Sx += rx;
+                Sxx += rxx;
+                Sy = fmaf(r0, ly, Sy);
+                Sxy = fmaf(rx, ly, Sxy);
+                Syy = fmaf(r0, ly * ly, Syy);
+                Si += ri;
+            }
+            if (hi) {  // rows 4..7: ly = ly_i + 4
+                Syy = fmaf(8.f, Sy, fmaf(16.f, S0, Syy));
+                Sxy = fmaf(4.f, Sx, Sxy);
+                Sy = fmaf(4.f, S0, Sy);
+            }
+            S0 = add_halves(S0); Sx = add_halves(Sx); Sy = add_halves(Sy);
+            Sxx = add_halves(Sxx); Sxy = add_halves(Sxy); Syy = add_halves(Syy);
+            if (INVD) Si = add_halves(Si);
             wave_lds_order();
-            // acc[r] at lane l: channel (r&3) + 8(r>>2) + 4(l>>5) of the batch's Gaussian l&31
-            if ((uint32_t)l32 < nb) {
-                const int64_t gg = gbase + bg_;
-                float* dst = gr.dL_dcolors + gg * GSR_C + 4 * hi;
+            // acc[r] at lane l: channel l&31 of the batch's slot (r&3) + 8(r>>2) + 4(l>>5)
+            if (ABL != 1) {
 #pragma unroll
                 for (int r = 0; r < 16; r++) {
-                    const float val = acc[r];
-                    if (val != 0.f) atomicAdd(dst + (r & 3) + 8 * (r >> 2), val);
+                    const uint32_t sl = (uint32_t)((r & 3) + 8 * (r >> 2) + 4 * hi);
+                    const uint32_t gsl = __builtin_amdgcn_readlane(bg_, (r & 3) + 8 * (r >> 2)) ;
+                    const uint32_t gsh = __builtin_amdgcn_readlane(bg_, (r & 3) + 8 * (r >> 2) + 4);
+                    const uint32_t gs = hi ? gsh : gsl;
+                    if ((amask >> sl) & 1u) atomicAdd(gr.dL_dcolors + (gbase + gs) * GSR_C + l32, acc[r]);
                 }
-                // the parked terms: lane l takes terms 4(l>>5) .. +3 of slot l&31
+            }
+            // the other terms of slot l&31, from the pixel moments of u about the Gaussian's centre
+            // (dx = X - lx, dy = Y - ly); lanes 0-31 write the slot's kGtWords row to LDS (the record
+            // tile is free now), then 8 lanes per slot add it to the slot's gterm row
+            {
+                const float X = ra_.x - cx, Y = ra_.y - cy;
+                const float Sdx = X * S0 - Sx;
+                const float Sdy = Y * S0 - Sy;
+                const float Sdxx = (X * X) * S0 - 2.f * X * Sx + Sxx;
+                const float Sdxy = (X * Y) * S0 - X * Sy - Y * Sx + Sxy;
+                const float Sdyy = (Y * Y) * S0 - 2.f * Y * Sy + Syy;
+                const float o = ra_.z;
+                const float ca = -2.0f * rc_.x, cb = -rc_.y, cc = -2.0f * rc_.z;  // conic a, b, c (exact)
+                float* row = reinterpret_cast<float*>(rl) + 8 * l32;
+                if (!hi) {
+                    // dL/dmean2D = sum dL/dG dG/ddelx ddelx/dx, dG/ddelx = -G (a dx + b dy)
+                    // (backward.cu:597-627); dL/dconic = -1/2 o sum u (dx^2, dx dy, dy^2)
+                    row[kGtM2x] = -o * ddelx_dx * (ca * Sdx + cb * Sdy);
+                    row[kGtM2y] = -o * ddely_dy * (cc * Sdy + cb * Sdx);
+                    row[kGtCx] = -0.5f * o * Sdxx;
+                    row[kGtCy] = -0.5f * o * Sdxy;
+                } else {
+                    row[kGtCw] = -0.5f * o * Sdyy;
+                    row[kGtOp] = S0;  // dL/dopacity = sum G dL/dalpha
+                    row[kGtInv] = Si;
+                    row[7] = 0.f;
+                }
+            }
+            wave_lds_order();
+            if (ABL != 1) {
+                const float* rows = reinterpret_cast<const float*>(rl);
 #pragma unroll
-                for (int u = 0; u < 4; u++) {
-                    const int comp = 4 * hi + u;
-                    const float val = cl[l32 * kBwdComps + comp];
-                    float* dc = nullptr;
-                    if (comp == 0) dc = gr.dL_dmean2D + gg * 3;
-                    else if (comp == 1) dc = gr.dL_dmean2D + gg * 3 + 1;
-                    else if (comp == 2) dc = gr.dL_dconic + gg * 4;
-                    else if (comp == 3) dc = gr.dL_dconic + gg * 4 + 1;
-                    else if (comp == 4) dc = gr.dL_dconic + gg * 4 + 3;
-                    else if (comp == 5) dc = gr.dL_dopacity + gg;
-                    else if (comp == 6 && INVD) dc = gr.dL_dinvdepth_g + gg;
-                    if (dc && val != 0.f) atomicAdd(dc, val);
+                for (int qq = 0; qq < 4; qq++) {
+                    const uint32_t sl = (uint32_t)(8 * qq + (lane >> 3));
+                    const uint32_t gs = (uint32_t)__shfl((int)bg_, (int)sl);
+                    const float val = rows[8 * sl + (lane & 7)];
+                    if (((amask >> sl) & 1u) && (lane & 7) != 7 && (INVD || (lane & 7) != kGtInv))
+                        atomicAdd(g.gterm + (gbase + gs) * kGtWords + (lane & 7), val);
                 }
             }
             wave_lds_order();
@@ -388,8 +408,16 @@ void launch_render_bwd(const Dims& d, const Inputs& in, const GeomArena& g, cons
     const int nwaves = d.B * d.T * kStrips;  // upper bound of the work items
     if (nwaves == 0) return;
     hipLaunchKernelGGL(k_zero_bwd_queues, dim3(1), dim3(64), 0, s, g.ctrl);
+    hipMemsetAsync(g.gterm, 0, (size_t)d.B * d.P * kGtWords * sizeof(float), s);
     const bool invd = gr.dL_dinvdepth != nullptr && gr.dL_dinvdepth_g != nullptr;
     const dim3 grid(min((nwaves + 3) / 4, persistent_grid(2))), blk(GSR_TILE_PIX);
+    static const int ablate = [] { const char* e = getenv("GSR_BWD_ABLATE"); return e ? atoi(e) : 0; }();
+    if (ablate >= 1 && ablate <= 3 && exact && invd) {
+        if (ablate == 1) hipLaunchKernelGGL((k_render_bwd<true, true, 1>), grid, blk, 0, s, d, in, g, im, b, gr);
+        if (ablate == 2) hipLaunchKernelGGL((k_render_bwd<true, true, 2>), grid, blk, 0, s, d, in, g, im, b, gr);
+        if (ablate == 3) hipLaunchKernelGGL((k_render_bwd<true, true, 3>), grid, blk, 0, s, d, in, g, im, b, gr);
+        return;
+    }
     if (exact) {
         if (invd) hipLaunchKernelGGL((k_render_bwd<true, true>), grid, blk, 0, s, d, in, g, im, b, gr);
         else hipLaunchKernelGGL((k_render_bwd<true, false>), grid, blk, 0, s, d, in, g, im, b, gr);

@@ -49,11 +49,11 @@ class SplatTrainer:
         self.dinv = torch.zeros((B, H, W), dtype=torch.float32, device=self.dev)  # materialised, as autograd does
 
     def _grow(self, err):
-        """An earlier step overflowed (and was skipped on the device): double the workspace."""
+        """An earlier step overflowed (and was skipped on the device): grow the workspace to 1.5x the
+        instance count that step needed (at least double)."""
         self.skipped_steps += 1
         old = self.rast
-        need = max(old.max_instances_seen(), old.R_capacity)
-        cap = int(need * 1.5) + 1024
+        cap = max(int(old.max_instances_seen() * 1.5), 2 * old.R_capacity) + 1024
         warnings.warn(f"SplatTrainer: {err}; step skipped, R capacity {old.R_capacity} -> {cap}")
         self.rast = BatchRasterizer(old.B, old.P, old.W, old.H, R_capacity=cap, device=self.dev)
         del old
