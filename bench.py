@@ -38,13 +38,14 @@ C = 32
 def _args():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--steps", type=int, default=400)
+    ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--batch", type=int, default=32, help="frames per step per GPU")
     ap.add_argument("--config", default="c2", choices=["c2", "c5"])
-    ap.add_argument("--pipeline", default="avatar", choices=["avatar", "raster", "train"],
+    ap.add_argument("--pipeline", default="avatar", choices=["avatar", "raster", "train", "frame"],
                     help="train = BASELINE config 4: raster fwd + fused-SSIM/L1 loss + raster bwd + "
-                         "gradient all-reduce + Adam (use --batch 6)")
+                         "gradient all-reduce + Adam (use --batch 6); frame = GUAVA's unchanged caller: "
+                         "one GaussianRasterizer_32 call per frame as gaussian_render.py:37-67 does")
     ap.add_argument("--inflight", type=int, default=1,
                     help="batches in flight on separate HIP streams (avatar/raster pipelines): the deform "
                          "and binning of one batch overlap the compositing of the other (2: +7%% frames/s, "
@@ -73,6 +74,13 @@ def _render_alg_bytes(P_vis, W, H):
     # means2D (8) + conic/opacity (16) + 1/depth (4); per pixel 32 channels + inverse depth out
     # (132 B) + final_T + n_contrib (8 B) kept for backward.
     return 156.0 * P_vis + 140.0 * W * H
+
+
+def _render_bwd_alg_bytes(P_vis, W, H):
+    # render_bwd compulsory traffic per frame: per pixel dL/dpixel (32 channels) + dL/dinvdepth read
+    # (132 B) + final_T + n_contrib (8 B); per visible Gaussian its render record (32 B) and 32
+    # features (128 B) read, its colour gradient (128 B) and 7 screen-space terms (28 B) written.
+    return 316.0 * P_vis + 140.0 * W * H
 
 
 def _path_alg_bytes(P, W, H):
@@ -158,7 +166,8 @@ def main():
     tanf = t(np.array([[c["tanfovx"], c["tanfovy"]] for c in cams], np.float32))
     bgs = torch.zeros((B, C), dtype=torch.float32, device=dev)
     avatar_inputs = None
-    workload = wl["name"] + {"avatar": "-deform+raster", "raster": "-raster", "train": "-train"}[a.pipeline]
+    workload = wl["name"] + {"avatar": "-deform+raster", "raster": "-raster", "train": "-train",
+                             "frame": "-per-frame-dropin"}[a.pipeline]
 
     if a.pipeline == "avatar":
         from guava_renderer_amd import avatar
@@ -208,8 +217,10 @@ def main():
         assert not ovf, "probe overflow"
         del probe
         torch.cuda.empty_cache()
-        # headroom for the attributes drifting under the optimizer
-        trainer = SplatTrainer(params, B, W, H, R_capacity=int(R_probe * 1.5) + 1024, device=dev)
+        # the trainable parameters are the raw attributes: a small learning rate
+        # keeps the per-step work at the avatar's distribution over the timed steps; capacity with
+        # headroom for the drift (an overflowing step is skipped on the device and counted)
+        trainer = SplatTrainer(params, B, W, H, R_capacity=int(R_probe * 2) + 1024, device=dev, lr=1e-5)
         rast = trainer.rast
         target = torch.rand((B, 3, H, W), device=dev, generator=torch.Generator(device=dev).manual_seed(rank))
 
@@ -217,6 +228,61 @@ def main():
 
         def step_on(i):
             return trainer.step(views, projs, tanf, target)
+    elif a.pipeline == "frame":
+        # GUAVA's unchanged caller (models/UbodyAvatar/gaussian_render.py:19-67, the refiner aside):
+        # one GaussianRasterizationSettings + GaussianRasterizer_32 call per frame, camera fields
+        # read per frame with int()/float() from device tensors, outputs stacked.  The deformed
+        # assets of the B frames come from the deform kernels, outside the timed region.
+        from diff_gaussian_rasterization_32 import GaussianRasterizationSettings, GaussianRasterizer_32
+        from guava_renderer_amd import avatar
+        from guava_renderer_amd.pipeline import AvatarPipeline
+        body, flame, extra = avatar.ehm_assets(seed=0)
+        verts, faces, tex = avatar.template_mesh()
+        g = avatar.gaussians(verts, faces, tex, P=P, seed=0)
+        bp_all, fp_all = avatar.ehm_params(B * world, seed=1000)
+        lo, hi = parallel.shard_range(B * world, rank, world)
+        bpt = {k: t(v[lo:hi]) for k, v in bp_all.items()}
+        fpt = {k: t(v[lo:hi]) for k, v in fp_all.items()}
+        dpipe = AvatarPipeline(body, flame, extra, g, B, W, H, R_capacity=24 * P * B, device=dev)
+        dg = dpipe.deform(bpt, fpt)
+        P = dpipe.P
+        assets = {"xyz": dg["xyz"], "rotation": dg["rotation"], "scaling": dg["scaling"],
+                  "opacity": dpipe.gauss.opacity.unsqueeze(0).expand(B, -1, -1),
+                  "features_color": dpipe.gauss.colors.unsqueeze(0).expand(B, -1, -1)}
+        cam_params = {"image_height": torch.full((B,), H, device=dev), "image_width": torch.full((B,), W, device=dev),
+                      "tanfovx": tanf[:, 0].contiguous(), "tanfovy": tanf[:, 1].contiguous(),
+                      "world_view_transform": views.view(B, 4, 4), "full_proj_transform": projs.view(B, 4, 4),
+                      "camera_center": t(np.stack([c["campos"] for c in cams]))}
+        scene = {"colors": g["colors"], "opacities": g["opacities"]}
+        avatar_inputs = (body, flame, extra, g, {k: v[lo:hi] for k, v in bp_all.items()},
+                         {k: v[lo:hi] for k, v in fp_all.items()})
+        rasts = []
+        last_radii = [None]
+
+        def step_on(i):
+            with torch.no_grad():
+                mean_3d = assets["xyz"]
+                features_color = assets["features_color"].clone()
+                mean_2d = torch.zeros_like(mean_3d, dtype=torch.float32, requires_grad=True, device=dev)
+                bg = torch.ones((B, features_color.shape[-1]), dtype=torch.float32, device=dev) * 0.0
+                imgs, radiis, depths = [], [], []
+                for bi in range(B):
+                    rs = GaussianRasterizationSettings(
+                        image_height=int(cam_params["image_height"][bi]), image_width=int(cam_params["image_width"][bi]),
+                        tanfovx=float(cam_params["tanfovx"][bi]), tanfovy=float(cam_params["tanfovy"][bi]),
+                        bg=bg[bi], scale_modifier=1.0, viewmatrix=cam_params["world_view_transform"][bi],
+                        projmatrix=cam_params["full_proj_transform"][bi], sh_degree=0,
+                        campos=cam_params["camera_center"][bi], prefiltered=False, debug=False, antialiasing=False)
+                    img, rad, dep = GaussianRasterizer_32(raster_settings=rs)(
+                        means3D=mean_3d[bi], means2D=mean_2d[bi], shs=None, colors_precomp=features_color[bi],
+                        opacities=assets["opacity"][bi], scales=assets["scaling"][bi],
+                        rotations=assets["rotation"][bi], cov3D_precomp=None)
+                    imgs.append(img)
+                    radiis.append(rad)
+                    depths.append(dep)
+                out = torch.stack(imgs, 0)
+                last_radii[0] = torch.stack(radiis, 0)
+                return out, torch.stack(depths, 0), last_radii[0]
     else:
         scene = scenes.avatar_cloud(P, seed=0, gaussians_per_texel=wl["gpt"])
         P = scene["means3D"].shape[0]
@@ -238,25 +304,36 @@ def main():
 
     # batches in flight: step k runs on stream k mod n with its own pipeline / workspace (each
     # batch is complete work -- deform, binning, compositing; only consecutive batches overlap)
-    n_inflight = len(rasts)
+    n_inflight = max(1, len(rasts))
     streams = [torch.cuda.current_stream(dev)] + [torch.cuda.Stream(dev) for _ in range(n_inflight - 1)]
     step_count = [0]
+
+    gather = dist is not None and a.pipeline != "train"
 
     def step():
         i = step_count[0] % n_inflight
         step_count[0] += 1
         with torch.cuda.stream(streams[i]):
-            return step_on(i)
+            res = step_on(i)
+            if gather:  # consumer boundary: every rank receives all ranks' RGB frames (RCCL all-gather)
+                rgb = res[0][:, :3]
+                parallel.gather_frames(rgb if backend == "nccl" else rgb.cpu(), B * world)
+            return res
 
     for _ in range(a.warmup):
         step()
     torch.cuda.synchronize(dev)
-    R_total, ovf = rast.status()
-    assert not any(r.status()[1] for r in rasts)
-    P_vis = int((rast.radii > 0).sum().item())
+    if rasts:
+        R_total, ovf = rast.status()
+        assert not any(r.status()[1] for r in rasts)
+        P_vis = int((rast.radii > 0).sum().item())
+    else:  # per-frame drop-in path: the _C calls size their own buffers (exact R, host sync)
+        R_total = None
+        P_vis = int((last_radii[0] > 0).sum().item())
     profile_read()  # reset accumulators
     profile_enable(("preprocess", "scan", "depth_sort", "chunk_count", "tile_scan", "ordered_scatter",
-                    "render_fwd", "render_bwd", "preprocess_bwd") if a.stages else ("render_fwd",))
+                    "render_fwd", "render_bwd", "preprocess_bwd") if a.stages else
+                   ("render_fwd", "render_bwd") if a.pipeline == "train" else ("render_fwd",))
     if dist is not None:
         dist.barrier()
     torch.cuda.synchronize(dev)
@@ -280,7 +357,10 @@ def main():
         deform_ms = e0.elapsed_time(e1) / a.steps
     # work counters of one extra (instrumented, untimed) step: which wall the render kernel hits
     work = render_counters(step, device=dev)
-    assert not any(r.status()[1] for r in rasts), "capacity overflow inside the timed region"
+    if a.pipeline == "train":
+        assert trainer.skipped_steps == 0 and not trainer.rast.status()[1], "capacity overflow inside the timed region"
+    else:
+        assert not any(r.status()[1] for r in rasts), "capacity overflow inside the timed region"
     if dist is not None:
         tt = torch.tensor([el], dtype=torch.float64, device=dev if backend == "nccl" else "cpu")
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
@@ -291,7 +371,8 @@ def main():
     ms_step = 1000.0 * el / a.steps
     rms, rcnt = prof.get("render_fwd", (0.0, 0))
     render_ms = rms / max(rcnt, 1)
-    bytes_launch = _render_alg_bytes(P_vis / B, W, H) * B
+    frames_per_launch = 1 if a.pipeline == "frame" else B
+    bytes_launch = _render_alg_bytes(P_vis / B, W, H) * frames_per_launch
     achieved = bytes_launch / (render_ms * 1e-3) / 1e9 if render_ms > 0 else None
     traffic = None
     pmc_path = os.path.join(ROOT, "profiles", "pmc_render_fwd.json")
@@ -317,7 +398,7 @@ def main():
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
-        "dtype": "f32",
+        "dtype": "f32" if a.exact_accum else "f32 (colour products in split-bf16: f = f_hi + f_lo, f32 accumulation)",
         "data": ("synthetic avatar (SMPL-X template mesh + UV-texel Gaussians, synthetic LBS bases, "
                  "GUAVA attribute distributions), one pose + one orbit camera per frame"
                  if a.pipeline == "avatar" else
@@ -326,10 +407,12 @@ def main():
         "config": {"workload": workload,
                    "pipeline": {"avatar": "EHM LBS -> Gaussian assembly -> rasterize",
                                 "raster": "rasterize",
-                                "train": "raster fwd -> L1 + fused SSIM -> raster bwd -> grad all-reduce -> Adam"
+                                "train": "raster fwd -> L1 + fused SSIM -> raster bwd -> grad all-reduce -> Adam",
+                                "frame": "deformed frames -> GaussianRasterizer_32 once per frame (gaussian_render.py:37-67)"
                                 }[a.pipeline] + (" + fused refiner conv_body_first" if a.refine else ""), "gaussians": P, "image": [W, H], "channels": C,
                    "frames_per_step_per_gpu": B, "global_batch": B * world,
-                   "parallelism": f"frame-sharded x{world}", "batches_in_flight": n_inflight,
+                   "parallelism": f"frame-sharded x{world}" + (", RGB all-gather per step" if world > 1 and a.pipeline != "train" else ""),
+                   "batches_in_flight": n_inflight,
                    "exp": "hw" if a.fast_exp else "exact-poly",
                    "colour_accum": "f32 mfma (bit-exact)" if a.exact_accum else "split-bf16 mfma (<=1e-4)",
                    "instances_per_step": R_total, "visible_gaussians_per_frame": P_vis / B},
@@ -354,6 +437,18 @@ def main():
                           "peak_tflops": F32_MFMA_PEAK_TFLOPS if a.exact_accum else BF16_MFMA_PEAK_TFLOPS,
                           "instruction": "v_mfma_f32_32x32x2_f32" if a.exact_accum else "v_mfma_f32_32x32x16_bf16",
                           "useful_frac": round(work["pairs_contributing"] / max(64 * work["strip_pairs_blended"], 1), 4)}
+    if a.pipeline == "train":
+        bms, bcnt = prof.get("render_bwd", (0.0, 0))
+        bwd_ms = bms / max(bcnt, 1)
+        bwd_bytes = _render_bwd_alg_bytes(P_vis / B, W, H) * B
+        bwd_ach = bwd_bytes / (bwd_ms * 1e-3) / 1e9 if bwd_ms > 0 else None
+        out["roofline_bwd"] = {"bound": "hbm", "kernel": "render_bwd",
+                               "achieved": round(bwd_ach, 1) if bwd_ach else None, "peak": HBM_PEAK_GBS,
+                               "unit": "GB/s", "frac": round(bwd_ach / HBM_PEAK_GBS, 4) if bwd_ach else None,
+                               "traffic": None, "alg_bytes_per_launch": bwd_bytes,
+                               "avg_launch_ms": round(bwd_ms, 4), "us_per_frame": round(1000 * bwd_ms / B, 2)}
+    if a.pipeline == "frame":
+        out["latency_ms_per_frame"] = round(1000.0 * el / (a.steps * B), 4)
     if deform_ms is not None:
         out["deform_ms_per_step"] = round(deform_ms, 4)
     if a.stages:

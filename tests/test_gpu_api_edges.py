@@ -1,0 +1,139 @@
+"""Edge cases of the drop-in API on the GPU.
+
+* markVisible (rasterize_points.cu:225-244, rasterizer_impl.cu:54-66,141-153): `_C.mark_visible` and
+  `GaussianRasterizer_32.markVisible` bit-exact with the oracle (view-space z > 0.2), including
+  points behind the camera and on the near plane.
+* A frame where every Gaussian is culled (P > 0, R = 0): the output is exactly the background
+  (the drop-in path allocates out_color with torch.empty, so every pixel must be written), radii
+  and inverse depth 0 -- through `_C` and through the batched entry.
+* Batched inputs with stride-0 frames (deform.py's expanded features_color / opacity) or
+  non-contiguous rows render exactly like contiguous copies.
+* The refiner head's prepared-feature cache follows tensor identity, not the address.
+"""
+import numpy as np
+import pytest
+import torch
+
+from helpers import make_scene, torch_inputs
+
+pytestmark = pytest.mark.gpu
+DEV = torch.device("cuda:0")
+
+
+def _world_z_for_view_z(d, m, zv):
+    """World z that puts points (x, y from m) at view-space depth zv (row-vector view matrix,
+    graphics_utils.py:44-50 layout: z_view = x V[0][2] + y V[1][2] + z V[2][2] + V[3][2])."""
+    V = d["viewmatrix"].astype(np.float64).reshape(4, 4)
+    z = (zv - m[:, 0] * V[0, 2] - m[:, 1] * V[1, 2] - V[3, 2]) / V[2, 2]
+    return z.astype(np.float32)
+
+
+def test_mark_visible_bit_exact():
+    import oracle
+    from diff_gaussian_rasterization_32 import GaussianRasterizationSettings, GaussianRasterizer_32
+    from guava_renderer_amd.diff_gaussian_rasterization_32 import _C
+    d = make_scene("random", 5000, 64, 64, seed=21)
+    m = d["means3D"].copy()
+    # put some points behind the camera and around the near plane (view-space z in [-1, 1], and 0.2)
+    m[:500, 2] = _world_z_for_view_z(d, m[:500], np.linspace(-1.0, 1.0, 500))
+    m[500:520, 2] = _world_z_for_view_z(d, m[500:520], np.full(20, 0.2))
+    t = torch_inputs(d)
+    mt = torch.tensor(m, device=DEV)
+    got = _C.mark_visible(mt, t["viewmatrix"], t["projmatrix"]).cpu().numpy()
+    ref = oracle.mark_visible(m, d["viewmatrix"], d["projmatrix"])
+    np.testing.assert_array_equal(got, ref)
+    assert 0 < ref.sum() < len(ref)
+    s = GaussianRasterizationSettings(64, 64, d["tanfovx"], d["tanfovy"], t["bg"], 1.0, t["viewmatrix"],
+                                      t["projmatrix"], 0, t["campos"], False, False, False)
+    vis = GaussianRasterizer_32(s).markVisible(mt)
+    assert vis.dtype == torch.bool
+    np.testing.assert_array_equal(vis.cpu().numpy(), ref)
+
+
+def test_all_culled_frame_is_background():
+    from guava_renderer_amd.batch import BatchRasterizer
+    from guava_renderer_amd.diff_gaussian_rasterization_32 import _C
+    d = make_scene("random", 3000, 80, 48, seed=22)
+    d["means3D"][:, 2] = _world_z_for_view_z(d, d["means3D"], np.full(3000, -3.0))  # all behind the camera
+    bg = np.linspace(-1.0, 2.0, 32).astype(np.float32)
+    t = torch_inputs(d)
+    t["bg"] = torch.tensor(bg, device=DEV)
+    empty = torch.Tensor([])
+    R, color, radii, gb, bb, ib, invd = _C.rasterize_gaussians(
+        t["bg"], t["means3D"], t["colors"], t["opacities"], t["scales"], t["rotations"], 1.0, empty,
+        t["viewmatrix"], t["projmatrix"], d["tanfovx"], d["tanfovy"], 48, 80, empty, 0, t["campos"],
+        False, False, False)
+    torch.cuda.synchronize()
+    assert R == 0
+    expect = np.broadcast_to(bg[:, None, None], (32, 48, 80))
+    np.testing.assert_array_equal(color.cpu().numpy(), expect)
+    assert (radii.cpu().numpy() == 0).all() and (invd.cpu().numpy() == 0).all()
+    # batched entry, 2 frames
+    r = BatchRasterizer(2, 3000, 80, 48, R_capacity=1024, device=DEV)
+    view = t["viewmatrix"].reshape(1, 16).expand(2, 16).contiguous()
+    proj = t["projmatrix"].reshape(1, 16).expand(2, 16).contiguous()
+    tanf = torch.tensor([[d["tanfovx"], d["tanfovy"]]] * 2, device=DEV)
+    col, inv, rad = r.forward(t["means3D"], t["colors"], t["opacities"], t["scales"], t["rotations"], view,
+                              proj, tanf, t["bg"])
+    r.poll(wait=True)
+    np.testing.assert_array_equal(col.cpu().numpy(), np.broadcast_to(expect, (2, 32, 48, 80)))
+    assert (rad.cpu().numpy() == 0).all() and (inv.cpu().numpy() == 0).all()
+
+
+def _cams(n, W, H):
+    from guava_renderer_amd import scenes
+    cams = scenes.frame_cameras(n, W, H, seed=1000)
+    t = lambda x: torch.tensor(np.ascontiguousarray(x), device=DEV)  # noqa: E731
+    return (t(np.stack([c["viewmatrix"].reshape(16) for c in cams])),
+            t(np.stack([c["projmatrix"].reshape(16) for c in cams])),
+            t(np.array([[c["tanfovx"], c["tanfovy"]] for c in cams], np.float32)))
+
+
+def test_batched_inputs_follow_tensor_strides():
+    from guava_renderer_amd import scenes
+    from guava_renderer_amd.batch import BatchRasterizer
+    B, P, W = 3, 20000, 128
+    sc = scenes.avatar_cloud(P, seed=4)
+    views, projs, tanf = _cams(B, W, W)
+    t = lambda x: torch.tensor(np.ascontiguousarray(x), device=DEV)  # noqa: E731
+    means = t(sc["means3D"])
+    cols, opac = t(sc["colors"]), t(sc["opacities"])
+    scales, rots = t(sc["scales"]), t(sc["rotations"])
+    bg = torch.zeros((B, 32), device=DEV)
+    ref = BatchRasterizer(B, P, W, W, R_capacity=16 * P * B, device=DEV)
+    c_ref, i_ref, r_ref = [x.clone() for x in ref.forward(means, cols, opac, scales, rots, views, projs, tanf, bg)]
+    r = BatchRasterizer(B, P, W, W, R_capacity=16 * P * B, device=DEV)
+    # deform.py's layout: per-frame geometry [B,P,k], features / opacity expanded (frame stride 0)
+    m3 = means.unsqueeze(0).repeat(B, 1, 1)
+    c_exp = cols.unsqueeze(0).expand(B, -1, -1)
+    o_exp = opac.unsqueeze(0).expand(B, -1, -1)
+    # rotations as a non-contiguous view ([B,P,4] slice of a wider buffer)
+    wide = torch.zeros((B, P, 6), device=DEV)
+    wide[..., 1:5] = rots
+    r_view = wide[..., 1:5]
+    s3 = scales.unsqueeze(0).repeat(B, 1, 1)
+    c1, i1, r1 = r.forward(m3, c_exp, o_exp, s3, r_view, views, projs, tanf, bg[:1].expand(B, -1))
+    torch.cuda.synchronize()
+    assert torch.equal(c1, c_ref) and torch.equal(i1, i_ref) and torch.equal(r1, r_ref)
+    with pytest.raises(ValueError):
+        r.forward(means[:10], cols, opac, scales, rots, views, projs, tanf, bg)
+    with pytest.raises(TypeError):
+        r.forward(means.double(), cols, opac, scales, rots, views, projs, tanf, bg)
+
+
+def test_refine_cache_follows_tensor_identity():
+    from guava_renderer_amd.batch import RefineHead
+    w = torch.randn(16, 32, device=DEV)
+    head = RefineHead(w, torch.zeros(16, device=DEV))
+    stream = torch.cuda.current_stream().cuda_stream
+    a = torch.randn(1000, 32, device=DEV)
+    pa = head.prepare(a, stream).clone()
+    assert head.prepare(a, stream) is head._prep  # cached
+    del a
+    b = torch.randn(1000, 32, device=DEV)  # may reuse a's address
+    pb = head.prepare(b, stream)
+    torch.testing.assert_close(pb[:, 4:20], b @ w.T, rtol=1e-5, atol=1e-5)
+    assert not torch.equal(pb, pa)
+    b.mul_(2.0)  # in-place torch update bumps the version
+    pb2 = head.prepare(b, stream)
+    torch.testing.assert_close(pb2[:, 4:20], b @ w.T, rtol=1e-5, atol=1e-5)

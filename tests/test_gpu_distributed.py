@@ -1,0 +1,73 @@
+"""World-size-2 run of the REAL rasterizer (frame sharding + all-gather of the rendered frames), two
+ranks on one GPU over gloo (the 8-GPU RCCL run is the driver's; the collective calls are the same,
+parallel.gather_frames).  The gathered batch must equal a single-process render of all frames,
+bit for bit (frames are independent; each rank runs the batched entry on its shard)."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+pytestmark = pytest.mark.gpu
+N_FRAMES, P, W = 5, 20000, 128
+
+
+def _inputs(frames):
+    from guava_renderer_amd import scenes
+    sc = scenes.avatar_cloud(P, seed=9)
+    cams = [scenes.frame_cameras(N_FRAMES, W, W, seed=1000)[i] for i in frames]
+    dev = torch.device("cuda:0")
+    t = lambda x: torch.tensor(np.ascontiguousarray(x), device=dev)  # noqa: E731
+    args = [t(sc[k]) for k in ("means3D", "colors", "opacities", "scales", "rotations")]
+    views = t(np.stack([c["viewmatrix"].reshape(16) for c in cams]))
+    projs = t(np.stack([c["projmatrix"].reshape(16) for c in cams]))
+    tanf = t(np.array([[c["tanfovx"], c["tanfovy"]] for c in cams], np.float32))
+    return args, views, projs, tanf, torch.zeros((len(frames), 32), device=dev)
+
+
+def _render(frames):
+    from guava_renderer_amd import _lib
+    from guava_renderer_amd.batch import BatchRasterizer
+    _lib.set_exact_exp(True)
+    _lib.set_split_bf16(False)
+    args, views, projs, tanf, bg = _inputs(frames)
+    r = BatchRasterizer(len(frames), P, W, W, R_capacity=16 * P * len(frames), device="cuda:0")
+    col, _, _ = r.forward(*args, views, projs, tanf, bg)
+    r.poll(wait=True)
+    return col.clone()
+
+
+def _worker(rank, world, port, q):
+    import torch.distributed as dist
+    from guava_renderer_amd import parallel
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        lo, hi = parallel.shard_range(N_FRAMES, rank, world)
+        local = _render(list(range(lo, hi)))
+        full = parallel.gather_frames(local.cpu(), N_FRAMES)
+        if rank == 0:
+            q.put(full.numpy())
+    finally:
+        dist.destroy_process_group()
+
+
+def test_two_ranks_real_rasterizer_gather():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    gathered = q.get(timeout=240)
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    ref = _render(list(range(N_FRAMES))).cpu().numpy()
+    assert gathered.shape == ref.shape
+    np.testing.assert_array_equal(gathered, ref)
