@@ -93,7 +93,12 @@ def cpu_baseline(scene, cams, W, H, budget_s, avatar_inputs=None):
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle  # CPU restatement of the reference algorithm (checker / baseline only)
     import lbs_oracle  # CPU restatement of the deformation (numpy)
-    threads = max(1, min(16, os.cpu_count() or 1))
+    # the cores this process may use (affinity), capped by OMP_NUM_THREADS where the host sets it
+    # (the GPU box: 16 per GPU job)
+    threads = len(os.sched_getaffinity(0))
+    omp = os.environ.get("OMP_NUM_THREADS", "")
+    if omp.isdigit() and int(omp) > 0:
+        threads = min(threads, int(omp))
     oracle.set_threads(threads)
     bg = np.zeros(C, np.float32)
     t0 = time.perf_counter()

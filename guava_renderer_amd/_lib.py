@@ -65,6 +65,13 @@ def load(path=None):
             raise GsrError(f"libgsr.so not found at {path} and could not be built: {e}") from e
     L = ctypes.CDLL(path)
     L.gsr_version.restype = ctypes.c_char_p
+    # stale-build guard: the library carries the hash of the sources it was built from
+    built = L.gsr_version().decode().split()[-1]
+    if path == LIB_PATH and os.environ.get("GSR_ALLOW_STALE") != "1":
+        from . import build as _build
+        if os.path.isdir(_build.CSRC) and built != _build.source_hash():
+            raise GsrError(f"{path} was built from other sources (hash {built}, tree {_build.source_hash()}): "
+                           "rebuild with `python -m guava_renderer_amd.build` (GSR_ALLOW_STALE=1 overrides)")
     L.gsr_last_error.restype = ctypes.c_char_p
     L.gsr_set_exact_exp.argtypes = [_i]
     L.gsr_set_exact_exp.restype = _i

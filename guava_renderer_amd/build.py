@@ -6,6 +6,7 @@
 evaluate the same expressions in the same order.
 """
 import concurrent.futures as cf
+import hashlib
 import os
 import subprocess
 import sys
@@ -28,6 +29,22 @@ FLAGS = ["-O3", "-std=c++17", "-fPIC", "-ffp-contract=off", f"--offload-arch={AR
 EXTRA = {"render_fwd.hip": ["-fno-slp-vectorize"], "render_bwd.hip": ["-fno-slp-vectorize"]}
 
 
+def source_hash():
+    """SHA-256 (first 16 hex digits) over every HIP source, internal header and include/*.h, plus the
+    compile flags: stamped into the library (gsr_version) so a stale prebuilt .so is detected at
+    load time (_lib.load) instead of silently running old code."""
+    h = hashlib.sha256()
+    inc = os.path.join(os.path.dirname(HERE), "include")
+    files = sorted(os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith((".hip", ".h")))
+    files += sorted(os.path.join(inc, f) for f in os.listdir(inc) if f.endswith(".h"))
+    for f in files:
+        h.update(os.path.basename(f).encode())
+        h.update(open(f, "rb").read())
+    h.update(" ".join(FLAGS).encode())
+    h.update(repr(sorted(EXTRA.items())).encode())
+    return h.hexdigest()[:16]
+
+
 def _newer(src_paths, dst):
     if not os.path.exists(dst):
         return True
@@ -40,11 +57,16 @@ def _compile(src):
     deps = [os.path.join(CSRC, src)] + [os.path.join(CSRC, h) for h in os.listdir(CSRC) if h.endswith(".h")]
     inc = os.path.join(os.path.dirname(HERE), "include")
     deps += [os.path.join(inc, h) for h in os.listdir(inc) if h.endswith(".h")]
-    if _newer(deps, obj):
-        cmd = [HIPCC] + FLAGS + EXTRA.get(src, []) + ["-c", os.path.join(CSRC, src), "-o", obj]
+    stamp = obj + ".hash"
+    want = source_hash()
+    stale = not os.path.exists(stamp) or open(stamp).read() != want
+    if stale or _newer(deps, obj):
+        cmd = [HIPCC] + FLAGS + EXTRA.get(src, []) + [f'-DGSR_SRC_HASH="{want}"', "-c", os.path.join(CSRC, src),
+                                                      "-o", obj]
         r = subprocess.run(cmd, capture_output=True, text=True)
         if r.returncode != 0:
             raise RuntimeError(f"hipcc failed for {src}:\n{r.stdout}\n{r.stderr}")
+        open(stamp, "w").write(want)
     return obj
 
 

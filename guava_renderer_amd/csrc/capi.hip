@@ -196,7 +196,12 @@ int gsr::api_fail(int status, const char* msg) { return fail((gsr_status)status,
 
 extern "C" {
 
-const char* gsr_version(void) { return "gsr-gfx950 0.1"; }
+#ifndef GSR_SRC_HASH
+#define GSR_SRC_HASH "unstamped"
+#endif
+// "gsr-gfx950 <version> <source hash>": the hash of the sources the library was built from
+// (guava_renderer_amd/build.py source_hash), checked against the tree by the Python loader
+const char* gsr_version(void) { return "gsr-gfx950 0.2 " GSR_SRC_HASH; }
 const char* gsr_last_error(void) { return g_err.c_str(); }
 int gsr_set_exact_exp(int on) {
     int prev = g_exact_exp;

@@ -46,10 +46,18 @@ def _cpu_model():
         return platform.processor() or "unknown"
 
 
+def _cores():
+    """Cores this process may use: the affinity set, capped by OMP_NUM_THREADS when the host sets
+    it (the GPU box gives one GPU's job 16 of its cores and exports OMP_NUM_THREADS=16)."""
+    n = len(os.sched_getaffinity(0))
+    omp = os.environ.get("OMP_NUM_THREADS")
+    return min(n, int(omp)) if omp and omp.isdigit() and int(omp) > 0 else n
+
+
 def oracle_rows():
     import oracle
     from guava_renderer_amd import camera, scenes
-    cores = len(os.sched_getaffinity(0))
+    cores = _cores()
     rows = []
     d = scenes.random_cloud(10000, 0)
     cam = camera.camera(256, 256)
@@ -114,7 +122,7 @@ def reference_lbs_rows():
 
 def main():
     out = {"host": platform.node(), "cpu": _cpu_model(), "affinity_cores": len(os.sched_getaffinity(0)),
-           "os_cpu_count": os.cpu_count(), "rows": oracle_rows() + reference_lbs_rows()}
+           "os_cpu_count": os.cpu_count(), "cores_used": _cores(), "rows": oracle_rows() + reference_lbs_rows()}
     s = json.dumps(out, indent=1)
     if len(sys.argv) > 1:
         open(sys.argv[1], "w").write(s + "\n")
