@@ -40,7 +40,7 @@ def source_hash():
     for f in files:
         h.update(os.path.basename(f).encode())
         h.update(open(f, "rb").read())
-    h.update(" ".join(FLAGS).encode())
+    h.update(" ".join(f for f in FLAGS if not f.startswith("-I")).encode())  # (no paths: the tree moves)
     h.update(repr(sorted(EXTRA.items())).encode())
     return h.hexdigest()[:16]
 

@@ -305,7 +305,7 @@ __device__ __forceinline__ void render_fwd_body(const Dims& d, const Inputs& in,
         int base = -64;
         uint64_t mask = 0;
         uint32_t cidx = 0;
-        uint32_t nidx = lane < n ? plist[lane] : 0u;
+
         // next survivor -> (g, pos); false at the end of the list
 #define GSR_NEXT(g_, pos_)                                                                          \
         ({                                                                                          \
@@ -313,11 +313,7 @@ __device__ __forceinline__ void render_fwd_body(const Dims& d, const Inputs& in,
             while (mask == 0) {                                                                     \
                 base += 64;                                                                         \
                 if (base >= n) { ok_ = false; break; }                                              \
-                cidx = nidx;                                                                        \
-                if (base + 64 < n) {                                                                \
-                    const int j_ = base + 64 + lane;                                                \
-                    nidx = j_ < n ? plist[j_] : 0u;                                                 \
-                }                                                                                   \
+                cidx = lane < n - base ? plist[base + lane] : 0u;                                   \
                 mask = __ballot(lane < n - base && (cidx & smask_bit) != 0u);                       \
                 if (STATS) n_staged += min(64, n - base);                                           \
             }                                                                                       \
