@@ -17,7 +17,7 @@ EXPORTS = ("gsr_version", "gsr_last_error", "gsr_set_exact_exp", "gsr_set_split_
            "gsr_refine_prepare", "gsr_batch_status_offset",
            # include/gsr_deform.h
            "gsr_lbs_workspace_bytes", "gsr_lbs", "gsr_blend_joints", "gsr_splice_head",
-           "gsr_deform_gaussians",
+           "gsr_pack_rows", "gsr_deform_gaussians",
            # include/gsr_ssim.h
            "gsr_fused_ssim", "gsr_fused_ssim_backward")
 
@@ -36,6 +36,12 @@ class RefineEpilogue(ctypes.Structure):
     """gsr_refine_epilogue (include/gsr.h)."""
     _fields_ = [("weight", _vp), ("bias", _vp), ("n_out", _i), ("negative_slope", _f),
                 ("out_refine", _vp), ("keep_channels", _i)]
+
+
+class RowSegment(ctypes.Structure):
+    """GsrRowSegment (include/gsr_deform.h)."""
+    _fields_ = [("src", _vp), ("dst", _vp), ("src_stride", _i64), ("dst_stride", _i64), ("width", _i),
+                ("pad_", _i)]
 
 
 class GsrError(RuntimeError):
@@ -130,6 +136,8 @@ def load(path=None):
     L.gsr_splice_head.argtypes = [_i, _i, _i, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i, _i, _i, _vp, _i,
                                   _i, _i, _vp, _vp, _vp]
     L.gsr_splice_head.restype = _i
+    L.gsr_pack_rows.argtypes = [_i, _i, ctypes.POINTER(RowSegment), _vp]
+    L.gsr_pack_rows.restype = _i
     L.gsr_deform_gaussians.argtypes = [_i, _i, _i, _i, _vp, _vp, _vp, _vp, _i64, _vp, _i64, _vp, _vp,
                                        _vp, _i64, _vp, _i64, _vp, _i64, _vp, _vp, _vp, _vp, _vp]
     L.gsr_deform_gaussians.restype = _i

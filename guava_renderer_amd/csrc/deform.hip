@@ -12,16 +12,22 @@
 //   ubody_gaussian.py:253-254,258,270)
 //
 // Kernels (all B frames per launch):
+//   k_pack_rows      segs x B WGs     the coefficient rows of EHM.forward from their pieces
 //   k_lbs_rodrigues  B*J threads      axis-angle -> R, pose feature R - I
 //   k_lbs_blend      3V/64 x B/16 WGs v_shaped = template + shapedirs.betas, v_posed = v_shaped +
 //                                     posedirs.feature: the bases are streamed once per 16 frames
 //                                     (HBM-bound: 4*(NB + 9(J-1)) bytes per vertex coordinate)
-//   k_lbs_joints     J x B workgroups J_regressor . v_shaped (+ joints_offset)
+//   k_lbs_blend_mfma 3V/32 x B/32 WGs the same for B > 16 on the matrix cores (f32 MFMA), bases
+//                                     streamed once per 32 frames
+//   k_lbs_joints     J/4 x B WGs      J_regressor . v_shaped (+ joints_offset)
 //   k_lbs_chain      B waves          the kinematic chain (J sequential 4x4 products) in LDS
 //   k_lbs_skin       V x B            T_v = sum_j w_vj A_j, v = T_v [v_posed; 1]
-//   k_deform_gaussians (V+N) x B      vertex + UV Gaussians straight into the rasterizer's inputs
+//   k_deform_gaussians (V+N) x B/8    vertex + UV Gaussians straight into the rasterizer's inputs
+//                                     (face frames once per face and frame, in LDS)
 // Every sum runs in a fixed order (fmaf chains over k in index order, 3-term dots left to right),
 // so results are deterministic run to run.
+#include <climits>
+#include <cstdlib>
 #include <string>
 
 #include "../../include/gsr.h"
@@ -29,6 +35,10 @@
 #include "gsr_internal.h"
 
 namespace gsr {
+
+#ifndef GSR_DEFORM_NOSTORE
+#define GSR_DEFORM_NOSTORE 0  // timing ablation only: skip the UV rotation and the means/scales stores
+#endif
 
 constexpr int kLbsFrames = 16;  // frames per k_lbs_blend workgroup (accumulators per thread)
 constexpr int kLbsSplit = 4;    // k_lbs_blend waves per workgroup, each an interleaved slice of k
@@ -188,6 +198,81 @@ __global__ __launch_bounds__(64 * kLbsSplit) void k_lbs_blend(int B, int M, int 
     }
 }
 
+// The same products for batches of more than kLbsFrames frames, on the matrix cores, with the
+// bases read ONCE per 32 frames: D[b][m] = sum_k coef[b][k] base[k][m] is a (32 frames x 32
+// coordinates) tile per workgroup, v_mfma_f32_32x32x2_f32 (exact f32 products) with A = the
+// frames' coefficients (row b, k) and B = the k-major bases (column m, coalesced 128-byte
+// half-wave loads).  The 4 waves take interleaved k-steps and their partial tiles are added in
+// wave order through LDS (deterministic); each wave then finishes 4 of the 16 output registers:
+// v_shaped = template + shape sum, v_posed = v_shaped + pose sum (the VALU kernel's association).
+// (Measured variants: 8 waves x 16 loads in flight, and the coefficient block staged transposed
+// in LDS, were both slower at B = 32.)
+typedef float floatx16 __attribute__((ext_vector_type(16)));
+constexpr int kBlendUnroll = 8;  // k-steps whose loads are issued before their MFMAs
+
+__device__ __forceinline__ void blend_mfma_part(floatx16& acc, const float* __restrict__ coef, int ncoef,
+                                                const float* __restrict__ base, int M, int K, int bA, bool bok,
+                                                int m, bool mok, int w, int hi) {
+    const int nsteps = (K + 1) / 2;
+    for (int s0 = w; s0 < nsteps; s0 += 4 * kBlendUnroll) {
+        float a[kBlendUnroll], bb[kBlendUnroll];
+#pragma unroll
+        for (int u = 0; u < kBlendUnroll; u++) {
+            const int k = 2 * (s0 + 4 * u) + hi;
+            const bool kok = s0 + 4 * u < nsteps && k < K;
+            a[u] = (bok && kok) ? coef[(int64_t)bA * ncoef + k] : 0.f;
+            bb[u] = (mok && kok) ? base[(int64_t)k * M + m] : 0.f;
+        }
+#pragma unroll
+        for (int u = 0; u < kBlendUnroll; u++) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a[u], bb[u], acc, 0, 0, 0);
+    }
+}
+
+__global__ __launch_bounds__(256) void k_lbs_blend_mfma(int B, int M, int NB, int NP,
+                                                        const float* __restrict__ vt, int64_t vt_stride,
+                                                        const float* __restrict__ betas,
+                                                        const float* __restrict__ sd_t,
+                                                        const float* __restrict__ feat,
+                                                        const float* __restrict__ pd,
+                                                        float* __restrict__ v_shaped,
+                                                        float* __restrict__ v_posed) {
+    __shared__ float red[4][2][16][64];  // per-wave partial tiles: [wave][shape/pose][register][lane]
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, hi = lane >> 5, l32 = lane & 31;
+    const int m0 = blockIdx.x * 32, b0 = blockIdx.y * 32;
+    const int m = m0 + l32, bA = b0 + l32;
+    const bool mok = m < M, bok = bA < B;
+    floatx16 as, ap;
+#pragma unroll
+    for (int r = 0; r < 16; r++) { as[r] = 0.f; ap[r] = 0.f; }
+    if (NB > 0) blend_mfma_part(as, betas, NB, sd_t, M, NB, bA, bok, m, mok, w, hi);
+    if (NP > 0 && v_posed) blend_mfma_part(ap, feat, NP, pd, M, NP, bA, bok, m, mok, w, hi);
+#pragma unroll
+    for (int r = 0; r < 16; r++) {
+        red[w][0][r][lane] = as[r];
+        red[w][1][r][lane] = ap[r];
+    }
+    __syncthreads();
+    // wave w finishes registers 4w..4w+3: row (frame) (r&3) + 8(r>>2) + 4(lane>>5), column m
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+        const int r = 4 * w + i;
+        const int b = b0 + (r & 3) + 8 * (r >> 2) + 4 * hi;
+        if (!mok || b >= B) continue;
+        float S = red[0][0][r][lane], Pz = red[0][1][r][lane];
+#pragma unroll
+        for (int u = 1; u < 4; u++) { S += red[u][0][r][lane]; Pz += red[u][1][r][lane]; }
+        const float tv = vt[(int64_t)b * vt_stride + m];
+        const float vs = NB > 0 ? tv + S : tv;
+        v_shaped[(int64_t)b * M + m] = vs;
+        if (v_posed) v_posed[(int64_t)b * M + m] = Pz + vs;
+    }
+}
+
+// blend launcher: the matrix-core kernel for more than kLbsFrames frames, the streaming one otherwise
+static void launch_blend(int B, int M, int NB, int NP, const float* vt, int64_t vt_stride, const float* betas,
+                         const float* sd_t, const float* feat, const float* pd, float* vs, float* vp,
+                         hipStream_t s);
+
 static size_t lbs_blend_lds(int NB, int NP) {
     const size_t coef = sizeof(float) * (size_t)(NB + NP) * kLbsFrames;
     const size_t red = sizeof(float) * (size_t)kLbsSplit * kLbsFrames * 64;
@@ -202,36 +287,86 @@ static void lbs_blend_attr(size_t lds) {
     }
 }
 
+static void launch_blend(int B, int M, int NB, int NP, const float* vt, int64_t vt_stride, const float* betas,
+                         const float* sd_t, const float* feat, const float* pd, float* vs, float* vp,
+                         hipStream_t s) {
+    static const bool valu_only = [] {  // timing A/B only
+        const char* e = getenv("GSR_BLEND_VALU");
+        return e && e[0] == '1';
+    }();
+    if (B > kLbsFrames && !valu_only) {
+        hipLaunchKernelGGL(k_lbs_blend_mfma, dim3((M + 31) / 32, (B + 31) / 32), dim3(256), 0, s, B, M, NB,
+                           vp ? NP : 0, vt, vt_stride, betas, sd_t, feat, pd, vs, vp);
+        return;
+    }
+    const size_t lds = lbs_blend_lds(NB, vp ? NP : 0);
+    lbs_blend_attr(lds);
+    hipLaunchKernelGGL(k_lbs_blend, lbs_blend_grid(M, B), dim3(64 * kLbsSplit), lds, s, B, M, NB, vp ? NP : 0,
+                       vt, vt_stride, betas, sd_t, feat, pd, vs, vp);
+}
+
 // vertices2joints (lbs.py:335-352): J[b,j,:] = sum_v J_regressor[j,v] v_shaped[b,v,:], plus
-// joints_offset (lbs.py:191/:295).  One workgroup per (joint, frame); fixed-shape tree reduction.
+// joints_offset (lbs.py:191/:295).  One workgroup per (group of kJointsPerWG joints, frame), so a
+// frame's vertices are read once per group rather than once per joint; fixed-shape tree reduction.
+constexpr int kJointsPerWG = 4;
+
 __global__ __launch_bounds__(256) void k_lbs_joints(int V, int J, const float* __restrict__ jreg,
                                                     const float* __restrict__ v_shaped,
                                                     const float* __restrict__ joff,
                                                     float* __restrict__ joints) {
-    __shared__ float red[3][256];
-    const int j = blockIdx.x, b = blockIdx.y;
+    __shared__ float red[3 * kJointsPerWG][256];
+    const int j0 = blockIdx.x * kJointsPerWG, b = blockIdx.y;
+    const int nj = min(kJointsPerWG, J - j0);
     const float* vs = v_shaped + (int64_t)b * V * 3;
-    const float* w = jreg + (int64_t)j * V;
-    float ax = 0.f, ay = 0.f, az = 0.f;
-    for (int v = threadIdx.x; v < V; v += blockDim.x) {
-        const float wv = w[v];
-        ax = fmaf(wv, vs[3 * v], ax);
-        ay = fmaf(wv, vs[3 * v + 1], ay);
-        az = fmaf(wv, vs[3 * v + 2], az);
+    float acc[kJointsPerWG][3];
+#pragma unroll
+    for (int q = 0; q < kJointsPerWG; q++) acc[q][0] = acc[q][1] = acc[q][2] = 0.f;
+    // four vertices' loads in flight per round; each thread still sums its vertices in index order
+    constexpr int kU = 4;
+    int v0 = threadIdx.x;
+    for (; v0 + 256 * (kU - 1) < V; v0 += 256 * kU) {
+        float x[kU], y[kU], z[kU], wv[kU][kJointsPerWG];
+#pragma unroll
+        for (int u = 0; u < kU; u++) {
+            const int v = v0 + 256 * u;
+            x[u] = vs[3 * v]; y[u] = vs[3 * v + 1]; z[u] = vs[3 * v + 2];
+#pragma unroll
+            for (int q = 0; q < kJointsPerWG; q++) wv[u][q] = q < nj ? jreg[(int64_t)(j0 + q) * V + v] : 0.f;
+        }
+#pragma unroll
+        for (int u = 0; u < kU; u++)
+#pragma unroll
+            for (int q = 0; q < kJointsPerWG; q++) {
+                acc[q][0] = fmaf(wv[u][q], x[u], acc[q][0]);
+                acc[q][1] = fmaf(wv[u][q], y[u], acc[q][1]);
+                acc[q][2] = fmaf(wv[u][q], z[u], acc[q][2]);
+            }
     }
-    red[0][threadIdx.x] = ax;
-    red[1][threadIdx.x] = ay;
-    red[2][threadIdx.x] = az;
+    for (int v = v0; v < V; v += 256) {
+        const float x = vs[3 * v], y = vs[3 * v + 1], z = vs[3 * v + 2];
+#pragma unroll
+        for (int q = 0; q < kJointsPerWG; q++) {
+            const float wv = q < nj ? jreg[(int64_t)(j0 + q) * V + v] : 0.f;
+            acc[q][0] = fmaf(wv, x, acc[q][0]);
+            acc[q][1] = fmaf(wv, y, acc[q][1]);
+            acc[q][2] = fmaf(wv, z, acc[q][2]);
+        }
+    }
+#pragma unroll
+    for (int q = 0; q < kJointsPerWG; q++)
+        for (int c = 0; c < 3; c++) red[3 * q + c][threadIdx.x] = acc[q][c];
     __syncthreads();
     for (int h = 128; h > 0; h >>= 1) {
         if ((int)threadIdx.x < h)
-            for (int c = 0; c < 3; c++) red[c][threadIdx.x] += red[c][threadIdx.x + h];
+#pragma unroll
+            for (int e = 0; e < 3 * kJointsPerWG; e++) red[e][threadIdx.x] += red[e][threadIdx.x + h];
         __syncthreads();
     }
-    if (threadIdx.x < 3) {
+    if ((int)threadIdx.x < 3 * nj) {
+        const int q = threadIdx.x / 3, c = threadIdx.x - 3 * q;
         float v = red[threadIdx.x][0];
-        if (joff) v = v + joff[((int64_t)b * J + j) * 3 + threadIdx.x];
-        joints[((int64_t)b * J + j) * 3 + threadIdx.x] = v;
+        if (joff) v = v + joff[((int64_t)b * J + j0 + q) * 3 + c];
+        joints[((int64_t)b * J + j0 + q) * 3 + c] = v;
     }
 }
 
@@ -297,14 +432,29 @@ __global__ __launch_bounds__(256) void k_lbs_skin(int V, int J, const float* __r
     __syncthreads();
     const int v = blockIdx.x * blockDim.x + threadIdx.x;
     if (v >= V) return;
+    // T = sum_j w_j A_j as 8 packed pairs (v_pk_fma_f32: two independent fmaf chains per
+    // instruction, each in j order); four weight loads in flight per round
+    typedef float f2 __attribute__((ext_vector_type(2)));
+    f2 T2[8];
+#pragma unroll
+    for (int e = 0; e < 8; e++) T2[e] = f2{0.f, 0.f};
+    const f2* A2 = reinterpret_cast<const f2*>(As);
+    // 16 weight loads in flight per round (the kernel is load-latency bound; J <= 64 is 4 rounds)
+    for (int j0 = 0; j0 < J; j0 += 16) {
+        float w16[16];
+#pragma unroll
+        for (int u = 0; u < 16; u++) w16[u] = j0 + u < J ? w_t[(int64_t)(j0 + u) * V + v] : 0.f;
+#pragma unroll
+        for (int u = 0; u < 16; u++) {
+            if (j0 + u >= J) break;
+#pragma unroll
+            for (int e = 0; e < 8; e++)
+                T2[e] = __builtin_elementwise_fma(f2{w16[u], w16[u]}, A2[8 * (j0 + u) + e], T2[e]);
+        }
+    }
     float T[16];
 #pragma unroll
-    for (int e = 0; e < 16; e++) T[e] = 0.f;
-    for (int j = 0; j < J; j++) {
-        const float w = w_t[(int64_t)j * V + v];
-#pragma unroll
-        for (int e = 0; e < 16; e++) T[e] = fmaf(w, As[16 * j + e], T[e]);
-    }
+    for (int e = 0; e < 8; e++) { T[2 * e] = T2[e].x; T[2 * e + 1] = T2[e].y; }
     const float* p = v_posed + ((int64_t)b * V + v) * 3;
     const float x = p[0], y = p[1], z = p[2];
     float* o = verts + ((int64_t)b * V + v) * 3;
@@ -353,6 +503,9 @@ __global__ __launch_bounds__(256) void k_splice_head(
 }
 
 // roma.rotmat_to_unitquat (scipy's from_matrix decision scheme), row-major m -> (x, y, z, w).
+// The branch on the largest of (m00, m11, m22, trace) picks one of four candidate quaternions;
+// the candidates share their off-diagonal sums, so all four are formed with 7 adds and the choice
+// is made with selects (no dynamically indexed arrays, which compile to compare/select ladders).
 __device__ __forceinline__ float4 rotmat_to_unitquat(const float m[9]) {
     const float d0 = m[0], d1 = m[4], d2 = m[8];
     const float d3 = (d0 + d1) + d2;
@@ -361,21 +514,16 @@ __device__ __forceinline__ float4 rotmat_to_unitquat(const float m[9]) {
     if (d1 > best) { best = d1; ch = 1; }
     if (d2 > best) { best = d2; ch = 2; }
     if (d3 > best) { best = d3; ch = 3; }
-    float q[4];
-    if (ch != 3) {
-        const int i = ch, j = (i + 1) % 3, k = (j + 1) % 3;
-        q[i] = (1.0f - d3) + 2.0f * m[4 * i];
-        q[j] = m[3 * j + i] + m[3 * i + j];
-        q[k] = m[3 * k + i] + m[3 * i + k];
-        q[3] = m[3 * k + j] - m[3 * j + k];
-    } else {
-        q[0] = m[7] - m[5];
-        q[1] = m[2] - m[6];
-        q[2] = m[3] - m[1];
-        q[3] = 1.0f + d3;
-    }
-    const float n = sqrtf(((q[0] * q[0] + q[1] * q[1]) + q[2] * q[2]) + q[3] * q[3]);
-    return make_float4(q[0] / n, q[1] / n, q[2] / n, q[3] / n);
+    const float t = 1.0f - d3;
+    const float s01 = m[1] + m[3], s02 = m[2] + m[6], s12 = m[5] + m[7];  // m[3j+i] + m[3i+j]
+    const float r0 = m[7] - m[5], r1 = m[2] - m[6], r2 = m[3] - m[1];     // the w candidates
+    float4 q;
+    q.x = ch == 0 ? t + 2.0f * m[0] : ch == 1 ? s01 : ch == 2 ? s02 : r0;
+    q.y = ch == 0 ? s01 : ch == 1 ? t + 2.0f * m[4] : ch == 2 ? s12 : r1;
+    q.z = ch == 0 ? s02 : ch == 1 ? s12 : ch == 2 ? t + 2.0f * m[8] : r2;
+    q.w = ch == 0 ? r0 : ch == 1 ? r1 : ch == 2 ? r2 : 1.0f + d3;
+    const float n = sqrtf(((q.x * q.x + q.y * q.y) + q.z * q.z) + q.w * q.w);
+    return make_float4(q.x / n, q.y / n, q.z / n, q.w / n);
 }
 
 // roma.quat_product, xyzw: (p_w q_v + q_w p_v + p_v x q_v, p_w q_w - p_v . q_v)
@@ -392,61 +540,13 @@ __device__ __forceinline__ float dot3(float ax, float ay, float az, float bx, fl
     return (ax * bx + ay * by) + az * bz;
 }
 
-// Vertex Gaussians (ubody_gaussian.py:252-254): xyz = LBS vertex, rotation =
-// normalize(q(T_v[:3,:3]) (x) q_v) in wxyz, scale unchanged.  UV Gaussians (:257-271): face frame
-// [a0 a1 a2] and scale of the deformed binding face, centre = bary . face vertices, xyz =
-// (frame . local) * s + centre, rotation = q(frame) (x) q_uv (not renormalised), scale = scale * s.
-__global__ __launch_bounds__(256) void k_deform_gaussians(
-    int V, int F, int N, const float* __restrict__ verts, const float* __restrict__ vtrans,
-    const int32_t* __restrict__ faces, const float* __restrict__ vrot, int64_t s_vrot,
-    const float* __restrict__ vscale, int64_t s_vscale, const int32_t* __restrict__ bind,
-    const float* __restrict__ bary, const float* __restrict__ lxyz, int64_t s_lxyz,
-    const float* __restrict__ urot, int64_t s_urot, const float* __restrict__ uscale,
-    int64_t s_uscale, float* __restrict__ means, float* __restrict__ rots,
-    float* __restrict__ scales, uint32_t* __restrict__ bad) {
-    const int b = blockIdx.y;
-    const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    const int P = V + N;
-    if (i >= P) return;
-    const int64_t o = (int64_t)b * P + i;
-    const float* vb = verts + (int64_t)b * V * 3;
-    if (i < V) {
-        const float4* tv = reinterpret_cast<const float4*>(vtrans + ((int64_t)b * V + i) * 16);
-        const float4 r0 = tv[0], r1 = tv[1], r2 = tv[2];
-        const float m[9] = {r0.x, r0.y, r0.z, r1.x, r1.y, r1.z, r2.x, r2.y, r2.z};
-        const float4 qd = rotmat_to_unitquat(m);
-        const float* qv = vrot + b * s_vrot + 4 * (int64_t)i;  // wxyz
-        const float4 q = quat_product(qd, make_float4(qv[1], qv[2], qv[3], qv[0]));
-        // F.normalize over the wxyz vector: x / max(||x||, 1e-12)
-        const float n = fmaxf(sqrtf(((q.w * q.w + q.x * q.x) + q.y * q.y) + q.z * q.z), 1e-12f);
-        reinterpret_cast<float4*>(rots)[o] = make_float4(q.w / n, q.x / n, q.y / n, q.z / n);
-        for (int c = 0; c < 3; c++) {
-            means[3 * o + c] = vb[3 * i + c];
-            scales[3 * o + c] = vscale[b * s_vscale + 3 * (int64_t)i + c];
-        }
-        return;
-    }
-    const int n = i - V;
-    int f = bind[n];
-    int i0 = 0, i1 = 0, i2 = 0;
-    bool ok = f >= 0 && f < F;
-    if (ok) {
-        i0 = faces[3 * f]; i1 = faces[3 * f + 1]; i2 = faces[3 * f + 2];
-        ok = i0 >= 0 && i0 < V && i1 >= 0 && i1 < V && i2 >= 0 && i2 < V;
-    }
-    if (!ok) {  // reference: an IndexError; here a flag and NaN outputs, no out-of-range access
-        if (bad) atomicOr(bad, 1u);
-        const float nan = __int_as_float(0x7fc00000);
-        for (int c = 0; c < 3; c++) { means[3 * o + c] = nan; scales[3 * o + c] = nan; }
-        reinterpret_cast<float4*>(rots)[o] = make_float4(nan, nan, nan, nan);
-        return;
-    }
+// compute_face_orientation (graphics_utils.py:61-80, safe_normalize eps 1e-20) of one deformed face
+// and the frame's rotmat_to_unitquat (ubody_gaussian.py:257-258): fr = {m[9] (row-major, columns
+// a0 a1 a2), s, q.xyzw}.
+__device__ __forceinline__ void face_frame(const float* __restrict__ vb, int i0, int i1, int i2, float fr[14]) {
     const float v0x = vb[3 * i0], v0y = vb[3 * i0 + 1], v0z = vb[3 * i0 + 2];
-    const float v1x = vb[3 * i1], v1y = vb[3 * i1 + 1], v1z = vb[3 * i1 + 2];
-    const float v2x = vb[3 * i2], v2y = vb[3 * i2 + 1], v2z = vb[3 * i2 + 2];
-    // compute_face_orientation (graphics_utils.py:61-80), safe_normalize with eps 1e-20
-    const float e1x = v1x - v0x, e1y = v1y - v0y, e1z = v1z - v0z;
-    const float e2x = v2x - v0x, e2y = v2y - v0y, e2z = v2z - v0z;
+    const float e1x = vb[3 * i1] - v0x, e1y = vb[3 * i1 + 1] - v0y, e1z = vb[3 * i1 + 2] - v0z;
+    const float e2x = vb[3 * i2] - v0x, e2y = vb[3 * i2 + 1] - v0y, e2z = vb[3 * i2 + 2] - v0z;
     const float l1 = sqrtf(fmaxf(dot3(e1x, e1y, e1z, e1x, e1y, e1z), 1e-20f));
     const float a0x = e1x / l1, a0y = e1y / l1, a0z = e1z / l1;
     const float c1x = a0y * e2z - a0z * e2y, c1y = a0z * e2x - a0x * e2z, c1z = a0x * e2y - a0y * e2x;
@@ -455,24 +555,139 @@ __global__ __launch_bounds__(256) void k_deform_gaussians(
     const float c2x = a1y * a0z - a1z * a0y, c2y = a1z * a0x - a1x * a0z, c2z = a1x * a0y - a1y * a0x;
     const float lc2 = sqrtf(fmaxf(dot3(c2x, c2y, c2z, c2x, c2y, c2z), 1e-20f));
     const float a2x = -(c2x / lc2), a2y = -(c2y / lc2), a2z = -(c2z / lc2);
-    const float s = (l1 + fabsf(dot3(a2x, a2y, a2z, e2x, e2y, e2z))) / 2.0f;
-    // orientation columns a0, a1, a2 (row-major m[r][c] = a_c[r])
     const float m[9] = {a0x, a1x, a2x, a0y, a1y, a2y, a0z, a1z, a2z};
-    const float4 qf = rotmat_to_unitquat(m);
-    const float* qu = urot + b * s_urot + 4 * (int64_t)n;  // wxyz
-    const float4 q = quat_product(qf, make_float4(qu[1], qu[2], qu[3], qu[0]));
-    reinterpret_cast<float4*>(rots)[o] = make_float4(q.w, q.x, q.y, q.z);
-    const float w0 = bary[3 * n], w1 = bary[3 * n + 1], w2 = bary[3 * n + 2];
-    const float* l = lxyz + b * s_lxyz + 3 * (int64_t)n;
-    const float lx = l[0], ly = l[1], lz = l[2];
-    const float cx = (w0 * v0x + w1 * v1x) + w2 * v2x;
-    const float cy = (w0 * v0y + w1 * v1y) + w2 * v2y;
-    const float cz = (w0 * v0z + w1 * v1z) + w2 * v2z;
-    means[3 * o] = dot3(m[0], m[1], m[2], lx, ly, lz) * s + cx;
-    means[3 * o + 1] = dot3(m[3], m[4], m[5], lx, ly, lz) * s + cy;
-    means[3 * o + 2] = dot3(m[6], m[7], m[8], lx, ly, lz) * s + cz;
-    const float* us = uscale + b * s_uscale + 3 * (int64_t)n;
-    for (int c = 0; c < 3; c++) scales[3 * o + c] = us[c] * s;
+    const float4 q = rotmat_to_unitquat(m);
+#pragma unroll
+    for (int k = 0; k < 9; k++) fr[k] = m[k];
+    fr[9] = (l1 + fabsf(dot3(a2x, a2y, a2z, e2x, e2y, e2z))) / 2.0f;
+    fr[10] = q.x; fr[11] = q.y; fr[12] = q.z; fr[13] = q.w;
+}
+
+constexpr int kDeformFrames = 8;  // frames per workgroup (GSR_DEFORM_FRAMES overrides, timing only)
+constexpr int kFrStride = 15;  // LDS floats per face frame (odd: conflict-free per-thread rows)
+
+// Vertex Gaussians (ubody_gaussian.py:252-254): xyz = LBS vertex, rotation =
+// normalize(q(T_v[:3,:3]) (x) q_v) in wxyz, scale unchanged.  UV Gaussians (:257-271): frame
+// [a0 a1 a2], scale s and q(frame) of the deformed binding face, centre = bary . face vertices,
+// xyz = (frame . local) * s + centre, rotation = q(frame) (x) q_uv (not renormalised), scale =
+// scale * s.
+//
+// One thread per Gaussian and fpw frames per workgroup: the frame-independent inputs (binding,
+// face vertex indices, barycentrics and, when shared, local offsets / rotations / scales) are read
+// once per workgroup instead of once per frame, which is most of the kernel's HBM traffic.  Face
+// frames are computed once per (face, frame) as the reference does: GUAVA's UV Gaussians come in
+// texel order, so a workgroup's 256 Gaussians bind a short run of faces, and the workgroup
+// computes that run's frames into LDS (one thread per face) for its Gaussians to read; a
+// workgroup whose faces span more than 256 ids computes per Gaussian (same function, same bits).
+__global__ __launch_bounds__(256) void k_deform_gaussians(
+    int B, int fpw, int V, int F, int N, const float* __restrict__ verts, const float* __restrict__ vtrans,
+    const int32_t* __restrict__ faces, const float* __restrict__ vrot, int64_t s_vrot,
+    const float* __restrict__ vscale, int64_t s_vscale, const int32_t* __restrict__ bind,
+    const float* __restrict__ bary, const float* __restrict__ lxyz, int64_t s_lxyz,
+    const float* __restrict__ urot, int64_t s_urot, const float* __restrict__ uscale,
+    int64_t s_uscale, float* __restrict__ means, float* __restrict__ rots, float* __restrict__ scales,
+    uint32_t* __restrict__ bad) {
+    __shared__ float fr_lds[256 * kFrStride];
+    __shared__ int range[2];
+    const int P = V + N;
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    const bool uv = i >= V && i < P;
+    const int n = i - V;
+    // binding resolved once (reference: an IndexError; here a flag and NaN outputs)
+    int f = -1, j0 = 0, j1 = 0, j2 = 0;
+    if (uv) {
+        const int bf = bind[n];
+        if (bf >= 0 && bf < F) {
+            const int a = faces[3 * bf], c = faces[3 * bf + 1], d = faces[3 * bf + 2];
+            if (a >= 0 && a < V && c >= 0 && c < V && d >= 0 && d < V) { f = bf; j0 = a; j1 = c; j2 = d; }
+        }
+        if (f < 0 && bad) atomicOr(bad, 1u);
+    }
+    float w0 = 0.f, w1 = 0.f, w2 = 0.f;
+    if (uv) { w0 = bary[3 * n]; w1 = bary[3 * n + 1]; w2 = bary[3 * n + 2]; }
+    // the workgroup's face run
+    if (threadIdx.x == 0) { range[0] = INT_MAX; range[1] = -1; }
+    __syncthreads();
+    if (f >= 0) { atomicMin(&range[0], f); atomicMax(&range[1], f); }
+    __syncthreads();
+    const int fmin = range[0], nf = range[1] - range[0] + 1;
+    const bool shared_frames = range[1] >= 0 && nf <= 256;
+    int t0 = -1, t1 = 0, t2 = 0;  // this thread's face in the run (shared mode)
+    if (shared_frames && (int)threadIdx.x < nf) {
+        const int ff = fmin + threadIdx.x;
+        const int a = faces[3 * ff], c = faces[3 * ff + 1], d = faces[3 * ff + 2];
+        if (a >= 0 && a < V && c >= 0 && c < V && d >= 0 && d < V) { t0 = a; t1 = c; t2 = d; }
+    }
+    const int b1 = min(B, (int)(blockIdx.y + 1) * fpw);
+    for (int b = blockIdx.y * fpw; b < b1; b++) {
+        const float* vb = verts + (int64_t)b * V * 3;
+        if (shared_frames) {
+            if (b > blockIdx.y * fpw) __syncthreads();  // the previous frame's readers are done
+            if (t0 >= 0) face_frame(vb, t0, t1, t2, fr_lds + threadIdx.x * kFrStride);
+            __syncthreads();
+        }
+        if (i >= P) continue;
+        const int64_t o = (int64_t)b * P + i;
+        if (i < V) {
+            const float4* tv = reinterpret_cast<const float4*>(vtrans + ((int64_t)b * V + i) * 16);
+            const float4 r0 = tv[0], r1 = tv[1], r2 = tv[2];
+            const float m[9] = {r0.x, r0.y, r0.z, r1.x, r1.y, r1.z, r2.x, r2.y, r2.z};
+            const float4 qd = rotmat_to_unitquat(m);
+            const float* qv = vrot + b * s_vrot + 4 * (int64_t)i;  // wxyz
+            const float4 q = quat_product(qd, make_float4(qv[1], qv[2], qv[3], qv[0]));
+            // F.normalize over the wxyz vector: x / max(||x||, 1e-12)
+            const float nn = fmaxf(sqrtf(((q.w * q.w + q.x * q.x) + q.y * q.y) + q.z * q.z), 1e-12f);
+            reinterpret_cast<float4*>(rots)[o] = make_float4(q.w / nn, q.x / nn, q.y / nn, q.z / nn);
+            for (int c = 0; c < 3; c++) {
+                means[3 * o + c] = vb[3 * i + c];
+                scales[3 * o + c] = vscale[b * s_vscale + 3 * (int64_t)i + c];
+            }
+            continue;
+        }
+        if (f < 0) {
+            const float nan = __int_as_float(0x7fc00000);
+            for (int c = 0; c < 3; c++) { means[3 * o + c] = nan; scales[3 * o + c] = nan; }
+            reinterpret_cast<float4*>(rots)[o] = make_float4(nan, nan, nan, nan);
+            continue;
+        }
+        float fr[14];
+        if (shared_frames) {
+            const float* src = fr_lds + (f - fmin) * kFrStride;
+#pragma unroll
+            for (int k = 0; k < 14; k++) fr[k] = src[k];
+        } else {
+            face_frame(vb, j0, j1, j2, fr);
+        }
+        const float s = fr[9];
+        const float* qu = urot + b * s_urot + 4 * (int64_t)n;  // wxyz
+        const float4 q = quat_product(make_float4(fr[10], fr[11], fr[12], fr[13]), make_float4(qu[1], qu[2], qu[3], qu[0]));
+        if (!GSR_DEFORM_NOSTORE || q.w == 12345.f) reinterpret_cast<float4*>(rots)[o] = make_float4(q.w, q.x, q.y, q.z);
+        const float* l = lxyz + b * s_lxyz + 3 * (int64_t)n;
+        const float lx = l[0], ly = l[1], lz = l[2];
+        const float cx = (w0 * vb[3 * j0] + w1 * vb[3 * j1]) + w2 * vb[3 * j2];
+        const float cy = (w0 * vb[3 * j0 + 1] + w1 * vb[3 * j1 + 1]) + w2 * vb[3 * j2 + 1];
+        const float cz = (w0 * vb[3 * j0 + 2] + w1 * vb[3 * j1 + 2]) + w2 * vb[3 * j2 + 2];
+        const float mx = dot3(fr[0], fr[1], fr[2], lx, ly, lz) * s + cx;
+        const float my = dot3(fr[3], fr[4], fr[5], lx, ly, lz) * s + cy;
+        const float mz = dot3(fr[6], fr[7], fr[8], lx, ly, lz) * s + cz;
+        const float* us = uscale + b * s_uscale + 3 * (int64_t)n;
+        if (!GSR_DEFORM_NOSTORE || mx == 12345.f) {
+            means[3 * o] = mx; means[3 * o + 1] = my; means[3 * o + 2] = mz;
+            for (int c = 0; c < 3; c++) scales[3 * o + c] = us[c] * s;
+        }
+    }
+}
+
+struct PackTable {
+    GsrRowSegment seg[GSR_PACK_MAX_SEGMENTS];
+};
+
+// gsr_pack_rows: one workgroup per (segment, frame); a row piece is at most a few hundred floats
+__global__ __launch_bounds__(256) void k_pack_rows(PackTable t) {
+    const GsrRowSegment sg = t.seg[blockIdx.x];
+    const int b = blockIdx.y;
+    for (int c = threadIdx.x; c < sg.width; c += 256)
+        sg.dst[b * sg.dst_stride + c] = sg.src ? sg.src[b * sg.src_stride + c] : 0.f;
 }
 
 namespace {
@@ -559,14 +774,10 @@ int gsr_lbs(int B, int V, int J, int NB, const float* v_template, int64_t v_temp
     hipLaunchKernelGGL(k_lbs_rodrigues, dim3((B * J + 255) / 256), dim3(256), 0, s, B, J, pose,
                        pose2rot, a.rot, a.feat);
     if (int rc = hip_check("lbs_rodrigues")) return rc;
-    const size_t lds = lbs_blend_lds(NB, NP);
-    if (lds > 160 * 1024) return api_fail(GSR_ERR_ARG, "gsr_lbs: NB + 9(J-1) too large for LDS");
-    lbs_blend_attr(lds);
-    hipLaunchKernelGGL(k_lbs_blend, lbs_blend_grid(M, B), dim3(64 * kLbsSplit),
-                       lds, s, B, M, NB, NP, v_template, v_template_stride, betas, shapedirs_t,
-                       a.feat, posedirs, vs, a.vp);
+    if (lbs_blend_lds(NB, NP) > 160 * 1024) return api_fail(GSR_ERR_ARG, "gsr_lbs: NB + 9(J-1) too large for LDS");
+    launch_blend(B, M, NB, NP, v_template, v_template_stride, betas, shapedirs_t, a.feat, posedirs, vs, a.vp, s);
     if (int rc = hip_check("lbs_blend")) return rc;
-    hipLaunchKernelGGL(k_lbs_joints, dim3(J, B), dim3(256), 0, s, V, J, J_regressor, vs,
+    hipLaunchKernelGGL(k_lbs_joints, dim3((J + kJointsPerWG - 1) / kJointsPerWG, B), dim3(256), 0, s, V, J, J_regressor, vs,
                        joints_offset, jr);
     if (int rc = hip_check("lbs_joints")) return rc;
     hipLaunchKernelGGL(k_lbs_chain, dim3(B), dim3(64), 0, s, J, par, a.rot, jr, joints_transformed, A);
@@ -587,16 +798,12 @@ int gsr_blend_joints(int B, int V, int J, int NB, const float* v_template, int64
     if (betas && (NB <= 0 || !shapedirs_t))
         return api_fail(GSR_ERR_ARG, "gsr_blend_joints: betas need NB > 0 and shapedirs");
     if (!betas) NB = 0;
-    const size_t lds = lbs_blend_lds(NB, 0);
-    if (lds > 160 * 1024) return api_fail(GSR_ERR_ARG, "gsr_blend_joints: NB too large for LDS");
-    lbs_blend_attr(lds);
+    if (lbs_blend_lds(NB, 0) > 160 * 1024) return api_fail(GSR_ERR_ARG, "gsr_blend_joints: NB too large for LDS");
     hipStream_t s = (hipStream_t)stream;
     const int M = V * 3;
-    hipLaunchKernelGGL(k_lbs_blend, lbs_blend_grid(M, B), dim3(64 * kLbsSplit),
-                       lds, s, B, M, NB, 0, v_template, v_template_stride, betas, shapedirs_t,
-                       nullptr, nullptr, v_shaped, nullptr);
+    launch_blend(B, M, NB, 0, v_template, v_template_stride, betas, shapedirs_t, nullptr, nullptr, v_shaped, nullptr, s);
     if (int rc = hip_check("blend_shapes")) return rc;
-    hipLaunchKernelGGL(k_lbs_joints, dim3(J, B), dim3(256), 0, s, V, J, J_regressor, v_shaped,
+    hipLaunchKernelGGL(k_lbs_joints, dim3((J + kJointsPerWG - 1) / kJointsPerWG, B), dim3(256), 0, s, V, J, J_regressor, v_shaped,
                        joints_offset, joints);
     return hip_check("vertices2joints");
 }
@@ -621,6 +828,21 @@ int gsr_splice_head(int B, int V_body, int N_head, const int32_t* head_index, co
     return hip_check("splice_head");
 }
 
+int gsr_pack_rows(int B, int nseg, const GsrRowSegment* segs, void* stream) {
+    if (B <= 0 || nseg < 0 || nseg > GSR_PACK_MAX_SEGMENTS) return api_fail(GSR_ERR_ARG, "gsr_pack_rows: bad sizes");
+    if (nseg == 0) return 0;
+    if (!segs) return api_fail(GSR_ERR_ARG, "gsr_pack_rows: null segment table");
+    PackTable t;
+    for (int i = 0; i < nseg; i++) {
+        t.seg[i] = segs[i];
+        if (!segs[i].dst || segs[i].width < 0 || segs[i].width > 4096 || segs[i].dst_stride < segs[i].width ||
+            segs[i].src_stride < 0)
+            return api_fail(GSR_ERR_ARG, "gsr_pack_rows: bad segment");
+    }
+    hipLaunchKernelGGL(k_pack_rows, dim3(nseg, B), dim3(256), 0, (hipStream_t)stream, t);
+    return hip_check("pack_rows");
+}
+
 int gsr_deform_gaussians(int B, int V, int F, int N, const float* verts,
                          const float* vert_transforms, const int32_t* faces,
                          const float* vtx_rotations, int64_t vtx_rot_stride,
@@ -636,15 +858,21 @@ int gsr_deform_gaussians(int B, int V, int F, int N, const float* verts,
         return api_fail(GSR_ERR_ARG, "gsr_deform_gaussians: null required pointer");
     if (V > 0 && (!vert_transforms || !vtx_rotations || !vtx_scales))
         return api_fail(GSR_ERR_ARG, "gsr_deform_gaussians: vertex Gaussians need transforms, rotations, scales");
-    if (N > 0 && (!faces || !binding_face || !face_bary || !local_xyz || !uv_rotations || !uv_scales))
+    if (N > 0 && (!faces || !binding_face || !face_bary || !local_xyz || !uv_rotations || !uv_scales || F == 0))
         return api_fail(GSR_ERR_ARG, "gsr_deform_gaussians: UV Gaussians need faces and binding data");
     auto bad_stride = [](int64_t st, int64_t full) { return st != 0 && st != full; };
     if (bad_stride(vtx_rot_stride, 4LL * V) || bad_stride(vtx_scale_stride, 3LL * V) ||
         bad_stride(local_stride, 3LL * N) || bad_stride(uv_rot_stride, 4LL * N) ||
         bad_stride(uv_scale_stride, 3LL * N))
         return api_fail(GSR_ERR_ARG, "gsr_deform_gaussians: strides must be 0 or a whole frame");
+    hipStream_t s = (hipStream_t)stream;
+    static const int fpw = [] {
+        const char* e = getenv("GSR_DEFORM_FRAMES");
+        const int v = e ? atoi(e) : kDeformFrames;
+        return v >= 1 && v <= 64 ? v : 1;
+    }();
     const int P = V + N;
-    hipLaunchKernelGGL(k_deform_gaussians, dim3((P + 255) / 256, B), dim3(256), 0, (hipStream_t)stream,
+    hipLaunchKernelGGL(k_deform_gaussians, dim3((P + 255) / 256, (B + fpw - 1) / fpw), dim3(256), 0, s, B, fpw,
                        V, F, N, verts, vert_transforms, faces, vtx_rotations, vtx_rot_stride, vtx_scales,
                        vtx_scale_stride, binding_face, face_bary, local_xyz, local_stride, uv_rotations,
                        uv_rot_stride, uv_scales, uv_scale_stride, means3D, rotations, scales,

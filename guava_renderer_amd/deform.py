@@ -142,6 +142,44 @@ def lbs_wobeta(pose, v_shaped, posedirs, J_regressor, parents, lbs_weights, join
                     joints_offset, pose2rot, True)
 
 
+def _seg(segs, dst, col, t, B, width=None):
+    """Queue a gsr_pack_rows segment: columns [col, col + width) of dst [B, W] from t, a [B, ...] or
+    [1, ...] tensor (one row per frame, or one row broadcast); t None leaves the columns to the zero
+    fill."""
+    if t is None:
+        return
+    t = _f32(t)
+    rows = t.reshape(t.shape[0], -1) if t.dim() > 1 else t.reshape(1, -1)  # 1-D: one broadcast row
+    if rows.shape[0] not in (1, B):
+        raise RuntimeError(f"parameter batch {rows.shape[0]} does not match the frame batch {B}")
+    w = rows.shape[1] if width is None else width
+    if w > rows.shape[1] or col + w > dst.shape[1]:
+        raise RuntimeError(f"parameter of width {rows.shape[1]} does not fit columns [{col}, {col + w}) "
+                           f"of a {dst.shape[1]}-wide coefficient row")
+    _dev_check(rows)
+    segs.append((rows, dst, col, w, 0 if rows.shape[0] == 1 else rows.stride(0)))
+
+
+def _fill_zeros(segs, dsts, B):
+    """The segment table: every queued copy plus a zero segment for each column run no copy covers."""
+    table = []
+    for rows, dst, col, w, sstr in segs:
+        if w > 0:
+            table.append(_lib.RowSegment(rows.data_ptr(), dst.data_ptr() + 4 * col, sstr, dst.stride(0), w, 0))
+    for dst in dsts:
+        covered = sorted((col, col + w) for _, d, col, w, _ in segs if d is dst and w > 0)
+        c = 0
+        for a, e in covered + [(dst.shape[1], dst.shape[1])]:
+            if a < c:
+                raise RuntimeError("overlapping coefficient segments")
+            if a > c:
+                table.append(_lib.RowSegment(None, dst.data_ptr() + 4 * c, 0, dst.stride(0), a - c, 0))
+            c = max(c, e)
+    if len(table) > 16:
+        raise RuntimeError("too many coefficient segments for one gsr_pack_rows launch")
+    return table
+
+
 class GaussianDeformer:
     """The Gaussian half of Ubody_Gaussian (ubody_gaussian.py:162-289) over precomputed LBS output.
 
@@ -209,8 +247,8 @@ class GaussianDeformer:
 class EHMDeformer:
     """EHM.forward (models/modules/ehm/EHM.py:36-156) for B frames on the GPU: FLAME head lbs ->
     eyelids and head scale -> body blend shapes and joints -> head splice -> body lbs_wobeta, with
-    every per-frame step a gfx950 kernel (gsr_lbs, gsr_blend_joints, gsr_splice_head) and no host
-    synchronisation.
+    every per-frame step a gfx950 kernel (gsr_pack_rows, gsr_lbs, gsr_blend_joints, gsr_splice_head)
+    and no host synchronisation or torch glue launches.
 
     body / flame: dicts of the LBS assets in the reference layouts (v_template [V,3], shapedirs
     [V,3,NB], posedirs, J_regressor, parents, lbs_weights); smplx2flame_ind [Nh] (SMPLX.py:191);
@@ -235,19 +273,12 @@ class EHMDeformer:
         self._ws = {}
 
     def _workspace(self, B, V, J, NB):
-        key = (B, V, J, NB)
+        # one per stream: batches in flight on different streams must not share scratch
+        key = (B, V, J, NB, torch.cuda.current_stream(self.dev).cuda_stream)
         if key not in self._ws:
             n = _lib.load().gsr_lbs_workspace_bytes(B, V, J, NB)
             self._ws[key] = torch.empty((n,), dtype=torch.uint8, device=self.dev)
         return self._ws[key]
-
-    def _zeros(self, B, n):
-        """A cached [B, n] zero block (the padding of the coefficient rows)."""
-        zs = self.__dict__.setdefault("_zero_blocks", {})
-        z = zs.get((B, n))
-        if z is None:
-            z = zs[(B, n)] = torch.zeros((B, n), dtype=torch.float32, device=self.dev)
-        return z
 
     def forward(self, body_param_dict, flame_param_dict):
         L = _lib.load()
@@ -258,28 +289,46 @@ class EHMDeformer:
         fa, ba = self.flame, self.body
         B = fp["shape_params"].shape[0]
         o = dict(dtype=torch.float32, device=self.dev)
-        # FLAME head (EHM.py:41-75): betas = shape ++ expression; pose = 0 global, 0 neck, jaw, eyes
         Vh, Jh, NBh = fa["J_regressor"].shape[1], fa["J_regressor"].shape[0], fa["shapedirs"].shape[2]
-        # each coefficient row is ONE cat (cached zero blocks, no fill launches per frame batch)
-        shp_h, exp_h = _f32(fp["shape_params"]), _f32(fp["expression_params"])
-        pad_h = NBh - shp_h.shape[1] - exp_h.shape[1]
-        betas_h = torch.cat([shp_h, exp_h] + ([self._zeros(B, pad_h)] if pad_h > 0 else []), 1)
-        pose_h = torch.cat([self._zeros(B, 6), _f32(fp["jaw_params"]).reshape(B, 3),
-                            _f32(fp["eye_pose_params"]).reshape(B, 6)], 1).contiguous()
+        Vb, Jb, NBb = ba["J_regressor"].shape[1], ba["J_regressor"].shape[0], ba["shapedirs"].shape[2]
+        # the coefficient rows of both LBS calls, assembled by ONE gsr_pack_rows launch (the
+        # reference's torch.cat / zeros / expand glue): FLAME betas = shape ++ expression ++ 0 and
+        # pose = 0 global, 0 neck, jaw, eyes (EHM.py:41-48); SMPL-X shape (cut or zero-padded to
+        # n_shape) ++ exp (:101-106); body pose = global, body, 0 jaw, 0 eyes, hands (:94-112)
+        hs = bp.get("head_scale")
+        widths = (NBh, 3 * Jh, NBb, 3 * Jb, 3 if hs is not None else 0)
+        buf = torch.empty((sum(widths) * B,), **o)
+        views, off = [], 0
+        for w in widths:
+            views.append(buf[off:off + B * w].view(B, w))
+            off += B * w
+        betas_h, pose_h, sc, pose, hsb = views
+        segs = []
+        _seg(segs, betas_h, 0, fp["shape_params"], B)
+        _seg(segs, betas_h, fp["shape_params"].shape[-1], fp["expression_params"], B)
+        _seg(segs, pose_h, 6, fp["jaw_params"], B)
+        _seg(segs, pose_h, 9, fp["eye_pose_params"], B)
+        n_shape = NBb - bp["exp"].shape[-1]
+        _seg(segs, sc, 0, bp["shape"], B, width=min(n_shape, bp["shape"].shape[-1]))
+        _seg(segs, sc, n_shape, bp["exp"], B)
+        _seg(segs, pose, 0, bp.get("global_pose"), B, width=3)
+        _seg(segs, pose, 3, bp.get("body_pose"), B, width=63)
+        _seg(segs, pose, 75, bp["left_hand_pose"], B)
+        _seg(segs, pose, 120, bp["right_hand_pose"], B)
+        if hs is not None:
+            _seg(segs, hsb, 0, hs, B)
+        table = _fill_zeros(segs, views, B)
+        _lib.check(L.gsr_pack_rows(B, len(table), (_lib.RowSegment * len(table))(*table), st), "gsr_pack_rows")
+        # FLAME head (EHM.py:41-75)
         hv = torch.empty((B, Vh, 3), **o)
         hj = torch.empty((B, Jh, 3), **o)
-        rc = L.gsr_lbs(B, Vh, Jh, NBh, _ptr(fa["v_template"]), 0, _ptr(betas_h.contiguous()),
+        rc = L.gsr_lbs(B, Vh, Jh, NBh, _ptr(fa["v_template"]), 0, _ptr(betas_h),
                        _ptr(fa["shapedirs_t"]), _ptr(pose_h), 1, _ptr(fa["posedirs"]),
                        _ptr(fa["J_regressor"]), fa["parents"].ctypes.data_as(ctypes.c_void_p),
                        _ptr(fa["lbs_weights_t"]), None, _ptr(hv), _ptr(hj), None, None, None, None,
                        _ptr(self._workspace(B, Vh, Jh, NBh)), st)
         _lib.check(rc, "gsr_lbs (FLAME head)")
         # body template (EHM.py:101-118): blend shapes of shape ++ exp, regressed joints + offset
-        Vb, Jb, NBb = ba["J_regressor"].shape[1], ba["J_regressor"].shape[0], ba["shapedirs"].shape[2]
-        n_shape = NBb - bp["exp"].shape[1]  # EHM.py:101-106: pad or cut shape to n_shape, then ++ exp
-        shp = _f32(bp["shape"])[:, :n_shape]
-        pad_b = n_shape - shp.shape[1]
-        sc = torch.cat([shp] + ([self._zeros(B, pad_b)] if pad_b > 0 else []) + [_f32(bp["exp"])], 1).contiguous()
         joff = _f32(bp["joints_offset"]) if bp.get("joints_offset") is not None else None
         vt = torch.empty((B, Vb, 3), **o)
         tj = torch.empty((B, Jb, 3), **o)
@@ -288,17 +337,10 @@ class EHMDeformer:
                                       _ptr(vt), _ptr(tj), st), "gsr_blend_joints")
         # head splice (EHM.py:72-75, 121-124)
         eyelid = _f32(fp["eyelid_params"]) if fp.get("eyelid_params") is not None else None
-        hs = bp.get("head_scale")
-        hs = _f32(hs).expand(B, 3).contiguous() if hs is not None else None
         _lib.check(L.gsr_splice_head(B, Vb, Vh, _ptr(self.head_index), _ptr(hv), _ptr(self.r_eyelid),
-                                     _ptr(self.l_eyelid), _ptr(eyelid), _ptr(hs), _ptr(hj), Jh,
+                                     _ptr(self.l_eyelid), _ptr(eyelid), _ptr(hsb) if hs is not None else None, _ptr(hj), Jh,
                                      self.HEAD_REF[0], self.HEAD_REF[1], _ptr(tj), Jb, self.BODY_REF[0],
                                      self.BODY_REF[1], _ptr(vt), _ptr(self.bad), st), "gsr_splice_head")
-        # body pose (EHM.py:94-112): global, body, jaw = 0, eyes = 0, hands
-        gp = _f32(bp["global_pose"]).reshape(B, 3) if bp.get("global_pose") is not None else self._zeros(B, 3)
-        bpose = _f32(bp["body_pose"]).reshape(B, 63) if bp.get("body_pose") is not None else self._zeros(B, 63)
-        pose = torch.cat([gp, bpose, self._zeros(B, 9), _f32(bp["left_hand_pose"]).reshape(B, 45),
-                          _f32(bp["right_hand_pose"]).reshape(B, 45)], 1).reshape(B, 55, 3).contiguous()
         verts = torch.empty((B, Vb, 3), **o)
         jt2 = torch.empty((B, Jb, 3), **o)
         J = torch.empty((B, Jb, 3), **o)

@@ -14,6 +14,7 @@
  *   gsr_blend_joints     <- blend_shapes + vertices2joints (lbs.py:355-376, :335-352), the body
  *                           template step of EHM.forward (EHM.py:114-118)
  *   gsr_splice_head      <- EHM.forward's FLAME-head splice (EHM.py:72-75, :121-124)
+ *   gsr_pack_rows        <- the torch.cat coefficient-row glue of EHM.forward (EHM.py:41-48, :94-112)
  *   gsr_deform_gaussians <- the Gaussian part of Ubody_Gaussian.forward
  *                           UbodyAvatar/ubody_gaussian.py:252-278: vertex Gaussians
  *                           (rotmat_to_unitquat of the per-vertex skinning matrix, quat_product,
@@ -81,6 +82,24 @@ int gsr_splice_head(int B, int V_body, int N_head, const int32_t* head_index, co
                     const float* body_joints, int J_body, int bj0, int bj1, float* body_v_shaped,
                     uint32_t* bad_index_flag, void* stream);
 
+/* One segment of gsr_pack_rows: for every frame b, dst[b * dst_stride + c] = src[b * src_stride + c]
+ * for c in [0, width) (src == NULL writes zeros; src_stride 0 broadcasts one row to every frame). */
+typedef struct {
+    const float* src;
+    float* dst;
+    int64_t src_stride;
+    int64_t dst_stride;
+    int32_t width;
+    int32_t pad_;
+} GsrRowSegment;
+#define GSR_PACK_MAX_SEGMENTS 16
+
+/* Assembles per-frame coefficient rows from pieces in ONE launch: the torch.cat / zeros / expand
+ * glue of EHM.forward (EHM.py:41-48 FLAME betas and pose, :94-112 SMPL-X shape ++ expression and
+ * the 55-joint pose with zero jaw/eyes, head_scale's broadcast).  nseg <= GSR_PACK_MAX_SEGMENTS,
+ * width <= 4096; segments must not overlap. */
+int gsr_pack_rows(int B, int nseg, const GsrRowSegment* segs, void* stream);
+
 /* Ubody_Gaussian.forward's Gaussian assembly for B frames; P = V + N Gaussians per frame, the V
  * vertex Gaussians first.
  *   verts [B,V,3], vert_transforms [B,V,16] (from gsr_lbs), faces [F,3] int32.
@@ -90,7 +109,9 @@ int gsr_splice_head(int B, int V_body, int N_head, const int32_t* head_index, co
  * Outputs: means3D [B,P,3], rotations [B,P,4] wxyz, scales [B,P,3].  Indices are validated on the
  * device: an out-of-range binding face or face-vertex index ORs 1 into *bad_index_flag (a device
  * uint32, may be NULL) and writes NaN for that Gaussian instead of reading out of range (the
- * reference raises IndexError). */
+ * reference raises IndexError).  compute_face_orientation runs once per (face, frame) as in the
+ * reference when a 256-Gaussian block's bindings span at most 256 consecutive faces (GUAVA's texel
+ * order), else once per bound Gaussian; the results are the same. */
 int gsr_deform_gaussians(int B, int V, int F, int N, const float* verts,
                          const float* vert_transforms, const int32_t* faces,
                          const float* vtx_rotations, int64_t vtx_rot_stride,

@@ -142,6 +142,9 @@ def test_deform_abi_validates_before_touching_memory():
     rc = L.gsr_deform_gaussians(1, 4, 2, 3, bogus, bogus, None, bogus, 0, bogus, 0, None, None, None,
                                 0, None, 0, None, 0, bogus, bogus, bogus, None, None)
     assert rc == -1 and b"UV Gaussians" in L.gsr_last_error()
+    seg = (_lib.RowSegment * 1)(_lib.RowSegment(None, None, 0, 4, 4, 0))
+    rc = L.gsr_pack_rows(2, 1, seg, None)
+    assert rc == -1 and b"bad segment" in L.gsr_last_error()
     with pytest.raises(RuntimeError, match="GPU only"):
         deform.lbs_wobeta(torch.zeros(1, 3, 3), torch.zeros(1, 4, 3), torch.zeros(18, 12),
                           torch.zeros(3, 4), torch.tensor([-1, 0, 1]), torch.zeros(4, 3))

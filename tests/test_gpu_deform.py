@@ -150,3 +150,52 @@ def test_ehm_forward_then_gaussians_match_oracle():
     for k in ("vertices", "joints", "joints_transform", "ver_transform_mat", "joint_transform_mat"):
         np.testing.assert_allclose(out[k].cpu().numpy(), ref[k], atol=ATOL, rtol=0, err_msg=k)
     assert int(ehm.bad.item()) == 0
+
+
+def test_ehm_forward_large_batch_matrix_core_blend():
+    """B=40 frames: the blend shapes run on the matrix-core kernel (k_lbs_blend_mfma, more than 16
+    frames), one full 32-frame tile and one partial tile; V*3 = 31,425 is not a multiple of the
+    32-coordinate tile either."""
+    from guava_renderer_amd import avatar, deform
+    body, flame, extra = avatar.ehm_assets(seed=0)
+    bp, fp = avatar.ehm_params(40, seed=2000)
+    ehm = deform.EHMDeformer(body, flame, extra["smplx2flame_ind"], extra["l_eyelid"], extra["r_eyelid"],
+                             device=DEV)
+    out = ehm({k: _t(v) for k, v in bp.items()}, {k: _t(v) for k, v in fp.items()})
+    ref = lo.ehm_forward(body, flame, extra, bp, fp)
+    for k in ("vertices", "joints", "joints_transform", "ver_transform_mat", "joint_transform_mat"):
+        np.testing.assert_allclose(out[k].cpu().numpy(), ref[k], atol=ATOL, rtol=0, err_msg=k)
+
+
+def test_ehm_broadcast_and_absent_params():
+    """The coefficient-row packing (gsr_pack_rows): a one-row identity shape and head_scale broadcast
+    over the frames, an absent global_pose (zero rows, EHM.py:94-96) -- against the oracle given the
+    explicit equivalents."""
+    from guava_renderer_amd import avatar, deform
+    body, flame, extra = avatar.ehm_assets(seed=0)
+    bp, fp = avatar.ehm_params(5, seed=3000)
+    ehm = deform.EHMDeformer(body, flame, extra["smplx2flame_ind"], extra["l_eyelid"], extra["r_eyelid"],
+                             device=DEV)
+    gbp = {k: _t(v) for k, v in bp.items()}
+    gbp["shape"] = _t(bp["shape"][:1])
+    gbp["head_scale"] = _t(bp["head_scale"][0])
+    del gbp["global_pose"]
+    out = ehm(gbp, {k: _t(v) for k, v in fp.items()})
+    rbp = dict(bp)
+    rbp["head_scale"] = np.broadcast_to(bp["head_scale"][:1], bp["head_scale"].shape)
+    rbp["global_pose"] = np.zeros_like(bp["global_pose"])
+    ref = lo.ehm_forward(body, flame, extra, rbp, fp)
+    for k in ("vertices", "joints", "ver_transform_mat"):
+        np.testing.assert_allclose(out[k].cpu().numpy(), ref[k], atol=ATOL, rtol=0, err_msg=k)
+
+
+def test_lbs_with_betas_b17_matrix_core_tails():
+    """deform.lbs at B=17 (a partial 32-frame tile) on the SMPL-X-size model, vs the oracle."""
+    from guava_renderer_amd import deform
+    m, g, faces, betas, pose = _full_avatar(B=17, P=20000)
+    verts, jt = deform.lbs(_t(betas), _t(pose), _t(m["v_template"]), _t(m["shapedirs"]), _t(m["posedirs"]),
+                           _t(m["J_regressor"]), torch.from_numpy(m["parents"]), _t(m["lbs_weights"]))
+    r_verts, r_jt, *_ = lo.lbs(betas, pose, m["v_template"], m["shapedirs"], m["posedirs"],
+                               m["J_regressor"], m["parents"], m["lbs_weights"])
+    np.testing.assert_allclose(verts.cpu().numpy(), r_verts, atol=ATOL, rtol=0)
+    np.testing.assert_allclose(jt.cpu().numpy(), r_jt, atol=ATOL, rtol=0)
