@@ -11,8 +11,9 @@ LIB_PATH = os.path.join(HERE, "lib", "libgsr.so")
 # every symbol declared in include/*.h
 EXPORTS = ("gsr_version", "gsr_last_error", "gsr_set_exact_exp", "gsr_set_split_bf16", "gsr_geometry_bytes",
            "gsr_image_bytes", "gsr_binning_bytes", "gsr_mark_visible", "gsr_forward",
+           "gsr_forward_async_bound", "gsr_forward_async",
            "gsr_backward", "gsr_batch_workspace_bytes", "gsr_forward_batch",
-           "gsr_backward_batch", "gsr_batch_status", "gsr_profile_enable", "gsr_profile_read",
+           "gsr_backward_batch", "gsr_backward_batch_shared", "gsr_batch_status", "gsr_profile_enable", "gsr_profile_read",
            "gsr_render_counters", "gsr_render_timeline", "gsr_forward_batch_refine",
            "gsr_refine_prepare", "gsr_batch_status_offset",
            # include/gsr_deform.h
@@ -95,6 +96,10 @@ def load(path=None):
                               _vp, _vp, _vp, _f, _vp, _vp, _vp, _vp, _vp, _f, _f, _i, _vp, _vp, _i,
                               _vp, _i, _vp]
     L.gsr_forward.restype = _i
+    L.gsr_forward_async_bound.argtypes = [_i, _i, _i]
+    L.gsr_forward_async_bound.restype = _i64
+    L.gsr_forward_async.argtypes = list(L.gsr_forward.argtypes[:-1]) + [_vp, _vp]
+    L.gsr_forward_async.restype = _i
     L.gsr_backward.argtypes = [_i, _i, _i, _i, _vp, _i, _i, _vp, _vp, _vp, _vp, _vp, _f, _vp, _vp,
                                _vp, _vp, _vp, _f, _f, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp,
                                _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i, _i, _vp]
@@ -116,6 +121,9 @@ def load(path=None):
                                      _i64, _f, _vp, _vp, _vp, _vp, _i64, _vp, _i64, _vp, _vp, _vp, _vp,
                                      _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i, _vp]
     L.gsr_backward_batch.restype = _i
+    L.gsr_backward_batch_shared.argtypes = list(L.gsr_backward_batch.argtypes[:24]) + [_vp, _vp, _vp, _vp, _vp,
+                                                                                       _i, _vp]
+    L.gsr_backward_batch_shared.restype = _i
     L.gsr_batch_status.argtypes = [_vp, _i, _i, ctypes.POINTER(_i64), ctypes.POINTER(_i), _vp]
     L.gsr_batch_status.restype = _i
     L.gsr_profile_enable.argtypes = [ctypes.c_uint32]

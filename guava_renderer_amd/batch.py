@@ -184,16 +184,14 @@ class BatchRasterizer:
 
     def backward(self, means3D, colors, opacities, scales, rotations, viewmatrices, projmatrices,
                  tanfov, backgrounds, dL_dcolor, dL_dinvdepth=None, scale_modifier=1.0,
-                 antialiasing=False):
+                 antialiasing=False, shared=False):
         """Gradients of the last forward, per frame: dict of [B,P,k] tensors (all zero when that
-        forward overflowed the capacity; the overflow is reported by the next forward / poll)."""
+        forward overflowed the capacity; the overflow is reported by the next forward / poll).
+        shared=True (attributes shared by every frame, e.g. one avatar under B cameras): the
+        attribute gradients summed over the frames instead, dict of [P,k] tensors (means3D, colors,
+        opacity, scales, rotations) -- gsr_backward_batch_shared, no [B,P,k] buffers."""
         B, P = self.B, self.P
         o = dict(dtype=torch.float32, device=self.device)
-        g = dict(mean2D=torch.zeros((B, P, 3), **o), conic=torch.zeros((B, P, 4), **o),
-                 opacity=torch.zeros((B, P, 1), **o), colors=torch.zeros((B, P, C), **o),
-                 invdepth=torch.zeros((B, P, 1), **o) if dL_dinvdepth is not None else None,
-                 means3D=torch.zeros((B, P, 3), **o), cov3D=torch.zeros((B, P, 6), **o),
-                 scales=torch.zeros((B, P, 3), **o), rotations=torch.zeros((B, P, 4), **o))
         keep, head, (v, pm, tf, bg, bs) = self._inputs(means3D, colors, opacities, scales, rotations,
                                                        viewmatrices, projmatrices, tanfov, backgrounds)
         if tuple(dL_dcolor.shape) != (B, C, self.H, self.W):
@@ -204,6 +202,23 @@ class BatchRasterizer:
             if dL_dinvdepth.numel() != B * self.H * self.W:
                 raise ValueError("dL_dinvdepth: expected [B,H,W]")
             dLi = dL_dinvdepth.to(torch.float32).contiguous()
+        if shared:
+            g = dict(colors=torch.zeros((P, C), **o), opacity=torch.empty((P, 1), **o),
+                     means3D=torch.empty((P, 3), **o), scales=torch.empty((P, 3), **o),
+                     rotations=torch.empty((P, 4), **o))
+            rc = self.L.gsr_backward_batch_shared(
+                *head, float(scale_modifier), v, pm, tf, bg, bs, self.workspace.data_ptr(), self.R_capacity,
+                dLc.data_ptr(), dLi.data_ptr() if dLi is not None else None, g["opacity"].data_ptr(),
+                g["colors"].data_ptr(), g["means3D"].data_ptr(), g["scales"].data_ptr(),
+                g["rotations"].data_ptr(), int(bool(antialiasing)), self._stream())
+            _lib.check(rc, "gsr_backward_batch_shared")
+            del keep
+            return g
+        g = dict(mean2D=torch.zeros((B, P, 3), **o), conic=torch.zeros((B, P, 4), **o),
+                 opacity=torch.zeros((B, P, 1), **o), colors=torch.zeros((B, P, C), **o),
+                 invdepth=torch.zeros((B, P, 1), **o) if dL_dinvdepth is not None else None,
+                 means3D=torch.zeros((B, P, 3), **o), cov3D=torch.zeros((B, P, 6), **o),
+                 scales=torch.zeros((B, P, 3), **o), rotations=torch.zeros((B, P, 4), **o))
         rc = self.L.gsr_backward_batch(
             *head, float(scale_modifier), v, pm, tf, bg, bs, self.workspace.data_ptr(), self.R_capacity,
             dLc.data_ptr(), dLi.data_ptr() if dLi is not None else None,

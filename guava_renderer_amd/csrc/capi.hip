@@ -223,6 +223,13 @@ size_t gsr_image_bytes(int width, int height) {
 }
 size_t gsr_binning_bytes(int64_t R) { return carve_bin(nullptr, R, nullptr); }
 
+// Instances one frame can produce at most: every Gaussian in every tile (getRect clamps to the
+// grid), capped at the int range of num_rendered.
+static int64_t async_bound(const Dims& d) {
+    const int64_t b = (int64_t)d.P * d.T;
+    return b < 0x7FFFFFFFll ? b : 0x7FFFFFFFll;
+}
+
 int gsr_mark_visible(int P, const float* means3D, const float* viewmatrix, const float* projmatrix,
                      uint8_t* present, void* stream) {
     if (P < 0) return fail(GSR_ERR_ARG, "P < 0");
@@ -232,16 +239,19 @@ int gsr_mark_visible(int P, const float* means3D, const float* viewmatrix, const
     return 0;
 }
 
-int gsr_forward(gsr_alloc_fn geometryBuffer, gsr_alloc_fn binningBuffer, gsr_alloc_fn imageBuffer,
-                void* alloc_ctx, int P, int D, int M, const float* background, int width, int height,
-                const float* means3D, const float* shs, const float* colors_precomp,
-                const float* opacities, const float* scales, float scale_modifier,
-                const float* rotations, const float* cov3D_precomp, const float* viewmatrix,
-                const float* projmatrix, const float* cam_pos, float tan_fovx, float tan_fovy,
-                int prefiltered, float* out_color, float* depth, int antialiasing, int* radii,
-                int debug, void* stream) {
+// status_host == nullptr: the reference's synchronous contract (R read back after the scan, the
+// binning buffer sized to R, num_rendered returned).  Otherwise the binning buffer is sized to
+// the upper bound P x tiles (R cannot exceed it), nothing waits on the device, and the control
+// words {R, overflow, error flags, 0} are copied to status_host (pinned) at the end of the stream.
+static int forward_single(gsr_alloc_fn geometryBuffer, gsr_alloc_fn binningBuffer, gsr_alloc_fn imageBuffer,
+                          void* alloc_ctx, int P, int D, int M, const float* background, int width, int height,
+                          const float* means3D, const float* shs, const float* colors_precomp,
+                          const float* opacities, const float* scales, float scale_modifier,
+                          const float* rotations, const float* cov3D_precomp, const float* viewmatrix,
+                          const float* projmatrix, const float* cam_pos, float tan_fovx, float tan_fovy,
+                          int prefiltered, float* out_color, float* depth, int antialiasing, int* radii,
+                          int debug, uint32_t* status_host, hipStream_t s) {
     (void)D; (void)M; (void)shs; (void)cam_pos;
-    hipStream_t s = (hipStream_t)stream;
     if (P < 0 || width <= 0 || height <= 0) return fail(GSR_ERR_ARG, "bad P/width/height");
     if (P >= kMaxGaussians) return fail(GSR_ERR_ARG, "P must be < 2^24");
     if ((int64_t)((width + 15) / 16) * ((height + 15) / 16) > kMaxTiles) return fail(GSR_ERR_ARG, "image too large");
@@ -279,6 +289,19 @@ int gsr_forward(gsr_alloc_fn geometryBuffer, gsr_alloc_fn binningBuffer, gsr_all
     HIP_TRY(hipMemsetAsync(g.bstart, 0, (size_t)d.B * (d.NB + 1) * 4, s));
     { StageTimer st_(0, s); launch_preprocess(d, in, g, o, s); }
     STAGE(debug, s, "preprocess");
+    if (status_host) {
+        const int64_t cap = async_bound(d);
+        { StageTimer st_(1, s); launch_scan_blocksums(d, g, cap, s); }
+        STAGE(debug, s, "scan");
+        char* bb = binningBuffer(alloc_ctx, carve_bin(nullptr, cap, nullptr));
+        if (!bb) return fail(GSR_ERR_ALLOC, "binningBuffer allocation failed");
+        BinArena bn;
+        carve_bin(bb, cap, &bn);
+        int rc = run_binning_and_render(d, in, g, im, bn, o, debug, s);
+        if (rc < 0) return rc;
+        HIP_TRY(hipMemcpyAsync(status_host, g.ctrl, 4 * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+        return 0;
+    }
     { StageTimer st_(1, s); launch_scan_blocksums(d, g, (int64_t)0xFFFFFFF0u, s); }
     STAGE(debug, s, "scan");
     uint32_t ctrl_h[4] = {0, 0, 0, 0};
@@ -296,6 +319,41 @@ int gsr_forward(gsr_alloc_fn geometryBuffer, gsr_alloc_fn binningBuffer, gsr_all
     int rc = run_binning_and_render(d, in, g, im, bn, o, debug, s);
     if (rc < 0) return rc;
     return (int)R;
+}
+
+int gsr_forward(gsr_alloc_fn geometryBuffer, gsr_alloc_fn binningBuffer, gsr_alloc_fn imageBuffer,
+                void* alloc_ctx, int P, int D, int M, const float* background, int width, int height,
+                const float* means3D, const float* shs, const float* colors_precomp,
+                const float* opacities, const float* scales, float scale_modifier,
+                const float* rotations, const float* cov3D_precomp, const float* viewmatrix,
+                const float* projmatrix, const float* cam_pos, float tan_fovx, float tan_fovy,
+                int prefiltered, float* out_color, float* depth, int antialiasing, int* radii,
+                int debug, void* stream) {
+    return forward_single(geometryBuffer, binningBuffer, imageBuffer, alloc_ctx, P, D, M, background, width,
+                          height, means3D, shs, colors_precomp, opacities, scales, scale_modifier, rotations,
+                          cov3D_precomp, viewmatrix, projmatrix, cam_pos, tan_fovx, tan_fovy, prefiltered,
+                          out_color, depth, antialiasing, radii, debug, nullptr, (hipStream_t)stream);
+}
+
+int64_t gsr_forward_async_bound(int P, int width, int height) {
+    if (P <= 0 || width <= 0 || height <= 0) return 0;
+    return async_bound(make_dims(1, P, width, height));
+}
+
+int gsr_forward_async(gsr_alloc_fn geometryBuffer, gsr_alloc_fn binningBuffer, gsr_alloc_fn imageBuffer,
+                      void* alloc_ctx, int P, int D, int M, const float* background, int width, int height,
+                      const float* means3D, const float* shs, const float* colors_precomp,
+                      const float* opacities, const float* scales, float scale_modifier,
+                      const float* rotations, const float* cov3D_precomp, const float* viewmatrix,
+                      const float* projmatrix, const float* cam_pos, float tan_fovx, float tan_fovy,
+                      int prefiltered, float* out_color, float* depth, int antialiasing, int* radii,
+                      int debug, uint32_t* status_host, void* stream) {
+    if (!status_host) return fail(GSR_ERR_ARG, "gsr_forward_async: null status_host");
+    if (debug) return fail(GSR_ERR_ARG, "gsr_forward_async: debug mode synchronises; use gsr_forward");
+    return forward_single(geometryBuffer, binningBuffer, imageBuffer, alloc_ctx, P, D, M, background, width,
+                          height, means3D, shs, colors_precomp, opacities, scales, scale_modifier, rotations,
+                          cov3D_precomp, viewmatrix, projmatrix, cam_pos, tan_fovx, tan_fovy, prefiltered,
+                          out_color, depth, antialiasing, radii, debug, status_host, (hipStream_t)stream);
 }
 
 int gsr_backward(int P, int D, int M, int R, const float* background, int width, int height,
@@ -341,6 +399,7 @@ int gsr_backward(int P, int D, int M, int R, const float* background, int width,
     gr.dL_dopacity = dL_dopacity;
     gr.dL_dcolors = dL_dcolor;
     gr.dL_dinvdepth_g = dL_invdepths ? dL_dinvdepth : nullptr;
+    gr.invd = gr.dL_dinvdepth != nullptr && gr.dL_dinvdepth_g != nullptr;
     gr.dL_dmeans3D = dL_dmean3D;
     gr.dL_dcov3D = dL_dcov3D;
     gr.dL_dscale = (cov3D_precomp == nullptr) ? dL_dscale : nullptr;
@@ -461,18 +520,12 @@ int gsr_refine_prepare(int n, const float* rows, const float* weight, int n_out,
     return 0;
 }
 
-int gsr_backward_batch(int B, int P, int width, int height, const float* means3D,
-                       int64_t means_stride, const float* colors, int64_t colors_stride,
-                       const float* opacities, int64_t opac_stride, const float* scales,
-                       int64_t scales_stride, const float* rotations, int64_t rot_stride,
-                       float scale_modifier, const float* viewmatrices, const float* projmatrices,
-                       const float* tanfov, const float* backgrounds, int64_t bg_stride,
-                       char* workspace, int64_t R_capacity, const float* dL_dpix,
-                       const float* dL_dinvdepth, float* dL_dmean2D, float* dL_dconic,
-                       float* dL_dopacity, float* dL_dcolor, float* dL_dinvdepth_g,
-                       float* dL_dmean3D, float* dL_dcov3D, float* dL_dscale, float* dL_drot,
-                       int antialiasing, void* stream) {
-    hipStream_t s = (hipStream_t)stream;
+static int backward_batch(int B, int P, int width, int height, const float* means3D, int64_t means_stride,
+                          const float* colors, int64_t colors_stride, const float* opacities, int64_t opac_stride,
+                          const float* scales, int64_t scales_stride, const float* rotations, int64_t rot_stride,
+                          float scale_modifier, const float* viewmatrices, const float* projmatrices,
+                          const float* tanfov, const float* backgrounds, int64_t bg_stride, char* workspace,
+                          int64_t R_capacity, const Grads& grads, int antialiasing, hipStream_t s) {
     if (B <= 0 || P <= 0 || !workspace || !tanfov) return fail(GSR_ERR_ARG, "bad batch arguments");
     if (P >= kMaxGaussians) return fail(GSR_ERR_ARG, "P must be < 2^24");
     const Dims d = make_dims(B, P, width, height);
@@ -492,6 +545,26 @@ int gsr_backward_batch(int B, int P, int width, int height, const float* means3D
     in.bg = backgrounds; in.s_bg = bg_stride;
     in.scale_mod = scale_modifier;
     in.antialiasing = antialiasing;
+    { StageTimer st_(7, s); launch_render_bwd(d, in, g, im, bn, grads, g_exact_exp != 0, s); }
+    { StageTimer st_(8, s); launch_preprocess_bwd(d, in, g, grads, s); }
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return fail(GSR_ERR_HIP, std::string("backward_batch: ") + hipGetErrorString(e));
+    return 0;
+}
+
+int gsr_backward_batch(int B, int P, int width, int height, const float* means3D,
+                       int64_t means_stride, const float* colors, int64_t colors_stride,
+                       const float* opacities, int64_t opac_stride, const float* scales,
+                       int64_t scales_stride, const float* rotations, int64_t rot_stride,
+                       float scale_modifier, const float* viewmatrices, const float* projmatrices,
+                       const float* tanfov, const float* backgrounds, int64_t bg_stride,
+                       char* workspace, int64_t R_capacity, const float* dL_dpix,
+                       const float* dL_dinvdepth, float* dL_dmean2D, float* dL_dconic,
+                       float* dL_dopacity, float* dL_dcolor, float* dL_dinvdepth_g,
+                       float* dL_dmean3D, float* dL_dcov3D, float* dL_dscale, float* dL_drot,
+                       int antialiasing, void* stream) {
+    if (!dL_dpix || !dL_dmean2D || !dL_dconic || !dL_dopacity || !dL_dcolor || !dL_dmean3D || !dL_dcov3D)
+        return fail(GSR_ERR_ARG, "backward_batch: null gradient buffer");
     Grads gr{};
     gr.dL_dpix = dL_dpix;
     gr.dL_dinvdepth = dL_dinvdepth;
@@ -500,15 +573,44 @@ int gsr_backward_batch(int B, int P, int width, int height, const float* means3D
     gr.dL_dopacity = dL_dopacity;
     gr.dL_dcolors = dL_dcolor;
     gr.dL_dinvdepth_g = dL_dinvdepth ? dL_dinvdepth_g : nullptr;
+    gr.invd = dL_dinvdepth != nullptr && dL_dinvdepth_g != nullptr;
     gr.dL_dmeans3D = dL_dmean3D;
     gr.dL_dcov3D = dL_dcov3D;
     gr.dL_dscale = dL_dscale;
     gr.dL_drot = dL_drot;
-    { StageTimer st_(7, s); launch_render_bwd(d, in, g, im, bn, gr, g_exact_exp != 0, s); }
-    { StageTimer st_(8, s); launch_preprocess_bwd(d, in, g, gr, s); }
-    hipError_t e = hipGetLastError();
-    if (e != hipSuccess) return fail(GSR_ERR_HIP, std::string("backward_batch: ") + hipGetErrorString(e));
-    return 0;
+    return backward_batch(B, P, width, height, means3D, means_stride, colors, colors_stride, opacities,
+                          opac_stride, scales, scales_stride, rotations, rot_stride, scale_modifier,
+                          viewmatrices, projmatrices, tanfov, backgrounds, bg_stride, workspace, R_capacity, gr,
+                          antialiasing, (hipStream_t)stream);
+}
+
+int gsr_backward_batch_shared(int B, int P, int width, int height, const float* means3D,
+                              int64_t means_stride, const float* colors, int64_t colors_stride,
+                              const float* opacities, int64_t opac_stride, const float* scales,
+                              int64_t scales_stride, const float* rotations, int64_t rot_stride,
+                              float scale_modifier, const float* viewmatrices, const float* projmatrices,
+                              const float* tanfov, const float* backgrounds, int64_t bg_stride,
+                              char* workspace, int64_t R_capacity, const float* dL_dpix,
+                              const float* dL_dinvdepth, float* dL_dopacity, float* dL_dcolor,
+                              float* dL_dmean3D, float* dL_dscale, float* dL_drot, int antialiasing,
+                              void* stream) {
+    if (!dL_dpix || !dL_dopacity || !dL_dcolor || !dL_dmean3D || !dL_dscale || !dL_drot)
+        return fail(GSR_ERR_ARG, "backward_batch_shared: null gradient buffer");
+    if (!scales || !rotations) return fail(GSR_ERR_ARG, "backward_batch_shared: needs scales and rotations");
+    Grads gr{};
+    gr.dL_dpix = dL_dpix;
+    gr.dL_dinvdepth = dL_dinvdepth;
+    gr.invd = dL_dinvdepth != nullptr;
+    gr.reduce = 1;
+    gr.dL_dopacity = dL_dopacity;
+    gr.dL_dcolors = dL_dcolor;
+    gr.dL_dmeans3D = dL_dmean3D;
+    gr.dL_dscale = dL_dscale;
+    gr.dL_drot = dL_drot;
+    return backward_batch(B, P, width, height, means3D, means_stride, colors, colors_stride, opacities,
+                          opac_stride, scales, scales_stride, rotations, rot_stride, scale_modifier,
+                          viewmatrices, projmatrices, tanfov, backgrounds, bg_stride, workspace, R_capacity, gr,
+                          antialiasing, (hipStream_t)stream);
 }
 
 int gsr_render_counters(uint64_t* device_counters) {

@@ -198,6 +198,10 @@ struct Grads {
     float* dL_dcov3D;            // [B][P][6]
     float* dL_dscale;            // [B][P][3] or null
     float* dL_drot;              // [B][P][4] or null
+    int invd;                    // dL_dinvdepth is given (its term enters dL/dt_z)
+    int reduce;                  // frame-reduced outputs: colors [P][C] (accumulated), opacity [P],
+                                 // means3D [P][3], scale [P][3], rot [P][4] summed over frames;
+                                 // the per-frame mean2D / conic / cov3D / invdepth outputs unused
 };
 
 // Records `msg` for gsr_last_error() and returns -status (capi.hip).

@@ -7,12 +7,14 @@ namespace gsr {
 
 __device__ __forceinline__ float sqf(float x) { return x * x; }
 
-__global__ __launch_bounds__(kScanBlock) void k_preprocess_bwd(Dims d, Inputs in, GeomArena g, Grads gr) {
-    const int b = blockIdx.y;
-    const int i = blockIdx.x * kScanBlock + threadIdx.x;
-    if (i >= d.P) return;
+// Gradients of Gaussian i in frame b; returns false (outputs untouched) when it was culled there.
+// The per-frame outputs (mean2D, conic, cov3D, invdepth) are stored unless gr.reduce; the
+// attributes' gradients come back in o_mean / o_op / o_scale / o_rot.
+__device__ __forceinline__ bool preprocess_bwd_frame(const Dims& d, const Inputs& in, const GeomArena& g,
+                                                     const Grads& gr, int b, int i, float o_mean[3], float& o_op,
+                                                     float o_scale[3], float o_rot[4]) {
     const int64_t gid = (int64_t)b * d.P + i;
-    if (!(g.radii[gid] > 0)) return;
+    if (!(g.radii[gid] > 0)) return false;
     const float* view = in.view + 16 * b;
     const float* proj = in.proj + 16 * b;
     const float tanx = in.tan_dev ? in.tan_dev[2 * b] : in.tanx;
@@ -29,13 +31,15 @@ __global__ __launch_bounds__(kScanBlock) void k_preprocess_bwd(Dims d, Inputs in
     const float4 gt0 = reinterpret_cast<const float4*>(g.gterm)[2 * gid];
     const float4 gt1 = reinterpret_cast<const float4*>(g.gterm)[2 * gid + 1];
     const float dcx = gt0.z, dcy = gt0.w, dcz = gt1.x;
-    gr.dL_dconic[4 * gid] = dcx;
-    gr.dL_dconic[4 * gid + 1] = dcy;
-    gr.dL_dconic[4 * gid + 3] = dcz;
-    gr.dL_dmean2D[3 * gid] = gt0.x;
-    gr.dL_dmean2D[3 * gid + 1] = gt0.y;
-    gr.dL_dopacity[gid] = gt1.y;
-    if (gr.dL_dinvdepth_g) gr.dL_dinvdepth_g[gid] = gt1.z;
+    if (!gr.reduce) {
+        gr.dL_dconic[4 * gid] = dcx;
+        gr.dL_dconic[4 * gid + 1] = dcy;
+        gr.dL_dconic[4 * gid + 3] = dcz;
+        gr.dL_dmean2D[3 * gid] = gt0.x;
+        gr.dL_dmean2D[3 * gid + 1] = gt0.y;
+        if (gr.dL_dinvdepth_g) gr.dL_dinvdepth_g[gid] = gt1.z;
+    }
+    o_op = gt1.y;
 
     // ---- computeCov2DCUDA ----
     float t[3];
@@ -65,7 +69,7 @@ __global__ __launch_bounds__(kScanBlock) void k_preprocess_bwd(Dims d, Inputs in
         const float h_conv = sqrtf(fmaxf(0.000025f, det_cov / det_cov_plus_h_cov));
         const float dL_dopacity_v = gt1.y;
         const float d_h_conv = dL_dopacity_v * in.opac[in.s_opac * b + i];
-        gr.dL_dopacity[gid] = dL_dopacity_v * h_conv;
+        o_op = dL_dopacity_v * h_conv;
         d_inside_root = (det_cov / det_cov_plus_h_cov) <= 0.000025f ? 0.f : d_h_conv / (2 * h_conv);
     } else {
         c_xx += h_var;
@@ -97,8 +101,9 @@ __global__ __launch_bounds__(kScanBlock) void k_preprocess_bwd(Dims d, Inputs in
 #pragma unroll
         for (int k = 0; k < 6; k++) dcov[k] = 0;
     }
+    if (!gr.reduce)
 #pragma unroll
-    for (int k = 0; k < 6; k++) gr.dL_dcov3D[6 * gid + k] = dcov[k];
+        for (int k = 0; k < 6; k++) gr.dL_dcov3D[6 * gid + k] = dcov[k];
     const float (*Vr)[3] = V.m;
     const float dL_dT00 = 2 * (T[0][0] * Vr[0][0] + T[0][1] * Vr[0][1] + T[0][2] * Vr[0][2]) * dL_dc_xx +
                           (T[1][0] * Vr[0][0] + T[1][1] * Vr[0][1] + T[1][2] * Vr[0][2]) * dL_dc_xy;
@@ -124,7 +129,7 @@ __global__ __launch_bounds__(kScanBlock) void k_preprocess_bwd(Dims d, Inputs in
     const float dL_dty = y_grad_mul * -h_y * tz2 * dL_dJ12;
     float dL_dtz = -h_x * tz2 * dL_dJ00 - h_y * tz2 * dL_dJ11 + (2 * h_x * t[0]) * tz3 * dL_dJ02 +
                    (2 * h_y * t[1]) * tz3 * dL_dJ12;
-    if (gr.dL_dinvdepth_g) dL_dtz -= gt1.z / (t[2] * t[2]);
+    if (gr.invd) dL_dtz -= gt1.z / (t[2] * t[2]);
     const float dt[3] = {dL_dtx, dL_dty, dL_dtz};
     float dm[3];
     xformvec_t(dt, view, dm);
@@ -139,9 +144,9 @@ __global__ __launch_bounds__(kScanBlock) void k_preprocess_bwd(Dims d, Inputs in
     dm[0] += (proj[0] * m_w - proj[3] * mul1) * d2x + (proj[1] * m_w - proj[3] * mul2) * d2y;
     dm[1] += (proj[4] * m_w - proj[7] * mul1) * d2x + (proj[5] * m_w - proj[7] * mul2) * d2y;
     dm[2] += (proj[8] * m_w - proj[11] * mul1) * d2x + (proj[9] * m_w - proj[11] * mul2) * d2y;
-    gr.dL_dmeans3D[3 * gid] = dm[0];
-    gr.dL_dmeans3D[3 * gid + 1] = dm[1];
-    gr.dL_dmeans3D[3 * gid + 2] = dm[2];
+    o_mean[0] = dm[0];
+    o_mean[1] = dm[1];
+    o_mean[2] = dm[2];
 
     // ---- computeCov3D bwd ----
     if (in.scales && in.rot && gr.dL_dscale && gr.dL_drot) {
@@ -167,23 +172,68 @@ __global__ __launch_bounds__(kScanBlock) void k_preprocess_bwd(Dims d, Inputs in
         mat3 dMt = tr3(dM);
 #pragma unroll
         for (int k = 0; k < 3; k++)
-            gr.dL_dscale[3 * gid + k] = Rt.m[k][0] * dMt.m[k][0] + Rt.m[k][1] * dMt.m[k][1] + Rt.m[k][2] * dMt.m[k][2];
+            o_scale[k] = Rt.m[k][0] * dMt.m[k][0] + Rt.m[k][1] * dMt.m[k][1] + Rt.m[k][2] * dMt.m[k][2];
 #pragma unroll
         for (int k = 0; k < 3; k++)
 #pragma unroll
             for (int rr = 0; rr < 3; rr++) dMt.m[k][rr] *= s[k];
         const float (*D)[3] = dMt.m;
-        gr.dL_drot[4 * gid + 0] = 2 * z * (D[0][1] - D[1][0]) + 2 * y * (D[2][0] - D[0][2]) + 2 * x * (D[1][2] - D[2][1]);
-        gr.dL_drot[4 * gid + 1] = 2 * y * (D[1][0] + D[0][1]) + 2 * z * (D[2][0] + D[0][2]) + 2 * r * (D[1][2] - D[2][1]) - 4 * x * (D[2][2] + D[1][1]);
-        gr.dL_drot[4 * gid + 2] = 2 * x * (D[1][0] + D[0][1]) + 2 * r * (D[2][0] - D[0][2]) + 2 * z * (D[1][2] + D[2][1]) - 4 * y * (D[2][2] + D[0][0]);
-        gr.dL_drot[4 * gid + 3] = 2 * r * (D[0][1] - D[1][0]) + 2 * x * (D[2][0] + D[0][2]) + 2 * y * (D[1][2] + D[2][1]) - 4 * z * (D[1][1] + D[0][0]);
+        o_rot[0] = 2 * z * (D[0][1] - D[1][0]) + 2 * y * (D[2][0] - D[0][2]) + 2 * x * (D[1][2] - D[2][1]);
+        o_rot[1] = 2 * y * (D[1][0] + D[0][1]) + 2 * z * (D[2][0] + D[0][2]) + 2 * r * (D[1][2] - D[2][1]) - 4 * x * (D[2][2] + D[1][1]);
+        o_rot[2] = 2 * x * (D[1][0] + D[0][1]) + 2 * r * (D[2][0] - D[0][2]) + 2 * z * (D[1][2] + D[2][1]) - 4 * y * (D[2][2] + D[0][0]);
+        o_rot[3] = 2 * r * (D[0][1] - D[1][0]) + 2 * x * (D[2][0] + D[0][2]) + 2 * y * (D[1][2] + D[2][1]) - 4 * z * (D[1][1] + D[0][0]);
+    }
+    return true;
+}
+
+// Per-frame mode: one thread per (Gaussian, frame), every output per frame.  Frame-reduced mode
+// (gr.reduce, the shared attributes of a training batch): one thread per Gaussian sums its frames in
+// frame order and writes each attribute gradient once -- no [B][P][k] buffers and no separate sum.
+__global__ __launch_bounds__(kScanBlock) void k_preprocess_bwd(Dims d, Inputs in, GeomArena g, Grads gr) {
+    const int i = blockIdx.x * kScanBlock + threadIdx.x;
+    if (i >= d.P) return;
+    const bool geo = in.scales && in.rot && gr.dL_dscale && gr.dL_drot;
+    if (!gr.reduce) {
+        const int b = blockIdx.y;
+        const int64_t gid = (int64_t)b * d.P + i;
+        float m[3], sc[3], r[4], op;
+        if (!preprocess_bwd_frame(d, in, g, gr, b, i, m, op, sc, r)) return;
+        gr.dL_dopacity[gid] = op;
+#pragma unroll
+        for (int k = 0; k < 3; k++) gr.dL_dmeans3D[3 * gid + k] = m[k];
+        if (geo) {
+#pragma unroll
+            for (int k = 0; k < 3; k++) gr.dL_dscale[3 * gid + k] = sc[k];
+#pragma unroll
+            for (int k = 0; k < 4; k++) gr.dL_drot[4 * gid + k] = r[k];
+        }
+        return;
+    }
+    float am[3] = {0.f, 0.f, 0.f}, as[3] = {0.f, 0.f, 0.f}, ar[4] = {0.f, 0.f, 0.f, 0.f}, aop = 0.f;
+    for (int b = 0; b < d.B; b++) {
+        float m[3], sc[3] = {0.f, 0.f, 0.f}, r[4] = {0.f, 0.f, 0.f, 0.f}, op;
+        if (!preprocess_bwd_frame(d, in, g, gr, b, i, m, op, sc, r)) continue;
+        aop += op;
+#pragma unroll
+        for (int k = 0; k < 3; k++) { am[k] += m[k]; as[k] += sc[k]; }
+#pragma unroll
+        for (int k = 0; k < 4; k++) ar[k] += r[k];
+    }
+    gr.dL_dopacity[i] = aop;
+#pragma unroll
+    for (int k = 0; k < 3; k++) gr.dL_dmeans3D[3 * (int64_t)i + k] = am[k];
+    if (geo) {
+#pragma unroll
+        for (int k = 0; k < 3; k++) gr.dL_dscale[3 * (int64_t)i + k] = as[k];
+#pragma unroll
+        for (int k = 0; k < 4; k++) gr.dL_drot[4 * (int64_t)i + k] = ar[k];
     }
 }
 
 void launch_preprocess_bwd(const Dims& d, const Inputs& in, const GeomArena& g, const Grads& gr,
                            hipStream_t s) {
     if (d.P == 0 || d.B == 0) return;
-    hipLaunchKernelGGL(k_preprocess_bwd, dim3(d.nblk, d.B), dim3(kScanBlock), 0, s, d, in, g, gr);
+    hipLaunchKernelGGL(k_preprocess_bwd, dim3(d.nblk, gr.reduce ? 1 : d.B), dim3(kScanBlock), 0, s, d, in, g, gr);
 }
 
 }  // namespace gsr

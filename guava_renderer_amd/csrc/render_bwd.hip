@@ -107,6 +107,7 @@ __global__ __launch_bounds__(GSR_TILE_PIX) __attribute__((amdgpu_waves_per_eu(2)
         const float4* __restrict__ rrec = g.rrec + (int64_t)b * d.P * 2;
         const float* __restrict__ colors = in.colors + in.s_colors * b;
         const int64_t gbase = (int64_t)b * d.P;
+        const int64_t cbase = gr.reduce ? 0 : gbase;  // frame-reduced colour gradients: one [P][C] block
 
         const float T_final = inside ? im.final_T[pix] : 0.f;
         const uint32_t last_contributor = inside ? im.n_contrib[pix] : 0u;
@@ -348,7 +349,7 @@ __global__ __launch_bounds__(GSR_TILE_PIX) __attribute__((amdgpu_waves_per_eu(2)
                     const uint32_t gsl = __builtin_amdgcn_readlane(bg_, (r & 3) + 8 * (r >> 2)) ;
                     const uint32_t gsh = __builtin_amdgcn_readlane(bg_, (r & 3) + 8 * (r >> 2) + 4);
                     const uint32_t gs = hi ? gsh : gsl;
-                    if ((amask >> sl) & 1u) atomicAdd(gr.dL_dcolors + (gbase + gs) * GSR_C + l32, acc[r]);
+                    if ((amask >> sl) & 1u) atomicAdd(gr.dL_dcolors + (cbase + gs) * GSR_C + l32, acc[r]);
                 }
             }
             // the other terms of slot l&31, from the pixel moments of u about the Gaussian's centre
@@ -409,7 +410,7 @@ void launch_render_bwd(const Dims& d, const Inputs& in, const GeomArena& g, cons
     if (nwaves == 0) return;
     hipLaunchKernelGGL(k_zero_bwd_queues, dim3(1), dim3(64), 0, s, g.ctrl);
     hipMemsetAsync(g.gterm, 0, (size_t)d.B * d.P * kGtWords * sizeof(float), s);
-    const bool invd = gr.dL_dinvdepth != nullptr && gr.dL_dinvdepth_g != nullptr;
+    const bool invd = gr.invd != 0;
     const dim3 grid(min((nwaves + 3) / 4, persistent_grid(2))), blk(GSR_TILE_PIX);
     static const int ablate = [] { const char* e = getenv("GSR_BWD_ABLATE"); return e ? atoi(e) : 0; }();
     if (ablate >= 1 && ablate <= 3 && exact && invd) {

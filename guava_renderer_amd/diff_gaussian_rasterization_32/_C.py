@@ -10,12 +10,126 @@ Differences by design: scratch buffers live on means3D's device (the reference u
 device); kernels run on the current HIP stream of that device.
 """
 import ctypes
+import os
+import weakref
 
 import torch
 
 from .. import _lib
 
 NUM_CHANNELS = 32
+# binning buffers up to this size take the no-sync forward (gsr_forward_async); larger ones (big
+# images x many Gaussians) size the buffer from the synchronous R read-back as the reference does
+ASYNC_BINNING_MB = int(os.environ.get("GSR_ASYNC_BINNING_MB", "512"))
+
+
+class PendingCount:
+    """num_rendered of a forward that did not wait for the device (gsr_forward_async): reading it
+    (int(), comparisons, arithmetic, printing) waits for that forward and raises the reference's
+    errors (a culled point with prefiltered set, an instance count beyond 2^31 - 1) then."""
+    __slots__ = ("_status", "_event", "_value", "__weakref__")
+
+    def __init__(self, status, event):
+        self._status, self._event, self._value = status, event, None
+
+    def __int__(self):
+        if self._value is None:
+            self._event.synchronize()
+            r, ovf, err = (int(x) for x in self._status[:3].tolist())
+            if err & 1:
+                raise RuntimeError("Point is filtered although prefiltered is set. This shouldn't happen!")
+            if ovf:
+                raise _lib.CapacityError("instance count exceeds 2^31 - 1 (num_rendered is an int)")
+            self._value = r
+        return self._value
+
+    __index__ = __int__
+
+    def __eq__(self, o):
+        return int(self) == o
+
+    def __lt__(self, o):
+        return int(self) < o
+
+    def __le__(self, o):
+        return int(self) <= o
+
+    def __gt__(self, o):
+        return int(self) > o
+
+    def __ge__(self, o):
+        return int(self) >= o
+
+    def __hash__(self):
+        return hash(int(self))
+
+    def __bool__(self):
+        return int(self) != 0
+
+    def __add__(self, o):
+        return int(self) + o
+
+    __radd__ = __add__
+
+    def __mul__(self, o):
+        return int(self) * o
+
+    __rmul__ = __mul__
+
+    def __sub__(self, o):
+        return int(self) - o
+
+    def __rsub__(self, o):
+        return o - int(self)
+
+    def __floordiv__(self, o):
+        return int(self) // o
+
+    def __mod__(self, o):
+        return int(self) % o
+
+    def __neg__(self):
+        return -int(self)
+
+    def __repr__(self):
+        return repr(int(self))
+
+    __str__ = __repr__
+
+    def __format__(self, spec):
+        return format(int(self), spec)
+
+
+class _StatusRing:
+    """Pinned 16-byte status slots for gsr_forward_async, reused round-robin.  A slot is handed out
+    again only after its copy has landed and its PendingCount (if still alive) has read it, so a
+    pending device-to-host copy never writes memory that belongs to someone else."""
+
+    def __init__(self, n=256):
+        self.buf = torch.zeros((n, 4), dtype=torch.int32, pin_memory=True)
+        self.owner = [None] * n  # (event, weakref to PendingCount)
+        self.i = 0
+
+    def take(self, stream):
+        k = self.i
+        self.i = (k + 1) % self.buf.shape[0]
+        prev = self.owner[k]
+        if prev is not None:
+            ev, ref = prev
+            pc = ref()
+            if pc is not None:
+                int(pc)  # resolve it from this slot before the slot is rewritten
+            else:
+                ev.synchronize()
+        ev = torch.cuda.Event()
+        slot = self.buf[k]
+        return slot, ev, k
+
+    def bind(self, k, ev, pc):
+        self.owner[k] = (ev, weakref.ref(pc))
+
+
+_RINGS = {}
 
 
 def _ptr(t):
@@ -89,15 +203,25 @@ def rasterize_gaussians(background, means3D, colors, opacity, scales, rotations,
         background = _dev_f32(background, dev, "bg")
         viewmatrix = _dev_f32(viewmatrix, dev, "viewmatrix")
         projmatrix = _dev_f32(projmatrix, dev, "projmatrix")
-        with torch.cuda.device(dev):
-            rc = L.gsr_forward(
-                geom.cb, binning.cb, img.cb, None, P, int(degree), M, _ptr(background), W, H,
+        args = (geom.cb, binning.cb, img.cb, None, P, int(degree), M, _ptr(background), W, H,
                 _ptr(means3D), _ptr(sh), _ptr(colors), _ptr(opacity), _ptr(scales),
                 float(scale_modifier), _ptr(rotations), _ptr(cov3D_precomp), _ptr(viewmatrix),
                 _ptr(projmatrix), _ptr(campos), float(tan_fovx), float(tan_fovy),
                 int(bool(prefiltered)), out_color.data_ptr(), out_invdepth.data_ptr(),
-                int(bool(antialiasing)), radii.data_ptr(), int(bool(debug)), _stream(dev))
-        rendered = _lib.check(rc, "rasterize_gaussians")
+                int(bool(antialiasing)), radii.data_ptr(), int(bool(debug)))
+        bound = L.gsr_forward_async_bound(P, W, H)
+        with torch.cuda.device(dev):
+            if not debug and bound < 0x7FFFFFFF and 4 * bound <= ASYNC_BINNING_MB << 20:
+                ring = _RINGS.get(dev)
+                if ring is None:
+                    ring = _RINGS[dev] = _StatusRing()
+                status, ev, k = ring.take(dev)
+                _lib.check(L.gsr_forward_async(*args, status.data_ptr(), _stream(dev)), "rasterize_gaussians")
+                ev.record(torch.cuda.current_stream(dev))
+                rendered = PendingCount(status, ev)
+                ring.bind(k, ev, rendered)
+            else:
+                rendered = _lib.check(L.gsr_forward(*args, _stream(dev)), "rasterize_gaussians")
     return rendered, out_color, radii, geom.t, binning.t, img.t, out_invdepth
 
 

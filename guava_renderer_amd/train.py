@@ -3,10 +3,14 @@
 One step over the B frames of this rank (main/trainer.py:82-102 does, per iteration: render the
 batch, Optimization_Loss, fabric.backward -> DDP gradient all-reduce, Adam step):
   1. BatchRasterizer.forward of the shared Gaussian attributes for B cameras (one launch set);
-  2. loss = (1 - lambda) * L1 + lambda * (1 - fused_ssim) on the RGB channels against the targets
-     (the fused_ssim HIP kernels, guava_renderer_amd/fused_ssim.py);
-  3. BatchRasterizer.backward (render_bwd + cov/preprocess backward kernels) -> per-frame
-     gradients [B,P,k], summed over frames into the shared attributes' gradients;
+  2. loss = (1 - lambda) * L1 + lambda * (1 - fused_ssim) of the raw RGB channels (the reference's
+     raw_renders term, utils/loss_utils.py:116-119; fused_ssim HIP kernels) + L1 of a refined image
+     made from ALL 32 channels (the reference's `renders` term, :92; its StyleUNet refiner is out
+     of scope, so a fixed random 1x1 conv 32 -> 3 stands in), so every feature channel carries a
+     gradient into the rasterizer backward as in the reference's training;
+  3. BatchRasterizer.backward(shared=True) (render_bwd + cov/preprocess backward kernels) -> the
+     shared attributes' gradients [P,k], summed over the frames inside the kernels (no [B,P,k]
+     buffers);
   4. world > 1: ONE flat RCCL all-reduce of those gradients (parallel.reduce_shared_grads; the
      reference's DDP all-reduce, trainer.py:40-43,95), averaged over ranks;
   5. Adam on the attributes (fused Adam).
@@ -20,6 +24,7 @@ The reference trains networks that predict the Gaussians; those networks are out
 (SURVEY.md 2.1), so the trainable parameters are the Gaussian attributes themselves -- the
 rasterizer-side work of the step (fwd, bwd, SSIM, all-reduce, update) is the same.
 """
+import os
 import warnings
 
 import torch
@@ -33,9 +38,10 @@ C = 32
 
 
 class SplatTrainer:
-    def __init__(self, params, B, W, H, R_capacity, device="cuda", lr=1e-3, lambda_ssim=0.2):
+    def __init__(self, params, B, W, H, R_capacity, device="cuda", lr=1e-3, lambda_ssim=0.2, refine_head=True):
         """params: dict of float32 device tensors means3D [P,3], colors [P,32], opacities [P,1],
-        scales [P,3], rotations [P,4] (made leaves with requires_grad)."""
+        scales [P,3], rotations [P,4] (made leaves with requires_grad).  refine_head=False: the loss
+        sees the RGB channels only."""
         self.dev = torch.device(device)
         self.p = {k: v.detach().clone().contiguous().requires_grad_(True) for k, v in params.items()}
         P = self.p["means3D"].shape[0]
@@ -45,8 +51,11 @@ class SplatTrainer:
         self.B, self.W, self.H = B, W, H
         self.lambda_ssim = lambda_ssim
         self.bg = torch.zeros((B, C), dtype=torch.float32, device=self.dev)
-        self.dL = torch.zeros((B, C, H, W), dtype=torch.float32, device=self.dev)
         self.dinv = torch.zeros((B, H, W), dtype=torch.float32, device=self.dev)  # materialised, as autograd does
+        g = torch.Generator().manual_seed(11)
+        self.refine_w = ((torch.rand((3, C), generator=g) * 2 - 1) / C ** 0.5).to(self.dev) if refine_head else None
+        self.shared_backward = os.environ.get("GSR_TRAIN_PERFRAME") != "1"  # "1": per-frame grads + sum (A/B)
+        self.dL_rgb = None if refine_head else torch.zeros((B, C, H, W), dtype=torch.float32, device=self.dev)
 
     def _grow(self, err):
         """An earlier step overflowed (and was skipped on the device): grow the workspace to 1.5x the
@@ -70,17 +79,41 @@ class SplatTrainer:
                                       p["scales"].detach(), p["rotations"].detach(), views, projs, tanf,
                                       self.bg)
         img = col[:, :3].detach().requires_grad_(True)
-        loss = (1.0 - self.lambda_ssim) * (img - target).abs().mean() + \
-            self.lambda_ssim * (1.0 - fused_ssim(img, target))
+        loss = self.rgb_loss(img, target)
         loss.backward()
-        self.dL[:, :3].copy_(img.grad)
+        if self.refine_w is not None:
+            # the refined-image L1 term and its gradient in closed form (two passes over the
+            # 32-channel frames instead of autograd's slice / conv / sum chain)
+            B, _, H, W = col.shape
+            refined = torch.matmul(self.refine_w, col.view(B, C, H * W))  # [B,3,HW]
+            diff = refined.view(B, 3, H, W) - target
+            loss = loss + diff.abs().mean()
+            s = torch.sign(diff).mul_(1.0 / diff.numel()).view(B, 3, H * W)
+            dL = torch.matmul(self.refine_w.t(), s).view(B, C, H, W)
+            dL[:, :3] += img.grad
+        else:
+            dL = self.dL_rgb
+            dL[:, :3].copy_(img.grad)
         g = self.rast.backward(p["means3D"].detach(), p["colors"].detach(), p["opacities"].detach(),
                                p["scales"].detach(), p["rotations"].detach(), views, projs, tanf, self.bg,
-                               self.dL, self.dinv)
-        grads = {"means3D": g["means3D"].sum(0), "colors": g["colors"].sum(0),
-                 "opacities": g["opacity"].sum(0), "scales": g["scales"].sum(0),
-                 "rotations": g["rotations"].sum(0)}
+                               dL, self.dinv, shared=self.shared_backward)
+        if not self.shared_backward:
+            g = {k: v.sum(0) for k, v in g.items() if v is not None and v.dim() == 3}
+        grads = {"means3D": g["means3D"], "colors": g["colors"], "opacities": g["opacity"],
+                 "scales": g["scales"], "rotations": g["rotations"]}
         return loss.detach(), grads
+
+    def rgb_loss(self, img, target):
+        """(1 - lambda) L1 + lambda (1 - SSIM) of the raw RGB channels [B,3,H,W]."""
+        return (1.0 - self.lambda_ssim) * (img - target).abs().mean() + \
+            self.lambda_ssim * (1.0 - fused_ssim(img, target))
+
+    def loss(self, feat, target):
+        """The step's loss of rendered features [B,32,H,W] against RGB targets [B,3,H,W]."""
+        loss = self.rgb_loss(feat[:, :3], target)
+        if self.refine_w is not None:
+            loss = loss + (torch.einsum("oc,bchw->bohw", self.refine_w, feat) - target).abs().mean()
+        return loss
 
     def step(self, views, projs, tanf, target):
         loss, grads = self.gradients(views, projs, tanf, target)

@@ -85,6 +85,24 @@ int gsr_forward(gsr_alloc_fn geometryBuffer, gsr_alloc_fn binningBuffer, gsr_all
                 int prefiltered, float* out_color, float* depth, int antialiasing, int* radii,
                 int debug, void* stream);
 
+/* gsr_forward without the host synchronisation after the scan (the reference reads num_rendered
+ * back before sizing the binning buffer, rasterizer_impl.cu:279-291 of the reference driver):
+ * the binning buffer is requested at the upper bound gsr_forward_async_bound(P, W, H) = P x tiles
+ * instances (4 B each; every Gaussian in every tile), so every later launch is queued at once.
+ * status_host (4 uint32, host-visible, e.g. pinned) receives {num_rendered, overflow, error bits,
+ * 0} at the end of the stream's work: read it after synchronising (error bit 0 = a culled point
+ * with prefiltered set, the reference's trap; overflow only if the bound hit 2^31 - 1).  Returns
+ * 0 or -status.  debug must be 0. */
+int64_t gsr_forward_async_bound(int P, int width, int height);
+int gsr_forward_async(gsr_alloc_fn geometryBuffer, gsr_alloc_fn binningBuffer, gsr_alloc_fn imageBuffer,
+                      void* alloc_ctx, int P, int D, int M, const float* background, int width, int height,
+                      const float* means3D, const float* shs, const float* colors_precomp,
+                      const float* opacities, const float* scales, float scale_modifier,
+                      const float* rotations, const float* cov3D_precomp, const float* viewmatrix,
+                      const float* projmatrix, const float* cam_pos, float tan_fovx, float tan_fovy,
+                      int prefiltered, float* out_color, float* depth, int antialiasing, int* radii,
+                      int debug, uint32_t* status_host, void* stream);
+
 /* Rasterizer::backward.  Gradient buffers are accumulated into and must be zeroed by the caller
  * (the reference's torch::zeros, rasterize_points.cu:163-179): dL_dmean2D [P,3], dL_dconic [P,4],
  * dL_dopacity [P], dL_dcolor [P,32], dL_dinvdepth [P] (NULL when dL_invdepths is NULL),
@@ -129,6 +147,23 @@ int gsr_backward_batch(int B, int P, int width, int height, const float* means3D
                        float* dL_dopacity, float* dL_dcolor, float* dL_dinvdepth_g,
                        float* dL_dmean3D, float* dL_dcov3D, float* dL_dscale, float* dL_drot,
                        int antialiasing, void* stream);
+
+/* gsr_backward_batch for Gaussian attributes SHARED by the B frames (one avatar seen from B
+ * cameras, the training batch of main/trainer.py:82-102): the attribute gradients come back summed
+ * over the frames, [P,k], with no per-frame [B,P,k] buffers (the reference's autograd sums the
+ * per-frame gradients of the shared leaves).  dL_dcolor [P,32] is ACCUMULATED into (zero it);
+ * dL_dopacity [P], dL_dmean3D [P,3], dL_dscale [P,3], dL_drot [P,4] are written.  Each Gaussian's
+ * frames are summed in frame order (deterministic, except dL_dcolor's float atomics). */
+int gsr_backward_batch_shared(int B, int P, int width, int height, const float* means3D,
+                              int64_t means_stride, const float* colors, int64_t colors_stride,
+                              const float* opacities, int64_t opac_stride, const float* scales,
+                              int64_t scales_stride, const float* rotations, int64_t rot_stride,
+                              float scale_modifier, const float* viewmatrices, const float* projmatrices,
+                              const float* tanfov, const float* backgrounds, int64_t bg_stride,
+                              char* workspace, int64_t R_capacity, const float* dL_dpix,
+                              const float* dL_dinvdepth, float* dL_dopacity, float* dL_dcolor,
+                              float* dL_dmean3D, float* dL_dscale, float* dL_drot, int antialiasing,
+                              void* stream);
 /* Refiner-head epilogue: GaussianRenderer feeds the 32-channel render to the
  * StyleUNet refiner (gaussian_render.py:73), whose first layer is a 1x1 conv 32 -> 16 + leaky ReLU
  * (styleunet.py:110,178).  The conv is linear in the features, so it commutes with compositing:

@@ -141,17 +141,19 @@ def test_trainer_gradients_match_cpu_recomputation():
     target = torch.rand((B, 3, W, W), device=DEV, generator=torch.Generator(device=DEV).manual_seed(3))
     loss, grads = tr.gradients(views, projs, tanf, target)
     torch.cuda.synchronize()
-    img = tr.rast.out_color[:, :3].detach().cpu().double().requires_grad_(True)
+    feat = tr.rast.out_color.detach().cpu().double().requires_grad_(True)
+    img = feat[:, :3]
     tgt = target.cpu().double()
     lam = tr.lambda_ssim
-    ref_loss = (1 - lam) * (img - tgt).abs().mean() + lam * (1 - _ssim64(img, tgt))
+    refined = torch.einsum("oc,bchw->bohw", tr.refine_w.cpu().double(), feat)
+    ref_loss = (1 - lam) * (img - tgt).abs().mean() + lam * (1 - _ssim64(img, tgt)) + (refined - tgt).abs().mean()
     ref_loss.backward()
     assert abs(loss.item() - ref_loss.item()) <= 1e-5 * abs(ref_loss.item()) + 1e-6
-    dimg = img.grad.float().numpy()
+    dfeat = feat.grad.float().numpy()
+    assert np.abs(dfeat[:, 3:]).max() > 0  # every channel carries a gradient
     acc = None
     for f in range(B):
-        dL = np.zeros((32, W, W), np.float32)
-        dL[:3] = dimg[f]
+        dL = np.ascontiguousarray(dfeat[f])
         o = _oracle_grads(sc, cams[f], dL, np.zeros((1, W, W), np.float32))
         o = {"means3D": o[3], "colors": o[1], "opacities": o[2], "scales": o[6], "rotations": o[7]}
         acc = o if acc is None else {k: acc[k] + o[k] for k in acc}
@@ -211,3 +213,32 @@ def test_trainer_skips_overflowing_step():
     assert tr.skipped_steps == 1 and tr.rast.R_capacity > 1000
     assert torch.isfinite(loss2)
     assert any(not torch.equal(v.detach(), before[k]) for k, v in tr.p.items())
+
+
+def test_shared_backward_equals_summed_per_frame_backward():
+    """gsr_backward_batch_shared (frame sums inside the kernels) vs the per-frame gradients of
+    gsr_backward_batch summed over the frames, with and without an inverse-depth gradient."""
+    from guava_renderer_amd import scenes
+    from guava_renderer_amd.batch import BatchRasterizer
+    B, W, P = 4, 256, 20000
+    sc = scenes.avatar_cloud(P, seed=4)
+    cams = scenes.frame_cameras(B, W, W, seed=1000)
+    t = lambda x: torch.tensor(np.ascontiguousarray(x), device=DEV)  # noqa: E731
+    views = t(np.stack([c["viewmatrix"].reshape(16) for c in cams]))
+    projs = t(np.stack([c["projmatrix"].reshape(16) for c in cams]))
+    tanf = t(np.array([[c["tanfovx"], c["tanfovy"]] for c in cams], np.float32))
+    args = [t(sc[k]) for k in ("means3D", "colors", "opacities", "scales", "rotations")]
+    bgs = torch.zeros((B, 32), device=DEV)
+    r = BatchRasterizer(B, P, W, W, R_capacity=24 * P * B, device=DEV)
+    r.forward(*args, views, projs, tanf, bgs)
+    gen = torch.Generator(device=DEV).manual_seed(9)
+    dL = torch.randn((B, 32, W, W), device=DEV, generator=gen)
+    dinv = torch.randn((B, W, W), device=DEV, generator=gen)
+    for di in (None, dinv):
+        per = r.backward(*args, views, projs, tanf, bgs, dL, di)
+        sh = r.backward(*args, views, projs, tanf, bgs, dL, di, shared=True)
+        torch.cuda.synchronize()
+        for k in ("means3D", "colors", "opacity", "scales", "rotations"):
+            ref = per[k].sum(0).cpu().numpy()
+            err = _rel_err(sh[k].cpu().numpy(), ref)
+            assert err <= 1e-5, f"{k} (invdepth {di is not None}): {err:.3g}"
