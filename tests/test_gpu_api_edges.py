@@ -137,3 +137,25 @@ def test_refine_cache_follows_tensor_identity():
     b.mul_(2.0)  # in-place torch update bumps the version
     pb2 = head.prepare(b, stream)
     torch.testing.assert_close(pb2[:, 4:20], b @ w.T, rtol=1e-5, atol=1e-5)
+
+
+def test_async_forward_equals_synchronous_forward(monkeypatch):
+    """gsr_forward_async (binning buffer at the P x tiles bound, no R read-back) and the reference's
+    synchronous gsr_forward give the same images, radii and num_rendered."""
+    from guava_renderer_amd import camera, scenes
+    from guava_renderer_amd.diff_gaussian_rasterization_32 import _C
+    d = scenes.avatar_cloud(20000, seed=5)
+    cam = camera.camera(200, 136)
+    t = lambda x: torch.tensor(np.ascontiguousarray(x), device="cuda")  # noqa: E731
+    empty = torch.Tensor([])
+    args = (t(np.zeros(32, np.float32)), t(d["means3D"]), t(d["colors"]), t(d["opacities"]), t(d["scales"]),
+            t(d["rotations"]), 1.0, empty, t(cam["viewmatrix"]), t(cam["projmatrix"]), cam["tanfovx"],
+            cam["tanfovy"], 136, 200, empty, 0, t(np.zeros(3, np.float32)), False, False, False)
+    Ra, ca, ra, _, bba, _, ia = _C.rasterize_gaussians(*args)
+    assert isinstance(Ra, _C.PendingCount)
+    monkeypatch.setattr(_C, "ASYNC_BINNING_MB", 0)
+    Rs, cs, rs, _, bbs, _, is_ = _C.rasterize_gaussians(*args)
+    torch.cuda.synchronize()
+    assert isinstance(Rs, int) and int(Ra) == Rs and Ra == Rs and Rs > 0
+    assert torch.equal(ca, cs) and torch.equal(ra, rs) and torch.equal(ia, is_)
+    assert bba.numel() >= bbs.numel()
