@@ -5,6 +5,7 @@
 // per-tile quantity a slab over B*T, every per-instance (Gaussian x tile) quantity a slab over
 // the batch's R.  Slabs start on 256-byte boundaries.
 #pragma once
+#include <cstdlib>
 #include <hip/hip_runtime.h>
 #include <stddef.h>
 #include <stdint.h>
@@ -135,7 +136,12 @@ inline Dims make_dims(int B, int P, int W, int H) {
     d.NB = nb;
     // count-table rows: kSlots Gaussians (one scatter pass) up to 1024 tiles; beyond, the dense
     // (row x tile) table and each row's base[] load outweigh the extra passes (1024-Gaussian rows)
-    d.chunk = d.T > 1024 ? 4 * kSlots : kSlots;
+    static const int passes_env = [] {  // GSR_CHUNK_PASSES: scatter passes per table row (tuning)
+        const char* e = getenv("GSR_CHUNK_PASSES");
+        const int v = e ? atoi(e) : 0;
+        return v >= 1 && v <= 64 ? v : 0;
+    }();
+    d.chunk = (passes_env ? passes_env : (d.T > 1024 ? 4 : 1)) * kSlots;
     d.nchunk = (P + d.chunk - 1) / d.chunk;
     return d;
 }
