@@ -412,7 +412,9 @@ def main():
         "config": {"workload": workload,
                    "pipeline": {"avatar": "EHM LBS -> Gaussian assembly -> rasterize",
                                 "raster": "rasterize",
-                                "train": "raster fwd -> L1 + fused SSIM -> raster bwd -> grad all-reduce -> Adam",
+                                "train": "raster fwd -> L1 + fused SSIM (raw RGB) + L1 of a fixed 32->3 refine stand-in "
+                                         "(all 32 channels carry gradient) -> frame-reduced raster bwd -> "
+                                         "grad all-reduce -> Adam",
                                 "frame": "deformed frames -> GaussianRasterizer_32 once per frame (gaussian_render.py:37-67)"
                                 }[a.pipeline] + (" + fused refiner conv_body_first" if a.refine else ""), "gaussians": P, "image": [W, H], "channels": C,
                    "frames_per_step_per_gpu": B, "global_batch": B * world,

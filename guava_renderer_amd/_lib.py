@@ -20,7 +20,7 @@ EXPORTS = ("gsr_version", "gsr_last_error", "gsr_set_exact_exp", "gsr_set_split_
            "gsr_lbs_workspace_bytes", "gsr_lbs", "gsr_blend_joints", "gsr_splice_head",
            "gsr_pack_rows", "gsr_deform_gaussians",
            # include/gsr_ssim.h
-           "gsr_fused_ssim", "gsr_fused_ssim_backward")
+           "gsr_fused_ssim", "gsr_fused_ssim_backward", "gsr_image_loss_partials", "gsr_image_loss")
 
 ALLOC_FN = ctypes.CFUNCTYPE(ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t)
 
@@ -153,6 +153,10 @@ def load(path=None):
     L.gsr_fused_ssim.restype = _i
     L.gsr_fused_ssim_backward.argtypes = [_i, _i, _i, _i, _f, _f, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp]
     L.gsr_fused_ssim_backward.restype = _i
+    L.gsr_image_loss_partials.argtypes = [_i, _i, _i]
+    L.gsr_image_loss_partials.restype = _i
+    L.gsr_image_loss.argtypes = [_i, _i, _i, _vp, _vp, _vp, _f, _f, _vp, _vp, _vp, _vp]
+    L.gsr_image_loss.restype = _i
     _lib = L
     return L
 

@@ -178,6 +178,65 @@ __global__ __launch_bounds__(256) void k_ssim_bwd(int CH, int H, int W, const fl
     }
 }
 
+
+// ---- the training step's L1 terms (gsr_image_loss): one thread per pixel, 32 channel reads and 32
+// gradient writes (coalesced across the workgroup's pixels), the refine head's 3 x 32 weights as
+// wave-uniform operands; the loss partial of each workgroup by a fixed-shape LDS tree.
+__device__ __forceinline__ float sgnf(float x) { return x > 0.f ? 1.f : (x < 0.f ? -1.f : 0.f); }
+
+__global__ __launch_bounds__(256) void k_image_loss(int HW, const float* __restrict__ feat,
+                                                    const float* __restrict__ target,
+                                                    const float* __restrict__ rw, float l1w, float rfw,
+                                                    float inv_n, const float* __restrict__ extra,
+                                                    float* __restrict__ dL, float* __restrict__ partials) {
+    __shared__ float red[256];
+    const int b = blockIdx.y;
+    const int p = blockIdx.x * 256 + threadIdx.x;
+    float part = 0.f;
+    if (p < HW) {
+        const float* f = feat + (int64_t)b * 32 * HW + p;
+        const float* t = target + (int64_t)b * 3 * HW + p;
+        float fc[32];
+#pragma unroll
+        for (int c = 0; c < 32; c++) fc[c] = f[(int64_t)c * HW];
+        float tt[3], s[3] = {0.f, 0.f, 0.f}, e[3];
+#pragma unroll
+        for (int o = 0; o < 3; o++) {
+            tt[o] = t[(int64_t)o * HW];
+            e[o] = fc[o] - tt[o];
+            part += l1w * fabsf(e[o]);
+        }
+        if (rw) {
+#pragma unroll
+            for (int o = 0; o < 3; o++) {
+                float r = 0.f;
+#pragma unroll
+                for (int c = 0; c < 32; c++) r = fmaf(rw[32 * o + c], fc[c], r);
+                const float d = r - tt[o];
+                part += rfw * fabsf(d);
+                s[o] = rfw * inv_n * sgnf(d);
+            }
+        }
+        float* g = dL + (int64_t)b * 32 * HW + p;
+#pragma unroll
+        for (int c = 0; c < 32; c++) {
+            float v = rw ? fmaf(rw[c], s[0], fmaf(rw[32 + c], s[1], rw[64 + c] * s[2])) : 0.f;
+            if (c < 3) {
+                v += l1w * inv_n * sgnf(e[c]);
+                if (extra) v += extra[(int64_t)b * 3 * HW + (int64_t)c * HW + p];
+            }
+            g[(int64_t)c * HW] = v;
+        }
+    }
+    red[threadIdx.x] = part;
+    __syncthreads();
+    for (int h = 128; h > 0; h >>= 1) {
+        if ((int)threadIdx.x < h) red[threadIdx.x] += red[threadIdx.x + h];
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) partials[(int64_t)b * gridDim.x + blockIdx.x] = red[0] * inv_n;
+}
+
 }  // namespace gsr
 
 using namespace gsr;
@@ -215,6 +274,27 @@ int gsr_fused_ssim_backward(int B, int CH, int H, int W, float C1, float C2, con
                        dm_dmu1, dm_dsigma1_sq, dm_dsigma12, dL_dimg1);
     hipError_t e = hipGetLastError();
     return e == hipSuccess ? 0 : api_fail(GSR_ERR_HIP, hipGetErrorString(e));
+}
+
+int gsr_image_loss_partials(int B, int H, int W) {
+    if (B <= 0 || H <= 0 || W <= 0) return 0;
+    return B * ((H * W + 255) / 256);
+}
+
+int gsr_image_loss(int B, int H, int W, const float* feat, const float* target, const float* refine_w,
+                   float l1_weight, float refine_weight, const float* extra_grad, float* dL_dfeat,
+                   float* loss_partials, void* stream) {
+    if (B <= 0 || H <= 0 || W <= 0) return gsr::api_fail(GSR_ERR_ARG, "gsr_image_loss: bad sizes");
+    if (!feat || !target || !dL_dfeat || !loss_partials)
+        return gsr::api_fail(GSR_ERR_ARG, "gsr_image_loss: null required pointer");
+    const int HW = H * W;
+    const double n = 3.0 * (double)B * (double)HW;
+    hipLaunchKernelGGL(gsr::k_image_loss, dim3((HW + 255) / 256, B), dim3(256), 0, (hipStream_t)stream, HW,
+                       feat, target, refine_w, l1_weight, refine_weight, (float)(1.0 / n), extra_grad, dL_dfeat,
+                       loss_partials);
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return gsr::api_fail(GSR_ERR_HIP, hipGetErrorString(e));
+    return 0;
 }
 
 }  // extern "C"

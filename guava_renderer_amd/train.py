@@ -7,7 +7,8 @@ batch, Optimization_Loss, fabric.backward -> DDP gradient all-reduce, Adam step)
      raw_renders term, utils/loss_utils.py:116-119; fused_ssim HIP kernels) + L1 of a refined image
      made from ALL 32 channels (the reference's `renders` term, :92; its StyleUNet refiner is out
      of scope, so a fixed random 1x1 conv 32 -> 3 stands in), so every feature channel carries a
-     gradient into the rasterizer backward as in the reference's training;
+     gradient into the rasterizer backward as in the reference's training; the L1 terms and the
+     gradient assembly are one gfx950 pass (gsr_image_loss);
   3. BatchRasterizer.backward(shared=True) (render_bwd + cov/preprocess backward kernels) -> the
      shared attributes' gradients [P,k], summed over the frames inside the kernels (no [B,P,k]
      buffers);
@@ -24,6 +25,7 @@ The reference trains networks that predict the Gaussians; those networks are out
 (SURVEY.md 2.1), so the trainable parameters are the Gaussian attributes themselves -- the
 rasterizer-side work of the step (fwd, bwd, SSIM, all-reduce, update) is the same.
 """
+import ctypes
 import os
 import warnings
 
@@ -55,7 +57,7 @@ class SplatTrainer:
         g = torch.Generator().manual_seed(11)
         self.refine_w = ((torch.rand((3, C), generator=g) * 2 - 1) / C ** 0.5).to(self.dev) if refine_head else None
         self.shared_backward = os.environ.get("GSR_TRAIN_PERFRAME") != "1"  # "1": per-frame grads + sum (A/B)
-        self.dL_rgb = None if refine_head else torch.zeros((B, C, H, W), dtype=torch.float32, device=self.dev)
+        self._loss_bufs = None  # (per-workgroup loss partials, dL/dfeatures [B,32,H,W])
 
     def _grow(self, err):
         """An earlier step overflowed (and was skipped on the device): grow the workspace to 1.5x the
@@ -78,22 +80,26 @@ class SplatTrainer:
         col, _, _ = self.rast.forward(p["means3D"].detach(), p["colors"].detach(), p["opacities"].detach(),
                                       p["scales"].detach(), p["rotations"].detach(), views, projs, tanf,
                                       self.bg)
+        # SSIM term through autograd (fused_ssim kernels); the two L1 terms, their gradient and the
+        # SSIM gradient's addition in one pass over the 32-channel frames (gsr_image_loss)
         img = col[:, :3].detach().requires_grad_(True)
-        loss = self.rgb_loss(img, target)
-        loss.backward()
-        if self.refine_w is not None:
-            # the refined-image L1 term and its gradient in closed form (two passes over the
-            # 32-channel frames instead of autograd's slice / conv / sum chain)
-            B, _, H, W = col.shape
-            refined = torch.matmul(self.refine_w, col.view(B, C, H * W))  # [B,3,HW]
-            diff = refined.view(B, 3, H, W) - target
-            loss = loss + diff.abs().mean()
-            s = torch.sign(diff).mul_(1.0 / diff.numel()).view(B, 3, H * W)
-            dL = torch.matmul(self.refine_w.t(), s).view(B, C, H, W)
-            dL[:, :3] += img.grad
-        else:
-            dL = self.dL_rgb
-            dL[:, :3].copy_(img.grad)
+        ssim_term = self.lambda_ssim * (1.0 - fused_ssim(img, target))
+        ssim_term.backward()
+        tgt = target.detach().to(torch.float32).contiguous()
+        B, _, H, W = col.shape
+        L = _lib.load()
+        n_part = L.gsr_image_loss_partials(B, H, W)
+        if self._loss_bufs is None or self._loss_bufs[0].shape[0] != n_part:
+            self._loss_bufs = (torch.empty((n_part,), dtype=torch.float32, device=self.dev),
+                               torch.empty_like(col))
+        part, dL = self._loss_bufs
+        _lib.check(L.gsr_image_loss(B, H, W, col.data_ptr(), tgt.data_ptr(),
+                                    self.refine_w.data_ptr() if self.refine_w is not None else None,
+                                    1.0 - self.lambda_ssim, 1.0 if self.refine_w is not None else 0.0,
+                                    img.grad.contiguous().data_ptr(), dL.data_ptr(), part.data_ptr(),
+                                    ctypes.c_void_p(torch.cuda.current_stream(self.dev).cuda_stream)),
+                   "gsr_image_loss")
+        loss = ssim_term.detach() + part.sum()
         g = self.rast.backward(p["means3D"].detach(), p["colors"].detach(), p["opacities"].detach(),
                                p["scales"].detach(), p["rotations"].detach(), views, projs, tanf, self.bg,
                                dL, self.dinv, shared=self.shared_backward)

@@ -242,3 +242,34 @@ def test_shared_backward_equals_summed_per_frame_backward():
             ref = per[k].sum(0).cpu().numpy()
             err = _rel_err(sh[k].cpu().numpy(), ref)
             assert err <= 1e-5, f"{k} (invdepth {di is not None}): {err:.3g}"
+
+
+def test_image_loss_kernel_matches_autograd():
+    """gsr_image_loss (the trainer's two L1 terms + the SSIM gradient's addition, one pass) vs torch
+    autograd of SplatTrainer.loss's L1 terms on the same features (float64)."""
+    import ctypes
+    from guava_renderer_amd import _lib
+    gen = torch.Generator(device=DEV).manual_seed(21)
+    B, H, W = 2, 64, 96
+    feat = torch.rand((B, 32, H, W), device=DEV, generator=gen)
+    tgt = torch.rand((B, 3, H, W), device=DEV, generator=gen)
+    extra = torch.randn((B, 3, H, W), device=DEV, generator=gen) * 1e-3
+    rw = (torch.rand((3, 32), device=DEV, generator=gen) * 2 - 1) / 32 ** 0.5
+    L = _lib.load()
+    for use_rw in (True, False):
+        part = torch.empty((L.gsr_image_loss_partials(B, H, W),), device=DEV)
+        dL = torch.empty_like(feat)
+        _lib.check(L.gsr_image_loss(B, H, W, feat.data_ptr(), tgt.data_ptr(), rw.data_ptr() if use_rw else None,
+                                    0.8, 1.0 if use_rw else 0.0, extra.data_ptr(), dL.data_ptr(), part.data_ptr(),
+                                    ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)), "gsr_image_loss")
+        f = feat.double().cpu().requires_grad_(True)
+        t = tgt.double().cpu()
+        ref = 0.8 * (f[:, :3] - t).abs().mean()
+        if use_rw:
+            ref = ref + (torch.einsum("oc,bchw->bohw", rw.double().cpu(), f) - t).abs().mean()
+        ref.backward()
+        g = f.grad.clone()
+        g[:, :3] += extra.double().cpu()
+        torch.cuda.synchronize()
+        assert abs(part.sum().item() - ref.item()) <= 1e-5 * abs(ref.item())
+        np.testing.assert_allclose(dL.cpu().double().numpy(), g.numpy(), atol=1e-9, rtol=1e-5)
