@@ -360,6 +360,23 @@ def main():
         e1.record()
         torch.cuda.synchronize(dev)
         deform_ms = e0.elapsed_time(e1) / a.steps
+    # the bit-exact colour accumulation on the same workload (split-bf16 off), a shorter run after
+    # the timed region: the line's `exact_accum` (N=1 avatar / raster pipelines, default mode only)
+    exact_line = None
+    if dist is None and not a.exact_accum and a.pipeline in ("avatar", "raster"):
+        _lib.set_split_bf16(False)
+        n_ex = max(20, a.steps // 4)
+        for _ in range(3):
+            step()
+        torch.cuda.synchronize(dev)
+        t_ex = time.perf_counter()
+        for _ in range(n_ex):
+            step()
+        torch.cuda.synchronize(dev)
+        ms_ex = (time.perf_counter() - t_ex) / n_ex * 1e3
+        _lib.set_split_bf16(True)
+        exact_line = {"value": round(1e3 * B / ms_ex, 2), "ms_per_step": round(ms_ex, 4), "steps": n_ex,
+                      "colour_accum": "f32 mfma (bit-exact with the oracle)"}
     # work counters of one extra (instrumented, untimed) step: which wall the render kernel hits
     work = render_counters(step, device=dev)
     if a.pipeline == "train":
@@ -458,6 +475,8 @@ def main():
         out["latency_ms_per_frame"] = round(1000.0 * el / (a.steps * B), 4)
     if deform_ms is not None:
         out["deform_ms_per_step"] = round(deform_ms, 4)
+    if exact_line is not None:
+        out["exact_accum"] = exact_line
     if a.stages:
         out["stage_ms_per_step"] = {k: round(v[0] / max(v[1], 1), 4) for k, v in prof.items()}
     if rank == 0 and world == 1 and not a.no_cpu_baseline and a.pipeline != "train":
