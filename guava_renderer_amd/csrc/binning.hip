@@ -687,7 +687,7 @@ __device__ __forceinline__ uint32_t strip_mask(float4 co, float4 pre, float2 m, 
 // 64-bit masks per column and per row, in LDS), and base[] advances by the pass's per-tile totals.
 // The (chunk x tile) table and the per-workgroup base[] load shrink with the chunk, not the pass.
 template <int ABL>  // timing ablations (GSR_SCATTER_ABLATE): 1 = no strip test, 2 = no list store
-__global__ __launch_bounds__(kSlots) void k_ordered_scatter(Dims d, GeomArena g, ImageArena im, BinArena bn) {
+__global__ __launch_bounds__(kSlots) __attribute__((amdgpu_waves_per_eu(6))) void k_ordered_scatter(Dims d, GeomArena g, ImageArena im, BinArena bn) {
     uint32_t sink = 0;
     extern __shared__ uint64_t masks[];  // colm[gx][4], rowm[gy][4], then uint32 tile bases[T]
     __shared__ uint32_t s_pref[kSlots];
