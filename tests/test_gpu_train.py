@@ -34,15 +34,15 @@ def _scene_c2(cams=1, seed=0):
     return sc, scenes.frame_cameras(max(cams, 2), 512, 512, seed=1000)
 
 
-def _oracle_grads(sc, cam, dL, dLinv):
+def _oracle_grads(sc, cam, dL, dLinv, W=512):
     import oracle
-    oracle.set_threads(8)
+    oracle.set_threads(16)
     bg = np.zeros(32, np.float32)
     _, _, _, st = oracle.forward(sc["means3D"], sc["colors"], sc["opacities"], sc["scales"], sc["rotations"],
-                                 None, cam["viewmatrix"], cam["projmatrix"], 512, 512, cam["tanfovx"],
+                                 None, cam["viewmatrix"], cam["projmatrix"], W, W, cam["tanfovx"],
                                  cam["tanfovy"], bg)
     return oracle.backward(st, sc["means3D"], sc["colors"], sc["opacities"], sc["scales"], sc["rotations"],
-                           None, cam["viewmatrix"], cam["projmatrix"], 512, 512, cam["tanfovx"], cam["tanfovy"],
+                           None, cam["viewmatrix"], cam["projmatrix"], W, W, cam["tanfovx"], cam["tanfovy"],
                            bg, dL, dLinv)
 
 
@@ -72,6 +72,38 @@ def test_fullsize_backward_single_frame_drop_in():
     for name, a, b in zip(NAMES, grads, o):
         if b.size:
             err = _rel_err(a.cpu().numpy(), b)
+            assert err <= TOL, f"{name}: {err:.3g}"
+
+
+def test_config5_backward_single_frame():
+    """Config 5 (300k Gaussians, 3 per UV texel, 1024^2): one frame's gradients through the batched
+    entry vs the oracle, 1e-4 of each gradient's scale."""
+    from guava_renderer_amd import _lib, scenes
+    from guava_renderer_amd.batch import BatchRasterizer
+    _lib.set_exact_exp(True)
+    P, W = 300000, 1024
+    sc = scenes.avatar_cloud(P, seed=0, gaussians_per_texel=3)
+    cam = scenes.frame_cameras(2, W, W, seed=1000)[1]
+    t = lambda x: torch.tensor(np.ascontiguousarray(x), device=DEV)  # noqa: E731
+    views = t(cam["viewmatrix"].reshape(1, 16))
+    projs = t(cam["projmatrix"].reshape(1, 16))
+    tanf = t(np.array([[cam["tanfovx"], cam["tanfovy"]]], np.float32))
+    args = [t(sc[k]) for k in ("means3D", "colors", "opacities", "scales", "rotations")]
+    r = BatchRasterizer(1, P, W, W, R_capacity=40 * P, device=DEV)
+    r.forward(*args, views, projs, tanf, torch.zeros((1, 32), device=DEV))
+    rng = np.random.default_rng(13)
+    dL = rng.normal(size=(1, 32, W, W)).astype(np.float32)
+    dLinv = rng.normal(size=(1, W, W)).astype(np.float32)
+    g = r.backward(*args, views, projs, tanf, torch.zeros((1, 32), device=DEV), t(dL), t(dLinv))
+    torch.cuda.synchronize()
+    assert not r.status()[1]
+    gpu = {k: v[0].cpu().numpy() for k, v in g.items() if v is not None}
+    o = _oracle_grads(sc, cam, dL[0], dLinv, W=W)
+    mine = {"means2D": gpu["mean2D"], "colors": gpu["colors"], "opacity": gpu["opacity"], "means3D": gpu["means3D"],
+            "cov3D": gpu["cov3D"], "scales": gpu["scales"], "rotations": gpu["rotations"]}
+    for name, b in zip(NAMES, o):
+        if name in mine:
+            err = _rel_err(mine[name], b)
             assert err <= TOL, f"{name}: {err:.3g}"
 
 
