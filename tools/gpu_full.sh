@@ -19,6 +19,8 @@ timeout -k 10 300 python bench.py --pipeline frame --steps 20 --warmup 3 --no-cp
 [ $rc -eq 0 ] || exit $rc
 timeout -k 10 300 python bench.py --pipeline train --batch 6 --steps 100 --warmup 10 --no-cpu-baseline > $OUT/bench_train.json 2> $OUT/bench_train.err; rc=$?; echo "train rc=$rc"
 [ $rc -eq 0 ] || exit $rc
+timeout -k 10 300 python bench.py --config c5 --pipeline raster --steps 20 --warmup 3 --no-cpu-baseline --stages > $OUT/bench_c5.json 2> $OUT/bench_c5.err; rc=$?; echo "c5 rc=$rc"
+[ $rc -eq 0 ] || exit $rc
 GSR_DIST_BACKEND=gloo timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus 2 --steps 20 --warmup 3 --no-cpu-baseline > $OUT/bench_n2.json 2> $OUT/bench_n2.err; rc=$?; echo "n2 rc=$rc"
 [ $rc -eq 0 ] || exit $rc
 timeout -k 10 300 python tools/bench_ssim.py > $OUT/ssim.json 2> $OUT/ssim.err; rc=$?; echo "ssim rc=$rc"
