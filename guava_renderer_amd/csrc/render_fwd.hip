@@ -220,7 +220,7 @@ __device__ __forceinline__ void overflow_fill(const Dims& d, const Outputs& o) {
 // in three rotating register slots: the records and feature operand of step s+3 are loaded while
 // step s+1's alphas (the exp-heavy, transmittance-independent part) are computed and step s's
 // serial blend and MFMA accumulation run.
-template <bool EXACT, bool STATS, bool TL, bool REFINE, int ABL = 0, int SPLIT = 0>
+template <bool EXACT, bool STATS, bool TL, bool REFINE, int ABL = 0, int SPLIT = 0, int NSLOT = 3>
 __device__ __forceinline__ void render_fwd_body(const Dims& d, const Inputs& in, const GeomArena& g,
                                                 const ImageArena& im, const BinArena& bn,
                                                 const Outputs& o) {
@@ -414,21 +414,52 @@ __device__ __forceinline__ void render_fwd_body(const Dims& d, const Inputs& in,
         GSR_SLOT(C)
         // An invalid slot takes nothing (alpha 0, feature 0); the loop leaves only at its head and
         // its foot, which keeps the MFMA accumulators in one register chain.
-        GSR_FETCH(A)
-        GSR_FETCH(B)
-        GSR_FETCH(C)
-        GSR_ALPHA(A)
-        while (Av) {
-            GSR_ALPHA(B)
-            GSR_TAKE(A)
+        if constexpr (NSLOT == 3) {
             GSR_FETCH(A)
-            GSR_ALPHA(C)
-            GSR_TAKE(B)
             GSR_FETCH(B)
-            GSR_ALPHA(A)
-            GSR_TAKE(C)
             GSR_FETCH(C)
-            if (!__any(!done)) break;  // every pixel of the strip finished
+            GSR_ALPHA(A)
+            while (Av) {
+                GSR_ALPHA(B)
+                GSR_TAKE(A)
+                GSR_FETCH(A)
+                GSR_ALPHA(C)
+                GSR_TAKE(B)
+                GSR_FETCH(B)
+                GSR_ALPHA(A)
+                GSR_TAKE(C)
+                GSR_FETCH(C)
+                if (!__any(!done)) break;  // every pixel of the strip finished
+            }
+        } else {
+            // latency mode (single-frame launches, where one wave's strip sets the kernel time): five
+            // slots, each slot's records requested four k-steps before its alphas
+            GSR_SLOT(D)
+            GSR_SLOT(E)
+            GSR_FETCH(A)
+            GSR_FETCH(B)
+            GSR_FETCH(C)
+            GSR_FETCH(D)
+            GSR_FETCH(E)
+            GSR_ALPHA(A)
+            while (Av) {
+                GSR_ALPHA(B)
+                GSR_TAKE(A)
+                GSR_FETCH(A)
+                GSR_ALPHA(C)
+                GSR_TAKE(B)
+                GSR_FETCH(B)
+                GSR_ALPHA(D)
+                GSR_TAKE(C)
+                GSR_FETCH(C)
+                GSR_ALPHA(E)
+                GSR_TAKE(D)
+                GSR_FETCH(D)
+                GSR_ALPHA(A)
+                GSR_TAKE(E)
+                GSR_FETCH(E)
+                if (!__any(!done)) break;
+            }
         }
 #undef GSR_NEXT
 #undef GSR_FETCH
@@ -466,10 +497,10 @@ __device__ __forceinline__ void render_fwd_body(const Dims& d, const Inputs& in,
     }
 }
 
-template <bool EXACT, bool STATS, bool TL, int SPLIT = 0>
+template <bool EXACT, bool STATS, bool TL, int SPLIT = 0, int NSLOT = 3>
 __global__ __launch_bounds__(GSR_TILE_PIX) void k_render_fwd(Dims d, Inputs in, GeomArena g,
                                                              ImageArena im, BinArena bn, Outputs o) {
-    render_fwd_body<EXACT, STATS, TL, false, 0, SPLIT>(d, in, g, im, bn, o);
+    render_fwd_body<EXACT, STATS, TL, false, 0, SPLIT, NSLOT>(d, in, g, im, bn, o);
 }
 
 // Timing ablations of the production kernel (GSR_RENDER_ABLATE=1: VALU stand-in for the MFMAs,
@@ -498,6 +529,8 @@ void launch_render_fwd(const Dims& d, const Inputs& in, const GeomArena& g, cons
     // workgroups per CU: resident capacity (4 waves/SIMD at the kernel's register count) by default,
     // so no render workgroup waits in the dispatcher ahead of another stream's kernels
     static const int wg_per_cu = [] { const char* e = getenv("GSR_RENDER_WG_PER_CU"); return e ? atoi(e) : 4; }();
+    // GSR_RENDER_LATENCY=0: single-frame launches use the throughput kernel (A/B)
+    static const bool latency_mode = [] { const char* e = getenv("GSR_RENDER_LATENCY"); return !(e && e[0] == '0'); }();
     const int grid = min((nwaves + 3) / 4, persistent_grid(wg_per_cu));
     const dim3 gr(grid), bl(GSR_TILE_PIX);
 #define GSR_LAUNCH(E, S, L) hipLaunchKernelGGL((k_render_fwd<E, S, L>), gr, bl, 0, s, d, in, g, im, b, o)
@@ -510,6 +543,16 @@ void launch_render_fwd(const Dims& d, const Inputs& in, const GeomArena& g, cons
     else if (ablate == 1) hipLaunchKernelGGL((k_render_fwd_ablate<1>), gr, bl, 0, s, d, in, g, im, b, o);
     else if (ablate == 2) hipLaunchKernelGGL((k_render_fwd_ablate<2>), gr, bl, 0, s, d, in, g, im, b, o);
     else if (ablate == 4) hipLaunchKernelGGL((k_render_fwd_ablate<4>), gr, bl, 0, s, d, in, g, im, b, o);
+    else if (d.B == 1 && latency_mode) {  // one frame: the longest strip's wave sets the time
+        const dim3 gl(min((nwaves + 3) / 4, persistent_grid(3)));  // 3 waves per SIMD at 5 slots
+        if (split) {
+            if (exact) hipLaunchKernelGGL((k_render_fwd<true, false, false, 1, 5>), gl, bl, 0, s, d, in, g, im, b, o);
+            else hipLaunchKernelGGL((k_render_fwd<false, false, false, 1, 5>), gl, bl, 0, s, d, in, g, im, b, o);
+        } else {
+            if (exact) hipLaunchKernelGGL((k_render_fwd<true, false, false, 0, 5>), gl, bl, 0, s, d, in, g, im, b, o);
+            else hipLaunchKernelGGL((k_render_fwd<false, false, false, 0, 5>), gl, bl, 0, s, d, in, g, im, b, o);
+        }
+    }
     else if (split && in.s_colors == 0) {  // one feature set for the batch: split it once
         hipLaunchKernelGGL(k_split_features, dim3((d.P * GSR_C / 4 + 255) / 256), dim3(256), 0, s,
                            d.P * GSR_C / 4, reinterpret_cast<const float4*>(in.colors),
