@@ -28,6 +28,18 @@
 
 namespace gsr {
 
+// How a k-step's two render records reach the wave (every lane needs both, uniform):
+//  0: four wave-uniform 16-B vector loads (each returns 1 KB through the texture data path);
+//  1: scalar loads (s_load_dwordx8: out-of-order returns, so every use waits for all of them);
+//  2: one 4-B vector load spread over lanes 0..15 (lane j: dword j&7 of record a or b), broadcast
+//     to SGPRs with v_readlane at the alpha stage.
+#ifndef GSR_REC_PATH
+#define GSR_REC_PATH 0
+#endif
+#ifndef GSR_BATCH_NSLOT
+#define GSR_BATCH_NSLOT 3  // pipeline slots of the batched (throughput) kernels
+#endif
+
 typedef float floatx16 __attribute__((ext_vector_type(16)));
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef unsigned uint4x __attribute__((ext_vector_type(4)));
@@ -85,6 +97,19 @@ __global__ __launch_bounds__(256) void k_split_features(int n4, const float4* __
 // one 16-byte half of a render record at a wave-uniform byte offset (SGPR soffset)
 __device__ __forceinline__ float4 rec_load(__amdgpu_buffer_rsrc_t rs, uint32_t off) {
     return __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rs, 0, (int)off, 0));
+}
+
+// one 16-byte half of a render record through the scalar data path (constant address space, index
+// wave-uniform: s_load_dwordx4 into SGPRs)
+typedef float floatx4 __attribute__((ext_vector_type(4)));
+typedef const floatx4 __attribute__((address_space(4))) cfloatx4;
+__device__ __forceinline__ float4 srec_load(const cfloatx4* __restrict__ p, uint32_t i) {
+    return __builtin_bit_cast(float4, p[i]);
+}
+
+// dword j of a k-step's record pair, held one per lane (GSR_REC_PATH 2), as a wave-uniform value
+__device__ __forceinline__ float rec_lane(unsigned v, int j) {
+    return __int_as_float(__builtin_amdgcn_readlane((int)v, j));
 }
 
 // Epilogue of one strip: final_T, n_contrib, inverse depth (lane = pixel) and the 32
@@ -288,6 +313,8 @@ __device__ __forceinline__ void render_fwd_body(const Dims& d, const Inputs& in,
         // one SGPR, no 64-bit address arithmetic per survivor
         const __amdgpu_buffer_rsrc_t rrs = __builtin_amdgcn_make_buffer_rsrc(
             (void*)(g.rrec + (int64_t)b * d.P * 2), 0, (int)min((int64_t)d.P * 32, (int64_t)0x7FFFFFFF), 0x00020000);
+        // the same records through the scalar path (GSR_REC_PATH 1)
+        const cfloatx4* __restrict__ srec = (const cfloatx4*)(g.rrec + (int64_t)b * d.P * 2);
         // feature rows through a buffer resource: 32-bit byte offsets, the base in SGPRs
         // (SPLIT == 2: the pre-split (hi, lo) words of k_split_features, shared by every frame)
         const __amdgpu_buffer_rsrc_t frs = __builtin_amdgcn_make_buffer_rsrc(
@@ -349,14 +376,30 @@ __device__ __forceinline__ void render_fwd_body(const Dims& d, const Inputs& in,
                 if (!S##hb) { gb_ = ga_; pb_ = pa_; }                                               \
             }                                                                                       \
             S##pa = pa_; S##pb = pb_;                                                               \
-            S##a0 = rec_load(rrs, ga_ * 32); S##a1 = rec_load(rrs, ga_ * 32 + 16);                  \
-            S##b0 = rec_load(rrs, gb_ * 32); S##b1 = rec_load(rrs, gb_ * 32 + 16);                  \
+            if (GSR_REC_PATH == 2) {                                                                \
+                S##r = __builtin_amdgcn_raw_buffer_load_b32(                                        \
+                    rrs, (int)(((lane & 8) ? gb_ : ga_) * 32 + (lane & 7) * 4), 0, 0);              \
+            } else if (GSR_REC_PATH == 1) {                                                         \
+                S##a0 = srec_load(srec, 2 * ga_); S##a1 = srec_load(srec, 2 * ga_ + 1);             \
+                S##b0 = srec_load(srec, 2 * gb_); S##b1 = srec_load(srec, 2 * gb_ + 1);             \
+            } else {                                                                                \
+                S##a0 = rec_load(rrs, ga_ * 32); S##a1 = rec_load(rrs, ga_ * 32 + 16);              \
+                S##b0 = rec_load(rrs, gb_ * 32); S##b1 = rec_load(rrs, gb_ * 32 + 16);              \
+            }                                                                                       \
             S##f = ABL == 2 ? 0.f : __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(           \
                 frs, (int)(((hi ? gb_ : ga_) * GSR_C + ch) * 4), 0, 0));                            \
         }
         // stage 2: the pixel-local alphas of slot S (a missing survivor has alpha 0)
 #define GSR_ALPHA(S)                                                                                \
         {                                                                                           \
+            if (GSR_REC_PATH == 2) {  /* dwords 0..6 of each record (w of the second half unused) */ \
+                S##a0 = make_float4(rec_lane(S##r, 0), rec_lane(S##r, 1), rec_lane(S##r, 2),          \
+                                    rec_lane(S##r, 3));                                             \
+                S##a1 = make_float4(rec_lane(S##r, 4), rec_lane(S##r, 5), rec_lane(S##r, 6), 0.f);    \
+                S##b0 = make_float4(rec_lane(S##r, 8), rec_lane(S##r, 9), rec_lane(S##r, 10),         \
+                                    rec_lane(S##r, 11));                                            \
+                S##b1 = make_float4(rec_lane(S##r, 12), rec_lane(S##r, 13), rec_lane(S##r, 14), 0.f); \
+            }                                                                                       \
             S##al = S##v ? alpha_of<EXACT>(S##a0, S##a1, pfx, pfy) : 0.f;                           \
             S##bl = S##hb ? alpha_of<EXACT>(S##b0, S##b1, pfx, pfy) : 0.f;                          \
             S##ai = S##a0.w;                                                                        \
@@ -407,7 +450,7 @@ __device__ __forceinline__ void render_fwd_body(const Dims& d, const Inputs& in,
                 acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(fa_, __uint_as_float(sw_[1]), acc1, 0, 0, 0); \
             }                                                                                       \
         }
-#define GSR_SLOT(S) bool S##v, S##hb; int S##pa, S##pb; float4 S##a0, S##a1, S##b0, S##b1; \
+#define GSR_SLOT(S) bool S##v, S##hb; int S##pa, S##pb; float4 S##a0, S##a1, S##b0, S##b1; unsigned S##r; \
         float S##f, S##al, S##bl, S##ai, S##bi; unsigned S##fp = 0;
         GSR_SLOT(A)
         GSR_SLOT(B)
@@ -497,7 +540,7 @@ __device__ __forceinline__ void render_fwd_body(const Dims& d, const Inputs& in,
     }
 }
 
-template <bool EXACT, bool STATS, bool TL, int SPLIT = 0, int NSLOT = 3>
+template <bool EXACT, bool STATS, bool TL, int SPLIT = 0, int NSLOT = GSR_BATCH_NSLOT>
 __global__ __launch_bounds__(GSR_TILE_PIX) void k_render_fwd(Dims d, Inputs in, GeomArena g,
                                                              ImageArena im, BinArena bn, Outputs o) {
     render_fwd_body<EXACT, STATS, TL, false, 0, SPLIT, NSLOT>(d, in, g, im, bn, o);
