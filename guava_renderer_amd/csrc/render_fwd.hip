@@ -30,11 +30,14 @@ namespace gsr {
 
 // How a k-step's two render records reach the wave (every lane needs both, uniform):
 //  0: four wave-uniform 16-B vector loads (each returns 1 KB through the texture data path);
-//  1: scalar loads (s_load_dwordx8: out-of-order returns, so every use waits for all of them);
-//  2: one 4-B vector load spread over lanes 0..15 (lane j: dword j&7 of record a or b), broadcast
-//     to SGPRs with v_readlane at the alpha stage.
+//  3: one 4-B vector load spread over lanes 0..15 (lane j: dword j&7 of record a or b), broadcast
+//     through a per-wave LDS slot (ds_write, four uniform-address ds_read_b128).
+// (Scalar loads and a v_readlane broadcast were measured and dropped: DESIGN.md §7.)
 #ifndef GSR_REC_PATH
-#define GSR_REC_PATH 0
+#define GSR_REC_PATH 3
+#endif
+#ifndef GSR_MFMA_K8
+#define GSR_MFMA_K8 1  // split-bf16 products on v_mfma_f32_32x32x8_bf16 (0: 32x32x16 with k 4..7 zero)
 #endif
 #ifndef GSR_BATCH_NSLOT
 #define GSR_BATCH_NSLOT 3  // pipeline slots of the batched (throughput) kernels
@@ -43,6 +46,8 @@ namespace gsr {
 typedef float floatx16 __attribute__((ext_vector_type(16)));
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef unsigned uint4x __attribute__((ext_vector_type(4)));
+typedef unsigned uint2x __attribute__((ext_vector_type(2)));
+typedef short shortx4 __attribute__((ext_vector_type(4)));
 
 // The blend step of forward.cu:349-381 split in two (both halves are branch-free):
 //  * alpha_of: the pixel-local alpha of one Gaussian, independent of the pixel's transmittance, with
@@ -94,22 +99,10 @@ __global__ __launch_bounds__(256) void k_split_features(int n4, const float4* __
     }
 }
 
-// one 16-byte half of a render record at a wave-uniform byte offset (SGPR soffset)
+// one 16-byte half of a render record at a wave-uniform byte offset (voffset, so that the range
+// check turns the null index P into zeros)
 __device__ __forceinline__ float4 rec_load(__amdgpu_buffer_rsrc_t rs, uint32_t off) {
-    return __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rs, 0, (int)off, 0));
-}
-
-// one 16-byte half of a render record through the scalar data path (constant address space, index
-// wave-uniform: s_load_dwordx4 into SGPRs)
-typedef float floatx4 __attribute__((ext_vector_type(4)));
-typedef const floatx4 __attribute__((address_space(4))) cfloatx4;
-__device__ __forceinline__ float4 srec_load(const cfloatx4* __restrict__ p, uint32_t i) {
-    return __builtin_bit_cast(float4, p[i]);
-}
-
-// dword j of a k-step's record pair, held one per lane (GSR_REC_PATH 2), as a wave-uniform value
-__device__ __forceinline__ float rec_lane(unsigned v, int j) {
-    return __int_as_float(__builtin_amdgcn_readlane((int)v, j));
+    return __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rs, (int)off, 0, 0));
 }
 
 // Epilogue of one strip: final_T, n_contrib, inverse depth (lane = pixel) and the 32
@@ -313,8 +306,9 @@ __device__ __forceinline__ void render_fwd_body(const Dims& d, const Inputs& in,
         // one SGPR, no 64-bit address arithmetic per survivor
         const __amdgpu_buffer_rsrc_t rrs = __builtin_amdgcn_make_buffer_rsrc(
             (void*)(g.rrec + (int64_t)b * d.P * 2), 0, (int)min((int64_t)d.P * 32, (int64_t)0x7FFFFFFF), 0x00020000);
-        // the same records through the scalar path (GSR_REC_PATH 1)
-        const cfloatx4* __restrict__ srec = (const cfloatx4*)(g.rrec + (int64_t)b * d.P * 2);
+        // this wave's record staging slot (GSR_REC_PATH 3)
+        __shared__ unsigned rec_lds_all[GSR_TILE_PIX / 64][16];
+        unsigned* rec_lds = rec_lds_all[threadIdx.x >> 6];
         // feature rows through a buffer resource: 32-bit byte offsets, the base in SGPRs
         // (SPLIT == 2: the pre-split (hi, lo) words of k_split_features, shared by every frame)
         const __amdgpu_buffer_rsrc_t frs = __builtin_amdgcn_make_buffer_rsrc(
@@ -373,15 +367,15 @@ __device__ __forceinline__ void render_fwd_body(const Dims& d, const Inputs& in,
             } else {                                                                                \
                 S##v = GSR_NEXT(ga_, pa_);                                                          \
                 S##hb = S##v && GSR_NEXT(gb_, pb_);                                                 \
-                if (!S##hb) { gb_ = ga_; pb_ = pa_; }                                               \
+                /* a missing survivor reads index P: past both buffer resources' ranges, so its */  \
+                /* record and feature load as zeros, opacity 0 gives alpha 0 and nothing is taken */ \
+                if (!S##v) ga_ = (uint32_t)d.P;                                                     \
+                if (!S##hb) { gb_ = (uint32_t)d.P; pb_ = pa_; }                                     \
             }                                                                                       \
             S##pa = pa_; S##pb = pb_;                                                               \
-            if (GSR_REC_PATH == 2) {                                                                \
+            if (GSR_REC_PATH == 3) {                                                                \
                 S##r = __builtin_amdgcn_raw_buffer_load_b32(                                        \
                     rrs, (int)(((lane & 8) ? gb_ : ga_) * 32 + (lane & 7) * 4), 0, 0);              \
-            } else if (GSR_REC_PATH == 1) {                                                         \
-                S##a0 = srec_load(srec, 2 * ga_); S##a1 = srec_load(srec, 2 * ga_ + 1);             \
-                S##b0 = srec_load(srec, 2 * gb_); S##b1 = srec_load(srec, 2 * gb_ + 1);             \
             } else {                                                                                \
                 S##a0 = rec_load(rrs, ga_ * 32); S##a1 = rec_load(rrs, ga_ * 32 + 16);              \
                 S##b0 = rec_load(rrs, gb_ * 32); S##b1 = rec_load(rrs, gb_ * 32 + 16);              \
@@ -392,16 +386,17 @@ __device__ __forceinline__ void render_fwd_body(const Dims& d, const Inputs& in,
         // stage 2: the pixel-local alphas of slot S (a missing survivor has alpha 0)
 #define GSR_ALPHA(S)                                                                                \
         {                                                                                           \
-            if (GSR_REC_PATH == 2) {  /* dwords 0..6 of each record (w of the second half unused) */ \
-                S##a0 = make_float4(rec_lane(S##r, 0), rec_lane(S##r, 1), rec_lane(S##r, 2),          \
-                                    rec_lane(S##r, 3));                                             \
-                S##a1 = make_float4(rec_lane(S##r, 4), rec_lane(S##r, 5), rec_lane(S##r, 6), 0.f);    \
-                S##b0 = make_float4(rec_lane(S##r, 8), rec_lane(S##r, 9), rec_lane(S##r, 10),         \
-                                    rec_lane(S##r, 11));                                            \
-                S##b1 = make_float4(rec_lane(S##r, 12), rec_lane(S##r, 13), rec_lane(S##r, 14), 0.f); \
+            if (GSR_REC_PATH == 3) {  /* through this wave's LDS slot: uniform-address b128 reads */ \
+                if (lane < 16) rec_lds[lane] = S##r;                                               \
+                __builtin_amdgcn_wave_barrier();                                                    \
+                S##a0 = __builtin_bit_cast(float4, *(const uint4x*)&rec_lds[0]);                    \
+                S##a1 = __builtin_bit_cast(float4, *(const uint4x*)&rec_lds[4]);                    \
+                S##b0 = __builtin_bit_cast(float4, *(const uint4x*)&rec_lds[8]);                    \
+                S##b1 = __builtin_bit_cast(float4, *(const uint4x*)&rec_lds[12]);                   \
+                __builtin_amdgcn_wave_barrier();                                                    \
             }                                                                                       \
-            S##al = S##v ? alpha_of<EXACT>(S##a0, S##a1, pfx, pfy) : 0.f;                           \
-            S##bl = S##hb ? alpha_of<EXACT>(S##b0, S##b1, pfx, pfy) : 0.f;                          \
+            S##al = alpha_of<EXACT>(S##a0, S##a1, pfx, pfy);                                        \
+            S##bl = alpha_of<EXACT>(S##b0, S##b1, pfx, pfy);                                        \
             S##ai = S##a0.w;                                                                        \
             S##bi = S##b0.w;                                                                        \
             if (SPLIT) S##fp = SPLIT == 2 ? __float_as_uint(S##f) : split_hl(S##f);                 \
@@ -409,7 +404,7 @@ __device__ __forceinline__ void render_fwd_body(const Dims& d, const Inputs& in,
         // stage 3: the serial blend of slot S and its accumulation on the matrix cores
 #define GSR_TAKE(S)                                                                                 \
         {                                                                                           \
-            const float f_ = (S##v && (!hi || S##hb)) ? S##f : 0.f;                                 \
+            const float f_ = S##f;                                                                  \
             const bool was_done_ = done;                                                            \
             const float wa_ = take_step(S##al, S##ai, (uint32_t)S##pa, T, invd, last, done);        \
             const bool done_a_ = done;                                                              \
@@ -434,16 +429,24 @@ __device__ __forceinline__ void render_fwd_body(const Dims& d, const Inputs& in,
                 acc0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a_, b0_, acc0, 0, 0, 0);               \
                 acc1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a_, b1_, acc1, 0, 0, 0);               \
             } else if (SPLIT) {  /* k 0..3 of each half: f_hi.w_hi + f_lo.w_hi + f_hi.w_lo + f_lo.w_lo */ \
-                const unsigned fp_ = (S##v && (!hi || S##hb)) ? S##fp : 0u;                         \
-                sa_.x = fp_; sa_.y = fp_;                                                           \
+                const unsigned fp_ = S##fp;                                                         \
                 unsigned h0_, l0_, h1_, l1_;                                                        \
                 split_hh_ll(__uint_as_float(sw_[0]), h0_, l0_);                                     \
                 split_hh_ll(__uint_as_float(sw_[1]), h1_, l1_);                                     \
-                sb0_.x = h0_; sb0_.y = l0_; sb1_.x = h1_; sb1_.y = l1_;                             \
-                acc0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, sa_),     \
-                                                               __builtin_bit_cast(bf16x8, sb0_), acc0, 0, 0, 0); \
-                acc1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, sa_),     \
-                                                               __builtin_bit_cast(bf16x8, sb1_), acc1, 0, 0, 0); \
+                if (GSR_MFMA_K8) {  /* k = 8: exactly the four products per lane half, no padding */ \
+                    const uint2x a2_ = {fp_, fp_}, b0_ = {h0_, l0_}, b1_ = {h1_, l1_};              \
+                    acc0 = __builtin_amdgcn_mfma_f32_32x32x8bf16_1k(__builtin_bit_cast(shortx4, a2_), \
+                                                                   __builtin_bit_cast(shortx4, b0_), acc0, 0, 0, 0); \
+                    acc1 = __builtin_amdgcn_mfma_f32_32x32x8bf16_1k(__builtin_bit_cast(shortx4, a2_), \
+                                                                   __builtin_bit_cast(shortx4, b1_), acc1, 0, 0, 0); \
+                } else {                                                                            \
+                    sa_.x = fp_; sa_.y = fp_;                                                       \
+                    sb0_.x = h0_; sb0_.y = l0_; sb1_.x = h1_; sb1_.y = l1_;                         \
+                    acc0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, sa_), \
+                                                                   __builtin_bit_cast(bf16x8, sb0_), acc0, 0, 0, 0); \
+                    acc1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, sa_), \
+                                                                   __builtin_bit_cast(bf16x8, sb1_), acc1, 0, 0, 0); \
+                }                                                                                   \
             } else {                                                                                \
                 const float fa_ = ABL == 2 ? 1.0f : f_;  /* timing ablation: no feature operand */  \
                 acc0 = __builtin_amdgcn_mfma_f32_32x32x2f32(fa_, __uint_as_float(sw_[0]), acc0, 0, 0, 0); \
