@@ -30,8 +30,9 @@ namespace gsr {
 
 // How a k-step's two render records reach the wave (every lane needs both, uniform):
 //  0: four wave-uniform 16-B vector loads (each returns 1 KB through the texture data path);
-//  3: one 4-B vector load spread over lanes 0..15 (lane j: dword j&7 of record a or b), broadcast
-//     through a per-wave LDS slot (ds_write, four uniform-address ds_read_b128).
+//  3: two 4-B vector loads on lanes 0..7 (lane j: dword j of record a, of record b; the record
+//     offsets in SGPRs), broadcast through a per-wave LDS slot (ds_write2, four uniform-address
+//     ds_read_b128).
 // (Scalar loads and a v_readlane broadcast were measured and dropped: DESIGN.md §7.)
 #ifndef GSR_REC_PATH
 #define GSR_REC_PATH 3
@@ -307,8 +308,16 @@ __device__ __forceinline__ void render_fwd_body(const Dims& d, const Inputs& in,
         const __amdgpu_buffer_rsrc_t rrs = __builtin_amdgcn_make_buffer_rsrc(
             (void*)(g.rrec + (int64_t)b * d.P * 2), 0, (int)min((int64_t)d.P * 32, (int64_t)0x7FFFFFFF), 0x00020000);
         // this wave's record staging slot (GSR_REC_PATH 3)
-        __shared__ unsigned rec_lds_all[GSR_TILE_PIX / 64][16];
+        // (words 0..15; lanes 8..63 write their out-of-range zeros to the spare words 24..87)
+        __shared__ unsigned rec_lds_all[GSR_TILE_PIX / 64][88];
         unsigned* rec_lds = rec_lds_all[threadIdx.x >> 6];
+        const int rec_widx = lane < 8 ? lane : 16 + lane;
+        // per-lane byte offsets, the survivor's row in the SGPR offset: lanes whose offset is kOOB
+        // fall outside the resource (num_records < 2^31, row offsets < 2^31) and read zeros
+        constexpr uint32_t kOOB = 0x80000000u;
+        const int rec_voff = (int)(lane < 8 ? (uint32_t)lane * 4 : kOOB);
+        const int feat_voff_a = (int)(hi ? kOOB : (uint32_t)ch * 4);
+        const int feat_voff_b = (int)(hi ? (uint32_t)ch * 4 : kOOB);
         // feature rows through a buffer resource: 32-bit byte offsets, the base in SGPRs
         // (SPLIT == 2: the pre-split (hi, lo) words of k_split_features, shared by every frame)
         const __amdgpu_buffer_rsrc_t frs = __builtin_amdgcn_make_buffer_rsrc(
@@ -373,21 +382,26 @@ __device__ __forceinline__ void render_fwd_body(const Dims& d, const Inputs& in,
                 if (!S##hb) { gb_ = (uint32_t)d.P; pb_ = pa_; }                                     \
             }                                                                                       \
             S##pa = pa_; S##pb = pb_;                                                               \
-            if (GSR_REC_PATH == 3) {                                                                \
-                S##r = __builtin_amdgcn_raw_buffer_load_b32(                                        \
-                    rrs, (int)(((lane & 8) ? gb_ : ga_) * 32 + (lane & 7) * 4), 0, 0);              \
+            if (GSR_REC_PATH == 3) {  /* lanes 0..7: dword `lane` of both records, SGPR offsets */  \
+                S##r = __builtin_amdgcn_raw_buffer_load_b32(rrs, rec_voff, (int)(ga_ * 32), 0);     \
+                S##r2 = __builtin_amdgcn_raw_buffer_load_b32(rrs, rec_voff, (int)(gb_ * 32), 0);    \
             } else {                                                                                \
                 S##a0 = rec_load(rrs, ga_ * 32); S##a1 = rec_load(rrs, ga_ * 32 + 16);              \
                 S##b0 = rec_load(rrs, gb_ * 32); S##b1 = rec_load(rrs, gb_ * 32 + 16);              \
             }                                                                                       \
-            S##f = ABL == 2 ? 0.f : __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(           \
-                frs, (int)(((hi ? gb_ : ga_) * GSR_C + ch) * 4), 0, 0));                            \
+            /* this lane's feature word: channel ch of survivor a (lanes 0..31) or b (32..63), */  \
+            /* the survivor's row offset in the SGPR offset (range-checked like voffset: past */    \
+            /* offset in SGPRs; the other half's lanes are out of range and read 0) */            \
+            S##fa = ABL == 2 ? 0u : __builtin_amdgcn_raw_buffer_load_b32(frs, feat_voff_a,          \
+                                                                        (int)(ga_ * (GSR_C * 4)), 0); \
+            S##fb = ABL == 2 ? 0u : __builtin_amdgcn_raw_buffer_load_b32(frs, feat_voff_b,          \
+                                                                        (int)(gb_ * (GSR_C * 4)), 0); \
         }
         // stage 2: the pixel-local alphas of slot S (a missing survivor has alpha 0)
 #define GSR_ALPHA(S)                                                                                \
         {                                                                                           \
             if (GSR_REC_PATH == 3) {  /* through this wave's LDS slot: uniform-address b128 reads */ \
-                if (lane < 16) rec_lds[lane] = S##r;                                               \
+                rec_lds[rec_widx] = S##r; rec_lds[rec_widx + 8] = S##r2;  /* lanes 8..63: spare */ \
                 __builtin_amdgcn_wave_barrier();                                                    \
                 S##a0 = __builtin_bit_cast(float4, *(const uint4x*)&rec_lds[0]);                    \
                 S##a1 = __builtin_bit_cast(float4, *(const uint4x*)&rec_lds[4]);                    \
@@ -399,6 +413,7 @@ __device__ __forceinline__ void render_fwd_body(const Dims& d, const Inputs& in,
             S##bl = alpha_of<EXACT>(S##b0, S##b1, pfx, pfy);                                        \
             S##ai = S##a0.w;                                                                        \
             S##bi = S##b0.w;                                                                        \
+            S##f = __uint_as_float(S##fa | S##fb);                                                  \
             if (SPLIT) S##fp = SPLIT == 2 ? __float_as_uint(S##f) : split_hl(S##f);                 \
         }
         // stage 3: the serial blend of slot S and its accumulation on the matrix cores
@@ -453,7 +468,7 @@ __device__ __forceinline__ void render_fwd_body(const Dims& d, const Inputs& in,
                 acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(fa_, __uint_as_float(sw_[1]), acc1, 0, 0, 0); \
             }                                                                                       \
         }
-#define GSR_SLOT(S) bool S##v, S##hb; int S##pa, S##pb; float4 S##a0, S##a1, S##b0, S##b1; unsigned S##r; \
+#define GSR_SLOT(S) bool S##v, S##hb; int S##pa, S##pb; float4 S##a0, S##a1, S##b0, S##b1; unsigned S##r, S##r2, S##fa, S##fb; \
         float S##f, S##al, S##bl, S##ai, S##bi; unsigned S##fp = 0;
         GSR_SLOT(A)
         GSR_SLOT(B)
