@@ -468,12 +468,12 @@ def main():
     ksteps = work["mfma_ksteps"]
     if a.exact_accum:
         mfma_flops = ksteps * 2 * (2 * 32 * 32 * 2)  # two v_mfma_f32_32x32x2f32 per wave k-step
-    else:  # two v_mfma_f32_32x32x16_bf16 per wave k-step (8 of 16 k-slots carry split products)
-        mfma_flops = ksteps * 2 * (2 * 32 * 32 * 16)
+    else:  # two v_mfma_f32_32x32x8_bf16 per wave k-step (every k-slot carries a split product)
+        mfma_flops = ksteps * 2 * (2 * 32 * 32 * 8)
     out["render_work_per_frame"] = {k: round(v / B, 1) for k, v in work.items()}
     out["render_mfma"] = {"issued_tflops": round(mfma_flops / (render_ms * 1e-3) / 1e12, 2) if render_ms else None,
                           "peak_tflops": F32_MFMA_PEAK_TFLOPS if a.exact_accum else BF16_MFMA_PEAK_TFLOPS,
-                          "instruction": "v_mfma_f32_32x32x2_f32" if a.exact_accum else "v_mfma_f32_32x32x16_bf16",
+                          "instruction": "v_mfma_f32_32x32x2_f32" if a.exact_accum else "v_mfma_f32_32x32x8_bf16",
                           "useful_frac": round(work["pairs_contributing"] / max(64 * work["strip_pairs_blended"], 1), 4)}
     if a.pipeline == "train":
         bms, bcnt = prof.get("render_bwd", (0.0, 0))
