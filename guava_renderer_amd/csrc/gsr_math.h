@@ -4,7 +4,7 @@
 // the library is compiled with -ffp-contract=off, so a*b+c is two roundings unless written as
 // fmaf().  The preprocess restates forward.cu:74-269 / auxiliary.h:40-176 of the reference
 // (submodules/diff-gaussian-rasterization-32) in glm's summation order; the blend uses the
-// fused form of the Gaussian exponent and gsr_expf() for a bit-reproducible exp.
+// fused form of the Gaussian exponent and blend_parts() for a bit-reproducible exp.
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -45,35 +45,37 @@ __device__ __forceinline__ float expf_exact(float x) {
     return (x != x) ? x : r_;  // NaN passes through (select, no branch)
 }
 
-// expf_exact for the blend: the same value wherever it can matter (x in [-87, 0], where alpha may
-// reach 1/255), without the clamp and the NaN select -- the render's alpha_of zeroes alpha outside
-// that range itself, and a NaN propagates through the polynomial on its own.  The power-of-two
-// scaling is v_ldexp_f32, exact like the bit construction above.
-__device__ __forceinline__ float expf_blend(float x) {
-    const float k = rintf(x * 1.44269504088896341f);
-    float r = fmaf(k, -0.693359375f, x);
-    r = fmaf(k, 2.12194440e-4f, r);
-    float p = 1.9875691500e-4f;
-    p = fmaf(p, r, 1.3981999507e-3f);
-    p = fmaf(p, r, 8.3334519073e-3f);
-    p = fmaf(p, r, 4.1665795894e-2f);
-    p = fmaf(p, r, 1.6666665459e-1f);
-    p = fmaf(p, r, 5.0000001201e-1f);
-    const float r2 = r * r;
-    p = fmaf(p, r2, r);
-    p = p + 1.0f;
-    return __builtin_amdgcn_ldexpf(p, (int)k);
+// The blend's exp, split as exp(x) = 2^k (1 + q) (the same op sequence as gsro_blend_parts in
+// oracle/gsr_oracle.c): k = rint(x log2e), r = x - k ln2 in one fma (|k| <= 8 wherever alpha can
+// reach 1/255, so the single-constant reduction is exact to 2e-8 there), q = r + r^2 P(r) with a
+// degree-4 minimax P on [-ln2/2, ln2/2] (exp within 0.97 ulp on [-5.6, 0]).  The opacity is folded
+// into the power-of-two scale, alpha = fma(o 2^k, q, o 2^k): one rounding instead of o * exp(x)'s
+// two (1.2 ulp from o exp(x) vs 1.8), and two VALU fewer per (pixel, Gaussian) pair than the
+// seven-coefficient exp followed by the opacity multiply.
+__device__ __forceinline__ void blend_parts(float x, float& q, int& k) {
+    const float kf = rintf(x * 1.44269504088896341f);
+    const float r = fmaf(kf, -0.693147182464599609375f, x);
+    float p = 1.3814539415761828e-3f;
+    p = fmaf(p, r, 8.36874544620514e-3f);
+    p = fmaf(p, r, 4.166838899254799e-2f);
+    p = fmaf(p, r, 1.666652113199234e-1f);
+    p = fmaf(p, r, 4.999999403953552e-1f);
+    q = fmaf(p, r * r, r);
+    k = (int)kf;  // v_cvt_i32_f32: NaN -> 0 (q is then NaN, so alpha is too)
+}
+// alpha before the 0.99 clamp: o exp(x) for x in [-87, 0]
+__device__ __forceinline__ float blend_oexp(float o, float q, int k) {
+    const float s = __builtin_amdgcn_ldexpf(o, k);
+    return fmaf(s, q, s);
+}
+// exp(x) itself (the backward's G)
+__device__ __forceinline__ float blend_G(float q, int k) {
+    return __builtin_amdgcn_ldexpf(q + 1.0f, k);
 }
 
 // Hardware exp2 path (v_exp_f32), used in "fast" mode.
 __device__ __forceinline__ float expf_fast(float x) {
     return __builtin_amdgcn_exp2f(x * 1.4426950408889634f);
-}
-
-template <bool EXACT>
-__device__ __forceinline__ float blend_exp(float x) {
-    if constexpr (EXACT) return expf_exact(x);
-    else return expf_fast(x);
 }
 
 // glm mat3, column-major m[col][row].

@@ -259,10 +259,20 @@ __global__ __launch_bounds__(GSR_TILE_PIX) __attribute__((amdgpu_waves_per_eu(2)
                 const float dx = ra.x - pfx, dy = ra.y - pfy;
                 // branch-free: every lane evaluates, `act` selects
                 const float power = blend_power(rc.x, rc.y, rc.z, dx, dy);
-                const float G = blend_exp<EXACT>(power);
-                const float alpha = fminf(0.99f, ra.z * G);
+                // alpha exactly as the forward's alpha_of (render_fwd.hip); power < -87 never blends
+                float G, alpha;
+                if constexpr (EXACT) {
+                    float q;
+                    int k;
+                    blend_parts(power, q, k);
+                    G = blend_G(q, k);
+                    alpha = fminf(0.99f, blend_oexp(ra.z, q, k));
+                } else {
+                    G = expf_fast(power);
+                    alpha = fminf(0.99f, ra.z * G);
+                }
                 const bool act = inside && contributor < last_contributor && !(power > 0.0f) &&
-                                 !(alpha < 1.0f / 255.0f);
+                                 !(power < -87.0f) && !(alpha < 1.0f / 255.0f);
                 const float one_m = 1.f - alpha;
                 const float rinv1m = __builtin_amdgcn_rcpf(one_m);
                 // T / (1 - alpha): reciprocal + one Newton step on the quotient (<= 1 ulp)

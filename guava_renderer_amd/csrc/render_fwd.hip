@@ -60,7 +60,15 @@ template <bool EXACT>
 __device__ __forceinline__ float alpha_of(const float4 ga, const float4 gc, float pfx, float pfy) {
     const float dx = ga.x - pfx, dy = ga.y - pfy;
     const float power = blend_power(gc.x, gc.y, gc.z, dx, dy);
-    const float alpha = fminf(0.99f, ga.z * (EXACT ? expf_blend(power) : expf_fast(power)));
+    float alpha;
+    if constexpr (EXACT) {
+        float q;
+        int k;
+        blend_parts(power, q, k);
+        alpha = fminf(0.99f, blend_oexp(ga.z, q, k));
+    } else {
+        alpha = fminf(0.99f, ga.z * expf_fast(power));
+    }
     // power < -87: exp < 2e-38, alpha < 1/255 -- never taken, as in the reference
     return (power > 0.0f || power < -87.0f) ? 0.0f : alpha;
 }

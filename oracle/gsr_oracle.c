@@ -58,7 +58,42 @@ float gsro_expf(float x) {
     return p * bitsf((uint32_t)(ki + 127) << 23);
 }
 
-static inline float blend_exp(float x, int exact) { return exact ? gsro_expf(x) : expf(x); }
+/* The blend's alpha = min(0.99, o * exp(power)) (forward.cu:361, backward.cu:529-531), with exp
+ * split as 2^k (1 + q) and the opacity folded into the power-of-two scale -- the op sequence of
+ * blend_parts / blend_oexp / blend_G in guava_renderer_amd/csrc/gsr_math.h, so the GPU's alphas are
+ * bit-identical.  k = rint(x log2e), r = x - k ln2 (one fma), q = r + r^2 P(r) with a degree-4
+ * minimax P on [-ln2/2, ln2/2]; alpha = fma(o 2^k, q, o 2^k).  Accuracy: exp within 0.97 ulp and
+ * o exp(x) within 1.2 ulp on [-5.6, 0] (alpha >= 1/255 needs x > -5.54); libm-free.
+ * power < -87 never blends (alpha 0, as exp(-87) * o < 1/255); a NaN power gives alpha 0.99. */
+static inline void blend_parts(float x, float* q, int* k) {
+    const float kf = rintf(x * 1.44269504088896341f);
+    const float r = fmaf(kf, -0.693147182464599609375f, x);
+    float p = 1.3814539415761828e-3f;
+    p = fmaf(p, r, 8.36874544620514e-3f);
+    p = fmaf(p, r, 4.166838899254799e-2f);
+    p = fmaf(p, r, 1.666652113199234e-1f);
+    p = fmaf(p, r, 4.999999403953552e-1f);
+    *q = fmaf(p, r * r, r);
+    *k = (kf == kf) ? (int)kf : 0; /* v_cvt_i32_f32 gives 0 for NaN; |kf| <= 126 otherwise */
+}
+float gsro_blend_alpha(float o, float x, int exact) {
+    if (!exact) return fminf(0.99f, o * expf(x));
+    if (x < -87.0f) return 0.0f;
+    float q;
+    int k;
+    blend_parts(x, &q, &k);
+    const float s = ldexpf(o, k);
+    return fminf(0.99f, fmaf(s, q, s));
+}
+/* exp(x) = 2^k (1 + q) for the backward's dL/dopacity and dL/dG terms */
+float gsro_blend_G(float x, int exact) {
+    if (!exact) return expf(x);
+    if (x < -87.0f) x = -87.0f; /* never used there (alpha is 0); keeps k in range */
+    float q;
+    int k;
+    blend_parts(x, &q, &k);
+    return ldexpf(q + 1.0f, k);
+}
 
 /* ---- glm-order helpers (glm mat3 is column-major: m[col][row]) ---- */
 typedef struct { float m[3][3]; } mat3;
@@ -370,7 +405,7 @@ void gsro_render(int W, int H, const uint32_t* ranges, const uint32_t* point_lis
                     const float A = -0.5f * co[0], Bb = -co[1], Cq = -0.5f * co[2];
                     const float power = fmaf(dy, fmaf(Cq, dy, Bb * dx), (A * dx) * dx);
                     if (power > 0.0f) continue;
-                    const float alpha = fminf(0.99f, co[3] * blend_exp(power, exact_exp));
+                    const float alpha = gsro_blend_alpha(co[3], power, exact_exp);
                     if (alpha < 1.0f / 255.0f) continue;
                     const float test_T = Tr * (1.0f - alpha);
                     if (test_T < 0.0001f) break; /* done: the reference stops iterating */
@@ -414,7 +449,7 @@ void gsro_render_counts(int W, int H, const uint32_t* ranges, const uint32_t* po
                     const float A = -0.5f * co[0], Bb = -co[1], Cq = -0.5f * co[2];
                     const float power = fmaf(dy, fmaf(Cq, dy, Bb * dx), (A * dx) * dx);
                     if (power > 0.0f) continue;
-                    const float alpha = fminf(0.99f, co[3] * blend_exp(power, exact_exp));
+                    const float alpha = gsro_blend_alpha(co[3], power, exact_exp);
                     if (alpha < 1.0f / 255.0f) continue;
                     const float test_T = Tr * (1.0f - alpha);
                     if (test_T < 0.0001f) break;
@@ -474,8 +509,8 @@ void gsro_render_backward(int W, int H, const uint32_t* ranges, const uint32_t* 
                     const float A = -0.5f * co[0], Bb = -co[1], Cq = -0.5f * co[2];
                     const float power = fmaf(dy, fmaf(Cq, dy, Bb * dx), (A * dx) * dx);
                     if (power > 0.0f) continue;
-                    const float G = blend_exp(power, exact_exp);
-                    const float alpha = fminf(0.99f, co[3] * G);
+                    const float G = gsro_blend_G(power, exact_exp);
+                    const float alpha = gsro_blend_alpha(co[3], power, exact_exp);
                     if (alpha < 1.0f / 255.0f) continue;
                     Tr = Tr / (1.f - alpha);
                     const float dchannel_dcolor = alpha * Tr;

@@ -47,6 +47,9 @@ extern "C" {
 
 /* Deterministic exp used by both the oracle and the HIP kernels ("exact" mode). */
 float gsro_expf(float x);
+/* the blend's alpha = min(0.99, o exp(x)) and exp(x) (gsr_oracle.c: blend_parts) */
+float gsro_blend_alpha(float o, float x, int exact);
+float gsro_blend_G(float x, int exact);
 
 /* markVisible: rasterizer_impl.cu:54-66 / auxiliary.h:151-176 (prefiltered=false). */
 void gsro_mark_visible(int P, const float* means3D, const float* view, const float* proj, uint8_t* present);
@@ -67,7 +70,7 @@ int64_t gsro_bin(int P, int W, int H, const int* radii, const float* means2D, co
                  const uint32_t* tiles_touched, uint32_t* point_offsets,
                  uint32_t* point_list, uint64_t* point_keys, uint32_t* ranges, int64_t R_cap);
 
-/* renderCUDA fwd (forward.cu:274-397).  exact_exp selects gsro_expf (1) or libm expf (0).
+/* renderCUDA fwd (forward.cu:274-397).  exact_exp selects the bit-reproducible blend exp (1, gsro_blend_alpha) or libm expf (0).
  * out_color[C*H*W], out_invdepth[H*W] (may be NULL), final_T[H*W], n_contrib[H*W]. */
 void gsro_render(int W, int H, const uint32_t* ranges, const uint32_t* point_list,
                  const float* means2D, const float* colors, const float* conic_opacity,

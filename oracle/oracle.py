@@ -40,6 +40,10 @@ def lib():
         L = ctypes.CDLL(_LIB_PATH)
         L.gsro_expf.restype = ctypes.c_float
         L.gsro_expf.argtypes = [ctypes.c_float]
+        L.gsro_blend_alpha.restype = ctypes.c_float
+        L.gsro_blend_alpha.argtypes = [ctypes.c_float, ctypes.c_float, ctypes.c_int]
+        L.gsro_blend_G.restype = ctypes.c_float
+        L.gsro_blend_G.argtypes = [ctypes.c_float, ctypes.c_int]
         L.gsro_mark_visible.argtypes = [ctypes.c_int, _f, _f, _f, _u8]
         L.gsro_preprocess.restype = ctypes.c_int
         L.gsro_preprocess.argtypes = [ctypes.c_int, _f, _f, ctypes.c_float, _f, _f, _f, _f, _f,
@@ -85,6 +89,17 @@ def get_threads():
 def expf(x):
     x = np.asarray(x, dtype=np.float32).ravel()
     return np.array([lib().gsro_expf(float(v)) for v in x], dtype=np.float32)
+
+
+def blend_alpha(o, x):
+    """min(0.99, o exp(x)) as the blend evaluates it (exact mode)."""
+    x = np.asarray(x, dtype=np.float32).ravel()
+    return np.array([lib().gsro_blend_alpha(float(o), float(v), 1) for v in x], dtype=np.float32)
+
+
+def blend_G(x):
+    x = np.asarray(x, dtype=np.float32).ravel()
+    return np.array([lib().gsro_blend_G(float(v), 1) for v in x], dtype=np.float32)
 
 
 def grid_dims(W, H):

@@ -32,6 +32,23 @@ def test_expf_accuracy():
     assert np.isnan(oracle.expf([np.nan])[0])
 
 
+def test_blend_exp_accuracy():
+    """The blend's exp (2^k (1 + q), gsr_oracle.c blend_parts) and alpha = fma(o 2^k, q, o 2^k):
+    within 1 ulp / 1.3 ulp of float64 o exp(x) wherever alpha can reach 1/255 (x > -5.54)."""
+    x = np.linspace(-5.6, 0.0, 40001).astype(np.float32)
+    ref = np.exp(x.astype(np.float64))
+    ulp = np.spacing(ref.astype(np.float32)).astype(np.float64)
+    assert (np.abs(oracle.blend_G(x) - ref) / ulp).max() <= 1.0
+    for o in (1.0, 0.37, 0.99, 0.013):
+        o32 = float(np.float32(o))
+        ref_a = np.minimum(0.99, o32 * ref)
+        ulp_a = np.spacing(ref_a.astype(np.float32)).astype(np.float64)
+        assert (np.abs(oracle.blend_alpha(o32, x) - ref_a) / ulp_a).max() <= 1.3
+    assert oracle.blend_alpha(0.5, [-90.0])[0] == 0.0           # never blends
+    assert oracle.blend_alpha(0.5, [np.nan])[0] == np.float32(0.99)  # as min(0.99, NaN) in the reference
+    assert oracle.blend_alpha(0.5, [0.0])[0] == 0.5
+
+
 def _single(o=0.5, W=64, H=64, scale=0.02, off=(0.0, 0.0, 0.0), feat=None):
     from guava_renderer_amd import camera
     cam = camera.camera(W, H)

@@ -9,7 +9,7 @@ mkdir -p $O
 V=${VARIANTS:-a b}
 for v in $V; do
   [ "$v" = a ] && continue
-  e=ENV_$v; env ${!e:-} GSR_LIB=$PWD/guava_renderer_amd/lib/ab/libgsr_$v.so timeout -k 10 300 python -u -m pytest tests/test_gpu_forward.py tests/test_gpu_fullsize.py -x -q --timeout 120 --timeout-method thread > $O/pytest_$v.log 2>&1; rc=$?; echo "pytest($v) rc=$rc"; tail -1 $O/pytest_$v.log
+  e=ENV_$v; env ${!e:-} GSR_LIB=$PWD/guava_renderer_amd/lib/ab/libgsr_$v.so timeout -k 10 600 python -u -m pytest ${ABL_TESTS:-tests/test_gpu_forward.py tests/test_gpu_fullsize.py} -x -q --timeout 120 --timeout-method thread > $O/pytest_$v.log 2>&1; rc=$?; echo "pytest($v) rc=$rc"; tail -1 $O/pytest_$v.log
   [ $rc -eq 0 ] || exit $rc
 done
 for r in 1 2 3; do for v in $V; do
