@@ -314,15 +314,21 @@ def main():
     step_count = [0]
 
     gather = dist is not None and a.pipeline != "train"
+    # consumer boundary: every rank receives all ranks' RGB frames (RCCL all-gather over xGMI),
+    # each batch's exchange overlapped with the next batch's rendering on a side stream
+    gatherer = None
+    if gather:
+        gdev = dev if backend == "nccl" else torch.device("cpu")
+        gatherer = parallel.FrameGather(B, (3, H, W), torch.float32, gdev)
 
     def step():
         i = step_count[0] % n_inflight
         step_count[0] += 1
         with torch.cuda.stream(streams[i]):
             res = step_on(i)
-            if gather:  # consumer boundary: every rank receives all ranks' RGB frames (RCCL all-gather)
+            if gatherer is not None:
                 rgb = res[0][:, :3]
-                parallel.gather_frames(rgb if backend == "nccl" else rgb.cpu(), B * world)
+                gatherer.push(rgb if backend == "nccl" else rgb.cpu())
             return res
 
     for _ in range(a.warmup):
@@ -350,6 +356,8 @@ def main():
     t0 = time.perf_counter()
     for _ in range(a.steps):
         step()
+    if gatherer is not None:
+        gatherer.wait()
     torch.cuda.synchronize(dev)
     el = time.perf_counter() - t0
     if dist is not None:
@@ -448,7 +456,7 @@ def main():
                                 "frame": "deformed frames -> GaussianRasterizer_32 once per frame (gaussian_render.py:37-67)"
                                 }[a.pipeline] + (" + fused refiner conv_body_first" if a.refine else ""), "gaussians": P, "image": [W, H], "channels": C,
                    "frames_per_step_per_gpu": B, "global_batch": B * world,
-                   "parallelism": f"frame-sharded x{world}" + (", RGB all-gather per step" if world > 1 and a.pipeline != "train" else ""),
+                   "parallelism": f"frame-sharded x{world}" + (", RGB all-gather per step (overlapped with the next step)" if world > 1 and a.pipeline != "train" else ""),
                    "batches_in_flight": n_inflight,
                    "exp": "hw" if a.fast_exp else "exact-poly",
                    "colour_accum": "f32 mfma (bit-exact)" if a.exact_accum else "split-bf16 mfma (<=1e-4)",

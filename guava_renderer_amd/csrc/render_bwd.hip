@@ -55,7 +55,8 @@ __device__ __forceinline__ float add_halves(float x) {
 }
 
 // ABL (timing ablations only, wrong gradients): 1 = no atomics, 2 = no serial replay, 3 = no
-// flush (colour MFMA, moments, atomics), 4 = no list walk beyond the ring fill (batches empty)
+// flush (colour MFMA, moments, atomics), 4 = no list walk beyond the ring fill (batches empty),
+// 5 / 6 = VALU stand-ins for the g / the colour contraction's MFMAs
 template <bool EXACT, bool INVD, int ABL = 0>
 __global__ __launch_bounds__(GSR_TILE_PIX) __attribute__((amdgpu_waves_per_eu(2))) void k_render_bwd(
     Dims d, Inputs in, GeomArena g, ImageArena im, BinArena bn, Grads gr) {
@@ -235,8 +236,13 @@ __global__ __launch_bounds__(GSR_TILE_PIX) __attribute__((amdgpu_waves_per_eu(2)
             for (int r = 0; r < 16; r++) { gd0[r] = 0.f; gd1[r] = 0.f; }
 #pragma unroll
             for (int k = 0; k < 16; k++) {
-                gd0 = __builtin_amdgcn_mfma_f32_32x32x2f32(fr[k], bh0[k], gd0, 0, 0, 0);
-                gd1 = __builtin_amdgcn_mfma_f32_32x32x2f32(fr[k], bh1[k], gd1, 0, 0, 0);
+                if (ABL == 5) {  /* timing ablation: VALU stand-in for the g contraction */
+                    gd0[k] = fmaf(fr[k], bh0[k], gd0[k]);
+                    gd1[k] = fmaf(fr[k], bh1[k], gd1[k]);
+                } else {
+                    gd0 = __builtin_amdgcn_mfma_f32_32x32x2f32(fr[k], bh0[k], gd0, 0, 0, 0);
+                    gd1 = __builtin_amdgcn_mfma_f32_32x32x2f32(fr[k], bh1[k], gd1, 0, 0, 0);
+                }
             }
             // to pixel lanes: gd0[r] = g of slot (r&3) + 8(r>>2), gd1[r] = of slot (r&3) + 8(r>>2) + 4
 #pragma unroll
@@ -314,7 +320,8 @@ __global__ __launch_bounds__(GSR_TILE_PIX) __attribute__((amdgpu_waves_per_eu(2)
 #pragma unroll
             for (int j = 0; j < kBwdBatch; j++) {
                 const float w = wl[l32 * kBwdPitch + 2 * j + hi];
-                acc = __builtin_amdgcn_mfma_f32_32x32x2f32(w, adl[j], acc, 0, 0, 0);
+                if (ABL == 6) acc[j & 15] = fmaf(w, adl[j], acc[j & 15]);  /* timing ablation */
+                else acc = __builtin_amdgcn_mfma_f32_32x32x2f32(w, adl[j], acc, 0, 0, 0);
             }
             // pixel moments of u for slot l&31 over this lane half's 32 pixels (strip rows 4h..4h+3):
             // lx = (i % 8) - 3.5, ly = (i / 8) - 3.5 + 4h
@@ -423,10 +430,12 @@ void launch_render_bwd(const Dims& d, const Inputs& in, const GeomArena& g, cons
     const bool invd = gr.invd != 0;
     const dim3 grid(min((nwaves + 3) / 4, persistent_grid(2))), blk(GSR_TILE_PIX);
     static const int ablate = [] { const char* e = getenv("GSR_BWD_ABLATE"); return e ? atoi(e) : 0; }();
-    if (ablate >= 1 && ablate <= 3 && exact && invd) {
+    if (ablate >= 1 && ablate <= 6 && exact && invd) {
         if (ablate == 1) hipLaunchKernelGGL((k_render_bwd<true, true, 1>), grid, blk, 0, s, d, in, g, im, b, gr);
         if (ablate == 2) hipLaunchKernelGGL((k_render_bwd<true, true, 2>), grid, blk, 0, s, d, in, g, im, b, gr);
         if (ablate == 3) hipLaunchKernelGGL((k_render_bwd<true, true, 3>), grid, blk, 0, s, d, in, g, im, b, gr);
+        if (ablate == 5) hipLaunchKernelGGL((k_render_bwd<true, true, 5>), grid, blk, 0, s, d, in, g, im, b, gr);
+        if (ablate == 6) hipLaunchKernelGGL((k_render_bwd<true, true, 6>), grid, blk, 0, s, d, in, g, im, b, gr);
         return;
     }
     if (exact) {

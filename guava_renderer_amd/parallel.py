@@ -4,7 +4,9 @@ Frames (camera views / poses of an avatar) are independent units of the rasteriz
 renders its own contiguous slice of the frame list with no collective on the data path
 (bench.py reports "scaling": "weak").  The only exchange is at the consumer boundary:
 `gather_frames` assembles the full [N, ...] batch on every rank (all_gather over RCCL on
-GPUs, gloo in the CPU tests), and `reduce_shared_grads` sums per-frame gradients of a
+GPUs, gloo in the CPU tests), `FrameGather` does the same for a stream of equal batches without
+copies and overlapped with the next batch's rendering, and `reduce_shared_grads` sums per-frame
+gradients of a
 shared avatar (the DP gradient all-reduce a trainer would do; one flat bucket, since xGMI
 rings are per-link bound and favour few large messages).
 """
@@ -42,6 +44,56 @@ def gather_frames(local, n_frames, group=None):
     dist.all_gather_into_tensor(out, pad, group=group)
     parts = [out[r * cap: r * cap + (hi - lo)] for r, (lo, hi) in enumerate(counts)]
     return torch.cat(parts, 0)
+
+
+class FrameGather:
+    """Overlapped all-gather of a stream of equal per-rank batches [n_local, *shape] into
+    [world * n_local, *shape] on every rank (frame order = rank order, as shard_range's contiguous
+    slices).  `push(frames)` copies the rank's frames into a staging buffer on the current stream
+    and starts the collective on a side stream once they are written, so batch i's exchange runs
+    under batch i+1's rendering; `n_buffers` batches may be in flight (a push waits for the
+    exchange that last used its buffer).  `wait()` orders the current stream after every exchange
+    pushed so far and returns the latest gathered batch.  One collective per batch, no padding and
+    no concatenation (RCCL rings over xGMI are per-link bound: one large message per batch)."""
+
+    def __init__(self, n_local, shape, dtype, device, group=None, n_buffers=2):
+        self.group = group
+        self.world = dist.get_world_size(group)
+        self.stream = torch.cuda.Stream(device) if device.type == "cuda" else None
+        self.bufs = [(torch.empty((n_local,) + tuple(shape), dtype=dtype, device=device),
+                      torch.empty((self.world * n_local,) + tuple(shape), dtype=dtype, device=device))
+                     for _ in range(n_buffers)]
+        self.done = [None] * n_buffers
+        self.k = 0
+        self.last = None
+
+    def push(self, frames):
+        j = self.k % len(self.bufs)
+        self.k += 1
+        src, dst = self.bufs[j]
+        if self.stream is None:  # CPU (gloo): synchronous
+            src.copy_(frames)
+            dist.all_gather_into_tensor(dst, src, group=self.group)
+            self.last = dst
+            return
+        cur = torch.cuda.current_stream(src.device)
+        if self.done[j] is not None:
+            cur.wait_event(self.done[j])  # the exchange that last read src / wrote dst
+        src.copy_(frames)
+        ready = torch.cuda.Event()
+        ready.record(cur)
+        with torch.cuda.stream(self.stream):
+            self.stream.wait_event(ready)
+            dist.all_gather_into_tensor(dst, src, group=self.group)
+            ev = torch.cuda.Event()
+            ev.record(self.stream)
+        self.done[j] = ev
+        self.last = dst
+
+    def wait(self):
+        if self.stream is not None:
+            torch.cuda.current_stream(self.bufs[0][0].device).wait_stream(self.stream)
+        return self.last
 
 
 def reduce_shared_grads(grads, group=None):

@@ -54,7 +54,16 @@ def _worker(rank, world, port, n_frames, q):
         parallel.reduce_shared_grads(g)
         ok_reduce = (torch.all(g["colors"] == sum(r + 1 for r in range(world))).item()
                      and torch.all(g["opacity"] == sum(2.0 * r for r in range(world))).item())
-        q.put((rank, ok_gather, ok_reduce))
+        ok_stream = True
+        if n_frames % world == 0:  # FrameGather (bench.py's overlapped exchange): equal shards
+            fg = parallel.FrameGather(len(frames), (32, 4, 4), torch.float32, torch.device("cpu"))
+            for step in range(3):  # successive batches through the two staging buffers
+                ids = [step * n_frames + f for f in frames]
+                fg.push(_fake_render(ids))
+                got = fg.wait()
+                want = _fake_render([step * n_frames + f for f in range(n_frames)])
+                ok_stream = ok_stream and torch.equal(got, want)
+        q.put((rank, ok_gather, ok_reduce and ok_stream))
     finally:
         dist.destroy_process_group()
 

@@ -71,3 +71,48 @@ def test_two_ranks_real_rasterizer_gather():
     ref = _render(list(range(N_FRAMES))).cpu().numpy()
     assert gathered.shape == ref.shape
     np.testing.assert_array_equal(gathered, ref)
+
+
+def _nccl_worker(port, q):
+    """World-1 RCCL group on the one GPU: FrameGather's device path (side stream, events, staging
+    buffers reused every other batch) on real renders, each gathered batch checked after the
+    next batch was pushed (so the overlap is exercised)."""
+    import torch.distributed as dist
+    from guava_renderer_amd import parallel
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dev = torch.device("cuda:0")
+    torch.cuda.set_device(dev)
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=dev)
+    try:
+        batches = [[0, 1], [2, 3], [4, 0], [1, 2]]
+        refs = [_render(b)[:, :3].clone() for b in batches]
+        fg = parallel.FrameGather(2, (3, W, W), torch.float32, dev)
+        ok = True
+        prev = None
+        for b, ref in zip(batches, refs):
+            fg.push(_render(b)[:, :3])
+            if prev is not None:  # the previous batch's buffer, read while this one is in flight
+                pb, pref = prev
+                torch.cuda.current_stream(dev).wait_stream(fg.stream)
+                ok = ok and torch.equal(fg.bufs[pb][1], pref)
+            prev = ((fg.k - 1) % len(fg.bufs), ref)
+        last = fg.wait()
+        ok = ok and torch.equal(last, refs[-1])
+        q.put(bool(ok))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_frame_gather_device_path_rccl_world1():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    p = ctx.Process(target=_nccl_worker, args=(port, q))
+    p.start()
+    ok = q.get(timeout=240)
+    p.join(timeout=120)
+    assert p.exitcode == 0
+    assert ok
