@@ -417,13 +417,14 @@ def main():
     frames_per_launch = 1 if a.pipeline == "frame" else B
     bytes_launch = _render_alg_bytes(P_vis / B, W, H) * frames_per_launch
     achieved = bytes_launch / (render_ms * 1e-3) / 1e9 if render_ms > 0 else None
-    traffic = None
+    traffic = issue = None
     pmc_path = os.path.join(ROOT, "profiles", "pmc_render_fwd.json")
     if os.path.exists(pmc_path):
         try:
             pm = json.load(open(pmc_path))
             if pm.get("config") == workload and pm.get("batch") == B:
                 traffic = pm.get("hbm_bytes_per_launch")
+                issue = pm.get("render_fwd_issue")
         except Exception:  # noqa: BLE001
             traffic = None
 
@@ -483,6 +484,12 @@ def main():
                           "peak_tflops": F32_MFMA_PEAK_TFLOPS if a.exact_accum else BF16_MFMA_PEAK_TFLOPS,
                           "instruction": "v_mfma_f32_32x32x2_f32" if a.exact_accum else "v_mfma_f32_32x32x8_bf16",
                           "useful_frac": round(work["pairs_contributing"] / max(64 * work["strip_pairs_blended"], 1), 4)}
+    if issue is not None and not a.exact_accum:
+        # the compute wall beside the HBM one: per-launch instruction counts and per-SIMD pipe busy
+        # of the contract kernel, from the committed PMC passes (profiles/pmc_render_fwd.json)
+        out["render_issue"] = dict(issue, source="profiles/pmc_render_fwd.json (tools/gpu_pmc_fwd.sh)",
+                                   valu_per_kstep=round(issue["valu_insts"] / max(ksteps, 1), 1)
+                                   if issue.get("valu_insts") else None)
     if a.pipeline == "train":
         bms, bcnt = prof.get("render_bwd", (0.0, 0))
         bwd_ms = bms / max(bcnt, 1)

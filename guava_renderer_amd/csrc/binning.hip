@@ -619,7 +619,7 @@ void launch_tile_scan(const Dims& d, const GeomArena& g, const ImageArena& im, h
 // of the conic's quadratic form Q = a dx^2 + 2b dx dy + c dy^2 (power = -Q/2 in the blend).  Q is
 // convex (a, c > 0, ac > b^2), so the minimum is 0 if the mean lies inside, else it lies on an edge:
 // each edge is a 1-D quadratic minimised by clamping its vertex.
-__device__ __forceinline__ float rect_qmin(float a, float b, float c, float ia, float ic, float dxl, float dxh,
+__host__ __device__ __forceinline__ float rect_qmin(float a, float b, float c, float ia, float ic, float dxl, float dxh,
                                            float dyl, float dyh) {
     if (dxl <= 0.f && dxh >= 0.f && dyl <= 0.f && dyh >= 0.f) return 0.f;
     float q = 3.0e38f;
@@ -639,12 +639,12 @@ __device__ __forceinline__ float rect_qmin(float a, float b, float c, float ia, 
 // Per-Gaussian part of the strip test, computed once per Gaussian (not once per instance):
 // (K = 2 ln(255 o), 1/a, 1/c, mode) with mode 0 = test the strips, 1 = no strip (o < 1/255:
 // alpha <= o < 1/255 at every pixel), 2 = every strip (non-finite or non-positive-definite conic).
-__device__ __forceinline__ float4 strip_pre(float4 co) {
+__host__ __device__ __forceinline__ float4 strip_pre(float4 co) {
     const float a = co.x, b = co.y, c = co.z, o = co.w;
-    if (o < 1.0f / 255.0f) return make_float4(0.f, 0.f, 0.f, __uint_as_float(1u));
+    if (o < 1.0f / 255.0f) return make_float4(0.f, 0.f, 0.f, __builtin_bit_cast(float, 1u));
     if (!(a > 0.f) || !(c > 0.f) || !(a * c - b * b > 0.f) || !(o <= 3.0e38f))
-        return make_float4(0.f, 0.f, 0.f, __uint_as_float(2u));
-    return make_float4(2.0f * logf(255.0f * o), 1.0f / a, 1.0f / c, __uint_as_float(0u));
+        return make_float4(0.f, 0.f, 0.f, __builtin_bit_cast(float, 2u));
+    return make_float4(2.0f * logf(255.0f * o), 1.0f / a, 1.0f / c, __builtin_bit_cast(float, 0u));
 }
 
 // Strip mask of one (Gaussian, tile) instance: bit s is set unless no pixel centre of the tile's
@@ -652,9 +652,11 @@ __device__ __forceinline__ float4 strip_pre(float4 co) {
 // on the whole strip.  A cleared bit only ever removes pairs the blend skips anyway (alpha < 1/255,
 // forward.cu:362-363), so culling with it is decision-preserving; the slack (1e-4 of the form's
 // term magnitudes + 1e-3 relative) covers float rounding of both this test and the blend's power.
-// Non-finite or non-positive-definite conics keep every strip.
-__device__ __forceinline__ uint32_t strip_mask(float4 co, float4 pre, float2 m, int tx, int ty) {
-    const uint32_t mode = __float_as_uint(pre.w);
+// Non-finite or non-positive-definite conics keep every strip.  Host-callable for
+// tools/strip_mask_check.cpp (brute force over the strip's 64 pixels: no strip with a pixel at
+// Q <= K is ever cleared; 0.4% more strips kept than needed on random conics).
+__host__ __device__ __forceinline__ uint32_t strip_mask(float4 co, float4 pre, float2 m, int tx, int ty) {
+    const uint32_t mode = __builtin_bit_cast(uint32_t, pre.w);
     if (mode == 1u) return 0u;
     if (mode == 2u) return (1u << kStrips) - 1u;
     const float a = co.x, b = co.y, c = co.z;

@@ -98,6 +98,14 @@ def main():
                                  "issue-stalled": round(sq.get("SQ_WAIT_INST_ANY", 0) / wc, 3),
                                  "issuing": round(sq.get("SQ_ACTIVE_INST_ANY", 0) / wc, 3),
                                  "valu issuing": round(sq.get("SQ_ACTIVE_INST_VALU", 0) / wc, 3)}}
+        if sq.get("GRBM_GUI_ACTIVE"):
+            # per-SIMD pipe busy: ACTIVE_INST_* are quad-cycles summed over waves; GRBM_GUI_ACTIVE
+            # sums the 8 XCDs' cycles; 256 CUs x 4 SIMDs
+            kc = sq["GRBM_GUI_ACTIVE"] / 8.0
+            res["render_fwd_issue"]["simd_busy_frac"] = {
+                "valu": round(4.0 * sq.get("SQ_ACTIVE_INST_VALU", 0) / (1024 * kc), 3),
+                "salu": round(4.0 * sq.get("SQ_ACTIVE_INST_SCA", 0) / (1024 * kc), 3),
+                "lds": round(4.0 * sq.get("SQ_ACTIVE_INST_LDS", 0) / (1024 * kc), 3)}
     json.dump(res, open(out, "w"), indent=1)
     print(json.dumps(res, indent=1))
 
