@@ -190,6 +190,33 @@ __device__ __forceinline__ void store_strip(const Dims& d, const ImageArena& im,
     }
 }
 
+// Epilogue of one half-strip wave (HALF): its 32 pixels start at (hx0, hy0) (kStripW wide); acc[r]
+// at lane l holds channel (r&3)+8*(r>>2)+4*(l>>5) of pixel l&31, whose state (T, ...) lane l holds.
+__device__ __forceinline__ void store_half(const Dims& d, const ImageArena& im, const Outputs& o, const float* bg,
+                                           int b, int hx0, int hy0, int lane, const floatx16& acc, float T,
+                                           float invd, uint32_t last) {
+    const int64_t HW = (int64_t)d.H * d.W;
+    const int j = lane & 31;
+    const int qx = hx0 + j % kStripW, qy = hy0 + j / kStripW;
+    const bool in_img = qx < d.W && qy < d.H;
+    if (in_img && lane < 32) {
+        const int64_t pix = b * HW + (int64_t)qy * d.W + qx;
+        im.final_T[pix] = T;
+        im.n_contrib[pix] = last;
+        if (o.out_invdepth) o.out_invdepth[pix] = invd;
+    }
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+        o.out_color + (int64_t)b * GSR_C * HW, 0, (int)((int64_t)GSR_C * HW * 4), 0x00020000);
+    const int hi = lane >> 5;
+    const int v = in_img ? (hi * 4 * (int)HW + qy * d.W + qx) * 4 : 0x7FFFFFF0;
+#pragma unroll
+    for (int r = 0; r < 16; r++) {
+        const int c = (r & 3) + 8 * (r >> 2);  // + 4 in the upper half-wave (in v)
+        const float bgc = hi ? bg[c + 4] : bg[c];
+        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(fmaf(T, bgc, acc[r])), rs, v, c * (int)HW * 4, 0);
+    }
+}
+
 // gsr_refine_prepare: rows [f_0..f_{keep-1}, W.f (n_out values), 0...] of 32 floats.
 __global__ __launch_bounds__(256) void k_refine_prepare(int n, const float* __restrict__ in,
                                                         const float* __restrict__ w, int n_out,
@@ -247,7 +274,8 @@ __device__ __forceinline__ void overflow_fill(const Dims& d, const Outputs& o) {
 // in three rotating register slots: the records and feature operand of step s+3 are loaded while
 // step s+1's alphas (the exp-heavy, transmittance-independent part) are computed and step s's
 // serial blend and MFMA accumulation run.
-template <bool EXACT, bool STATS, bool TL, bool REFINE, int ABL = 0, int SPLIT = 0, int NSLOT = 3>
+template <bool EXACT, bool STATS, bool TL, bool REFINE, int ABL = 0, int SPLIT = 0, int NSLOT = 3,
+          bool HALF = false>
 __device__ __forceinline__ void render_fwd_body(const Dims& d, const Inputs& in, const GeomArena& g,
                                                 const ImageArena& im, const BinArena& bn,
                                                 const Outputs& o) {
@@ -255,8 +283,10 @@ __device__ __forceinline__ void render_fwd_body(const Dims& d, const Inputs& in,
         overflow_fill(d, o);
         return;
     }
+    static_assert(!HALF || (!STATS && !TL && !REFINE && ABL == 0), "half-strip waves: production kernel only");
     const uint32_t ne = g.ctrl[kCtrlNonEmpty];
-    const uint32_t nstrip = (uint32_t)kStrips * ne;
+    // HALF: every strip is two work items (one wave per 32-pixel half, the strip's rows 0-3 / 4-7)
+    const uint32_t nstrip = (HALF ? 2u : 1u) * (uint32_t)kStrips * ne;
     const uint32_t nitems = nstrip + (uint32_t)(d.B * d.T) - ne;
     const int lane = threadIdx.x & 63;
     const int hi = lane >> 5;
@@ -270,7 +300,8 @@ __device__ __forceinline__ void render_fwd_body(const Dims& d, const Inputs& in,
             uint32_t k = 0;
             if (lane == 0) k = atomicAdd(&g.ctrl[kCtrlXcdQueue + kCtrlXcdStride * q], 1u);
             k = __builtin_amdgcn_readfirstlane(k);
-            item = queue_item(q, k, ne, nitems - nstrip, in.xcd_map);
+            item = HALF ? queue_item_half(q, k, ne, nitems - nstrip, in.xcd_map)
+                        : queue_item(q, k, ne, nitems - nstrip, in.xcd_map);
             if (item != 0xFFFFFFFFu) break;
             q = (q + 1) & 7u;
             q_left--;
@@ -290,10 +321,11 @@ __device__ __forceinline__ void render_fwd_body(const Dims& d, const Inputs& in,
             continue;
         }
         // the longest strips bound the kernel's latency: give them issue priority on their SIMD
-        if (item < in.prio_items) __builtin_amdgcn_s_setprio(3);
+        if ((HALF ? item >> 1 : item) < in.prio_items) __builtin_amdgcn_s_setprio(3);
         else __builtin_amdgcn_s_setprio(0);
         const uint64_t t_start = TL ? __builtin_amdgcn_s_memrealtime() : 0;
-        const uint32_t code = im.strip_list[item];
+        const uint32_t code = im.strip_list[HALF ? item >> 1 : item];
+        const int half = HALF ? (int)(item & 1u) : 0;
         const int tile_g = (int)(code >> 2);
         const int strip = (int)(code & 3u);
         const int b = tile_g / d.T;
@@ -301,8 +333,11 @@ __device__ __forceinline__ void render_fwd_body(const Dims& d, const Inputs& in,
         const int tx = t % d.gx, ty = t / d.gx;
         int sx0, sy0;
         strip_origin(tx, ty, strip, sx0, sy0);
-        const int px = sx0 + lane % kStripW;
-        const int py = sy0 + lane / kStripW;
+        // this lane's pixel of the strip: HALF: pixel 32 half + (lane & 31), in both lane halves
+        // (lanes l and l + 32 carry the same pixel's state; their alphas are Gaussians a and b)
+        const int lpix = HALF ? 32 * half + (lane & 31) : lane;
+        const int px = sx0 + lpix % kStripW;
+        const int py = sy0 + lpix / kStripW;
         const float pfx = (float)px, pfy = (float)py;
         bool done = !(px < d.W && py < d.H);
         float T = 1.0f, invd = 0.f;
@@ -408,25 +443,54 @@ __device__ __forceinline__ void render_fwd_body(const Dims& d, const Inputs& in,
         // stage 2: the pixel-local alphas of slot S (a missing survivor has alpha 0)
 #define GSR_ALPHA(S)                                                                                \
         {                                                                                           \
-            if (GSR_REC_PATH == 3) {  /* through this wave's LDS slot: uniform-address b128 reads */ \
-                rec_lds[rec_widx] = S##r; rec_lds[rec_widx + 8] = S##r2;  /* lanes 8..63: spare */ \
+            if (HALF) {  /* each lane its own Gaussian's record: a in lanes 0-31, b in 32-63 */     \
+                rec_lds[rec_widx] = S##r; rec_lds[rec_widx + 8] = S##r2;                            \
                 __builtin_amdgcn_wave_barrier();                                                    \
-                S##a0 = __builtin_bit_cast(float4, *(const uint4x*)&rec_lds[0]);                    \
-                S##a1 = __builtin_bit_cast(float4, *(const uint4x*)&rec_lds[4]);                    \
-                S##b0 = __builtin_bit_cast(float4, *(const uint4x*)&rec_lds[8]);                    \
-                S##b1 = __builtin_bit_cast(float4, *(const uint4x*)&rec_lds[12]);                   \
+                S##a0 = __builtin_bit_cast(float4, *(const uint4x*)&rec_lds[8 * hi]);               \
+                S##a1 = __builtin_bit_cast(float4, *(const uint4x*)&rec_lds[8 * hi + 4]);           \
                 __builtin_amdgcn_wave_barrier();                                                    \
+                S##al = alpha_of<EXACT>(S##a0, S##a1, pfx, pfy);                                    \
+                S##ai = S##a0.w;                                                                    \
+            } else {                                                                                \
+                if (GSR_REC_PATH == 3) {  /* through this wave's LDS slot: uniform-address b128 reads */ \
+                    rec_lds[rec_widx] = S##r; rec_lds[rec_widx + 8] = S##r2;  /* lanes 8..63: spare */ \
+                    __builtin_amdgcn_wave_barrier();                                                \
+                    S##a0 = __builtin_bit_cast(float4, *(const uint4x*)&rec_lds[0]);                \
+                    S##a1 = __builtin_bit_cast(float4, *(const uint4x*)&rec_lds[4]);                \
+                    S##b0 = __builtin_bit_cast(float4, *(const uint4x*)&rec_lds[8]);                \
+                    S##b1 = __builtin_bit_cast(float4, *(const uint4x*)&rec_lds[12]);               \
+                    __builtin_amdgcn_wave_barrier();                                                \
+                }                                                                                   \
+                S##al = alpha_of<EXACT>(S##a0, S##a1, pfx, pfy);                                    \
+                S##bl = alpha_of<EXACT>(S##b0, S##b1, pfx, pfy);                                    \
+                S##ai = S##a0.w;                                                                    \
+                S##bi = S##b0.w;                                                                    \
             }                                                                                       \
-            S##al = alpha_of<EXACT>(S##a0, S##a1, pfx, pfy);                                        \
-            S##bl = alpha_of<EXACT>(S##b0, S##b1, pfx, pfy);                                        \
-            S##ai = S##a0.w;                                                                        \
-            S##bi = S##b0.w;                                                                        \
             S##f = __uint_as_float(S##fa | S##fb);                                                  \
             if (SPLIT) S##fp = SPLIT == 2 ? __float_as_uint(S##f) : split_hl(S##f);                 \
         }
         // stage 3: the serial blend of slot S and its accumulation on the matrix cores
 #define GSR_TAKE(S)                                                                                 \
-        {                                                                                           \
+        if (HALF) {  /* both alphas to every lane (one swap each), the pixel's blend duplicated */ \
+            const auto sal_ = __builtin_amdgcn_permlane32_swap(__float_as_uint(S##al),              \
+                                                               __float_as_uint(S##al), false, false); \
+            const auto sai_ = __builtin_amdgcn_permlane32_swap(__float_as_uint(S##ai),              \
+                                                               __float_as_uint(S##ai), false, false); \
+            const float wa_ = take_step(__uint_as_float(sal_[0]), __uint_as_float(sai_[0]),         \
+                                        (uint32_t)S##pa, T, invd, last, done);                      \
+            const float wb_ = take_step(__uint_as_float(sal_[1]), __uint_as_float(sai_[1]),         \
+                                        (uint32_t)S##pb, T, invd, last, done);                      \
+            const float w_ = hi ? wb_ : wa_;  /* k 0..3: Gaussian a (lanes 0-31), 4..7: b */        \
+            if (SPLIT) {                                                                            \
+                unsigned h_, l_;                                                                    \
+                split_hh_ll(w_, h_, l_);                                                            \
+                const uint2x a2_ = {S##fp, S##fp}, b2_ = {h_, l_};                                  \
+                acc0 = __builtin_amdgcn_mfma_f32_32x32x8bf16_1k(__builtin_bit_cast(shortx4, a2_),   \
+                                                               __builtin_bit_cast(shortx4, b2_), acc0, 0, 0, 0); \
+            } else {                                                                                \
+                acc0 = __builtin_amdgcn_mfma_f32_32x32x2f32(S##f, w_, acc0, 0, 0, 0);               \
+            }                                                                                       \
+        } else {                                                                                    \
             const float f_ = S##f;                                                                  \
             const bool was_done_ = done;                                                            \
             const float wa_ = take_step(S##al, S##ai, (uint32_t)S##pa, T, invd, last, done);        \
@@ -561,15 +625,17 @@ __device__ __forceinline__ void render_fwd_body(const Dims& d, const Inputs& in,
             rec[2] = (uint32_t)n_steps;
             rec[3] = __builtin_amdgcn_s_getreg((3 << 11) | 20) & 7u;
         }
-        store_strip<false, REFINE>(d, im, o, in.bg + in.s_bg * b, b, sx0, sy0, lane, acc0, acc1, T,
-                           invd, last);
+        if constexpr (HALF) store_half(d, im, o, in.bg + in.s_bg * b, b, sx0, sy0 + half * (32 / kStripW), lane,
+                                       acc0, T, invd, last);
+        else store_strip<false, REFINE>(d, im, o, in.bg + in.s_bg * b, b, sx0, sy0, lane, acc0, acc1, T,
+                                        invd, last);
     }
 }
 
-template <bool EXACT, bool STATS, bool TL, int SPLIT = 0, int NSLOT = GSR_BATCH_NSLOT>
+template <bool EXACT, bool STATS, bool TL, int SPLIT = 0, int NSLOT = GSR_BATCH_NSLOT, bool HALF = false>
 __global__ __launch_bounds__(GSR_TILE_PIX) void k_render_fwd(Dims d, Inputs in, GeomArena g,
                                                              ImageArena im, BinArena bn, Outputs o) {
-    render_fwd_body<EXACT, STATS, TL, false, 0, SPLIT, NSLOT>(d, in, g, im, bn, o);
+    render_fwd_body<EXACT, STATS, TL, false, 0, SPLIT, NSLOT, HALF>(d, in, g, im, bn, o);
 }
 
 // Timing ablations of the production kernel (GSR_RENDER_ABLATE=1: VALU stand-in for the MFMAs,
@@ -597,9 +663,12 @@ void launch_render_fwd(const Dims& d, const Inputs& in, const GeomArena& g, cons
     if (nwaves == 0) return;
     // workgroups per CU: resident capacity (4 waves/SIMD at the kernel's register count) by default,
     // so no render workgroup waits in the dispatcher ahead of another stream's kernels
-    static const int wg_per_cu = [] { const char* e = getenv("GSR_RENDER_WG_PER_CU"); return e ? atoi(e) : 4; }();
+    static const int wg_per_cu = [] { const char* e = getenv("GSR_RENDER_WG_PER_CU"); return e ? atoi(e) : 3; }();
     // GSR_RENDER_LATENCY=0: single-frame launches use the throughput kernel (A/B)
     static const bool latency_mode = [] { const char* e = getenv("GSR_RENDER_LATENCY"); return !(e && e[0] == '0'); }();
+    // GSR_RENDER_HALF=0: single-frame launches use full-strip waves (A/B); GSR_RENDER_HALF_WG: WGs per CU
+    static const bool half_mode = [] { const char* e = getenv("GSR_RENDER_HALF"); return !(e && e[0] == '0'); }();
+    static const int half_wg = [] { const char* e = getenv("GSR_RENDER_HALF_WG"); return e ? atoi(e) : 3; }();
     const int grid = min((nwaves + 3) / 4, persistent_grid(wg_per_cu));
     const dim3 gr(grid), bl(GSR_TILE_PIX);
 #define GSR_LAUNCH(E, S, L) hipLaunchKernelGGL((k_render_fwd<E, S, L>), gr, bl, 0, s, d, in, g, im, b, o)
@@ -612,6 +681,18 @@ void launch_render_fwd(const Dims& d, const Inputs& in, const GeomArena& g, cons
     else if (ablate == 1) hipLaunchKernelGGL((k_render_fwd_ablate<1>), gr, bl, 0, s, d, in, g, im, b, o);
     else if (ablate == 2) hipLaunchKernelGGL((k_render_fwd_ablate<2>), gr, bl, 0, s, d, in, g, im, b, o);
     else if (ablate == 4) hipLaunchKernelGGL((k_render_fwd_ablate<4>), gr, bl, 0, s, d, in, g, im, b, o);
+    else if (d.B == 1 && latency_mode && half_mode) {
+        // one frame, half-strip waves: a strip's two halves run in parallel, each lane one
+        // (pixel, Gaussian) alpha per k-step -- the longest strip's time is what counts here
+        const dim3 gl(min((2 * nwaves + 3) / 4, persistent_grid(half_wg)));
+        if (split) {
+            if (exact) hipLaunchKernelGGL((k_render_fwd<true, false, false, 1, 5, true>), gl, bl, 0, s, d, in, g, im, b, o);
+            else hipLaunchKernelGGL((k_render_fwd<false, false, false, 1, 5, true>), gl, bl, 0, s, d, in, g, im, b, o);
+        } else {
+            if (exact) hipLaunchKernelGGL((k_render_fwd<true, false, false, 0, 5, true>), gl, bl, 0, s, d, in, g, im, b, o);
+            else hipLaunchKernelGGL((k_render_fwd<false, false, false, 0, 5, true>), gl, bl, 0, s, d, in, g, im, b, o);
+        }
+    }
     else if (d.B == 1 && latency_mode) {  // one frame: the longest strip's wave sets the time
         const dim3 gl(min((nwaves + 3) / 4, persistent_grid(3)));  // 3 waves per SIMD at 5 slots
         if (split) {
