@@ -327,25 +327,39 @@ __global__ __launch_bounds__(kCountThreads) void k_bucket_count_lds(Dims d, Geom
 }
 
 // One workgroup per frame: bucket counts -> bucket starts (entry NB = visible count); buckets
-// longer than kTinyBucket go to the segment-sort worklist.
+// longer than kTinyBucket go to the segment-sort worklist.  The table (NB + 1 <= 16385 words) is
+// staged through LDS with coalesced loads and stores; each thread scans a contiguous run of it
+// there (odd run length: conflict-free), so no thread walks global memory at a stride.
+constexpr int kBucketScanLds = (1 << 14) + 1;
 __global__ __launch_bounds__(1024) void k_bucket_scan(Dims d, GeomArena g) {
     __shared__ uint32_t sh[1024 / 64 + 1];
+    __shared__ uint32_t tab[kBucketScanLds];
     if (g.ctrl[kCtrlOverflow]) return;
     const int b = blockIdx.x;
     uint32_t* bs = g.bstart + (int64_t)b * (d.NB + 1);
     const int n = d.NB + 1;
+    const bool staged = n <= kBucketScanLds;  // uniform (NB <= 16384 up to 512k Gaussians)
+    uint32_t* t = staged ? tab : bs;
+    if (staged) {
+        for (int k = threadIdx.x; k < n; k += 1024) tab[k] = bs[k];
+        __syncthreads();
+    }
     const int per = (n + 1023) / 1024;
     const int beg = threadIdx.x * per;
     const int end = min(n, beg + per);
     uint32_t s = 0;
-    for (int k = beg; k < end; k++) s += bs[k];
+    for (int k = beg; k < end; k++) s += t[k];
     uint32_t total;
-    uint32_t ex = block_excl_scan<uint32_t, 1024>(s, &total, sh);
+    uint32_t ex = block_excl_scan<uint32_t, 1024>(s, &total, sh);  // (barriers inside)
     for (int k = beg; k < end; k++) {
-        const uint32_t c = bs[k];
-        bs[k] = ex;
+        const uint32_t c = t[k];
+        t[k] = ex;
         if (c > (uint32_t)kTinyBucket) g.big[atomicAdd(&g.ctrl[kCtrlNumBig], 1u)] = (uint32_t)(b * d.NB + k);
         ex += c;
+    }
+    if (staged) {
+        __syncthreads();
+        for (int k = threadIdx.x; k < n; k += 1024) bs[k] = tab[k];
     }
     if (threadIdx.x == 0) g.fstat[kFsWords * b + kFsVisible] = total;
 }
