@@ -632,8 +632,16 @@ __device__ __forceinline__ void render_fwd_body(const Dims& d, const Inputs& in,
     }
 }
 
+// Register budget: 5 waves per SIMD (96 registers; the few values spilled live outside the blend
+// loop) for the 3-slot and half-strip kernels, launched 5 workgroups per CU: the blend loop is
+// VALU-issue-bound with latency that 4 waves did not cover.  The full-strip 5-slot latency kernel
+// keeps a 3-wave budget (it is launched 3 per CU).
+#ifndef GSR_RENDER_WPE
+#define GSR_RENDER_WPE 5
+#endif
 template <bool EXACT, bool STATS, bool TL, int SPLIT = 0, int NSLOT = GSR_BATCH_NSLOT, bool HALF = false>
-__global__ __launch_bounds__(GSR_TILE_PIX) void k_render_fwd(Dims d, Inputs in, GeomArena g,
+__global__ __launch_bounds__(GSR_TILE_PIX)
+__attribute__((amdgpu_waves_per_eu((NSLOT == 5 && !HALF) ? 3 : GSR_RENDER_WPE))) void k_render_fwd(Dims d, Inputs in, GeomArena g,
                                                              ImageArena im, BinArena bn, Outputs o) {
     render_fwd_body<EXACT, STATS, TL, false, 0, SPLIT, NSLOT, HALF>(d, in, g, im, bn, o);
 }
@@ -661,9 +669,12 @@ void launch_render_fwd(const Dims& d, const Inputs& in, const GeomArena& g, cons
     static const int ablate = [] { const char* e = getenv("GSR_RENDER_ABLATE"); return e ? atoi(e) : 0; }();
     const int nwaves = d.B * d.T * kStrips;  // upper bound of the work items
     if (nwaves == 0) return;
-    // workgroups per CU: resident capacity (4 waves/SIMD at the kernel's register count) by default,
-    // so no render workgroup waits in the dispatcher ahead of another stream's kernels
-    static const int wg_per_cu = [] { const char* e = getenv("GSR_RENDER_WG_PER_CU"); return e ? atoi(e) : 3; }();
+    // workgroups per CU: at most the resident capacity (GSR_RENDER_WPE waves/SIMD at the kernel's
+    // register budget), so no render workgroup waits in the dispatcher ahead of another stream's
+    // kernels.  Large batches take all 5 (-3% at 32 frames); small ones 4 (5 was +4% at the
+    // 6-frame training batch, where fewer strips per wave leave a longer tail).
+    static const int wg_env = [] { const char* e = getenv("GSR_RENDER_WG_PER_CU"); return e ? atoi(e) : 0; }();
+    const int wg_per_cu = wg_env > 0 ? wg_env : (d.B >= 16 ? GSR_RENDER_WPE : 4);
     // GSR_RENDER_LATENCY=0: single-frame launches use the throughput kernel (A/B)
     static const bool latency_mode = [] { const char* e = getenv("GSR_RENDER_LATENCY"); return !(e && e[0] == '0'); }();
     // GSR_RENDER_HALF=0: single-frame launches use full-strip waves (A/B); GSR_RENDER_HALF_WG: WGs per CU
@@ -674,9 +685,10 @@ void launch_render_fwd(const Dims& d, const Inputs& in, const GeomArena& g, cons
 #define GSR_LAUNCH(E, S, L) hipLaunchKernelGGL((k_render_fwd<E, S, L>), gr, bl, 0, s, d, in, g, im, b, o)
     if (o.stats) { if (exact) GSR_LAUNCH(true, true, false); else GSR_LAUNCH(false, true, false); }
     else if (o.timeline) { if (exact) GSR_LAUNCH(true, false, true); else GSR_LAUNCH(false, false, true); }
-    else if (o.out_refine) {
-        if (exact) hipLaunchKernelGGL((k_render_fwd_refine<true>), gr, bl, 0, s, d, in, g, im, b, o);
-        else hipLaunchKernelGGL((k_render_fwd_refine<false>), gr, bl, 0, s, d, in, g, im, b, o);
+    else if (o.out_refine) {  // (4-wave register budget: 4 workgroups per CU)
+        const dim3 grf(min((nwaves + 3) / 4, persistent_grid(4)));
+        if (exact) hipLaunchKernelGGL((k_render_fwd_refine<true>), grf, bl, 0, s, d, in, g, im, b, o);
+        else hipLaunchKernelGGL((k_render_fwd_refine<false>), grf, bl, 0, s, d, in, g, im, b, o);
     }
     else if (ablate == 1) hipLaunchKernelGGL((k_render_fwd_ablate<1>), gr, bl, 0, s, d, in, g, im, b, o);
     else if (ablate == 2) hipLaunchKernelGGL((k_render_fwd_ablate<2>), gr, bl, 0, s, d, in, g, im, b, o);
