@@ -213,6 +213,7 @@ __global__ __launch_bounds__(GSR_TILE_PIX) __attribute__((amdgpu_waves_per_eu(2)
 
         // strip-centred pixel offsets (exact in f32): the moments use lx = x - cx, ly = y - cy
         const float cx = (float)sx0 + 3.5f, cy = (float)sy0 + 3.5f;
+        const float bg_term = -T_final * bg_dot;  // per pixel, so the background term is one fma per slot
         float T = T_final;
         float accum_dot = 0.f, last_gdot = 0.f, last_alpha = 0.f;
         float accum_inv = 0.f, last_inv = 0.f;
@@ -286,22 +287,23 @@ __global__ __launch_bounds__(GSR_TILE_PIX) __attribute__((amdgpu_waves_per_eu(2)
                 Tq = fmaf(fmaf(-Tq, one_m, T), rinv1m, Tq);
                 T = act ? Tq : T;
                 const float wgt = act ? alpha * T : 0.f;
-                const float acc_n = last_alpha * last_gdot + (1.f - last_alpha) * accum_dot;
+                // the reference's recurrence a' = la * lg + (1 - la) a (backward.cu:532-537), as a + la (lg - a)
+                const float acc_n = fmaf(last_alpha, last_gdot - accum_dot, accum_dot);
                 accum_dot = act ? acc_n : accum_dot;
                 last_gdot = act ? gdot : last_gdot;
                 float dL_dalpha = gdot - accum_dot;
                 if (INVD) {
-                    const float ai_n = last_alpha * last_inv + (1.f - last_alpha) * accum_inv;
+                    const float ai_n = fmaf(last_alpha, last_inv - accum_inv, accum_inv);
                     accum_inv = act ? ai_n : accum_inv;
                     last_inv = act ? ra.w : last_inv;
                     dL_dalpha += (ra.w - accum_inv) * dL_inv;
                 }
                 dL_dalpha *= T;
                 last_alpha = act ? alpha : last_alpha;
-                dL_dalpha += (-T_final * rinv1m) * bg_dot;
+                dL_dalpha = fmaf(bg_term, rinv1m, dL_dalpha);  // + (-T_final / (1 - alpha)) bg . dL
                 // u = G dL/dalpha (0 where the pixel does not take the Gaussian; G may be inf there)
                 const float u = act ? G * dL_dalpha : 0.f;
-                amask |= __any(act) ? (1u << s) : 0u;
+                amask |= __builtin_amdgcn_ballot_w64(act) ? (1u << s) : 0u;
                 wl[s * kBwdPitch + lane] = wgt;
                 ul[s * kBwdPitch + lane] = u;
                 __builtin_amdgcn_sched_barrier(0);  // slot by slot: no register build-up across slots
