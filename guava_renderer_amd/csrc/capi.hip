@@ -404,7 +404,7 @@ int gsr_backward(int P, int D, int M, int R, const float* background, int width,
     gr.dL_dcov3D = dL_dcov3D;
     gr.dL_dscale = (cov3D_precomp == nullptr) ? dL_dscale : nullptr;
     gr.dL_drot = (cov3D_precomp == nullptr) ? dL_drot : nullptr;
-    { StageTimer st_(7, s); launch_render_bwd(d, in, g, im, bn, gr, g_exact_exp != 0, s); }
+    { StageTimer st_(7, s); launch_render_bwd(d, in, g, im, bn, gr, g_exact_exp != 0, g_split_bf16 != 0, s); }
     STAGE(debug, s, "render_bwd");
     { StageTimer st_(8, s); launch_preprocess_bwd(d, in, g, gr, s); }
     STAGE(debug, s, "preprocess_bwd");
@@ -545,7 +545,7 @@ static int backward_batch(int B, int P, int width, int height, const float* mean
     in.bg = backgrounds; in.s_bg = bg_stride;
     in.scale_mod = scale_modifier;
     in.antialiasing = antialiasing;
-    { StageTimer st_(7, s); launch_render_bwd(d, in, g, im, bn, grads, g_exact_exp != 0, s); }
+    { StageTimer st_(7, s); launch_render_bwd(d, in, g, im, bn, grads, g_exact_exp != 0, g_split_bf16 != 0, s); }
     { StageTimer st_(8, s); launch_preprocess_bwd(d, in, g, grads, s); }
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return fail(GSR_ERR_HIP, std::string("backward_batch: ") + hipGetErrorString(e));

@@ -270,7 +270,9 @@ void launch_ordered_scatter(const Dims& d, const GeomArena& g, const ImageArena&
 void launch_render_fwd(const Dims& d, const Inputs& in, const GeomArena& g, const ImageArena& im,
                        const BinArena& b, const Outputs& o, bool exact, bool split, hipStream_t s);
 void launch_render_bwd(const Dims& d, const Inputs& in, const GeomArena& g, const ImageArena& im,
-                       const BinArena& b, const Grads& gr, bool exact, hipStream_t s);
+                       const BinArena& b, const Grads& gr, bool exact, bool split, hipStream_t s);
+// the split-bf16 (hi | lo << 16) words of a [P][32] feature table -> out (g.fsplit)
+void launch_split_features(int P, const float* colors, uint32_t* out, hipStream_t s);
 void launch_preprocess_bwd(const Dims& d, const Inputs& in, const GeomArena& g, const Grads& gr,
                            hipStream_t s);
 void launch_refine_prepare(int n, const float* in, const float* w, int n_out, int keep, float* out,

@@ -18,7 +18,12 @@
 //    a, b, c, o combinations of sum u, sum u dx, sum u dy, sum u dx^2, sum u dx dy, sum u dy^2 --
 //    see the flush), with dL/dinvdepth = sum w dL/dinvdepth_px; the batch's atomics go out together.
 //
-// Both contractions run on v_mfma_f32_32x32x2_f32 (exact f32 products, f32 accumulation).
+// Both contractions run on v_mfma_f32_32x32x2_f32 (exact f32 products, f32 accumulation).  With the
+// split-bf16 switch (gsr_set_split_bf16, SPLIT > 0) the g contraction runs on
+// v_mfma_f32_32x32x8_bf16 instead: f = f_hi + f_lo and dL = d_hi + d_lo, all four products of a
+// channel exact in f32 and summed in f32 (<= 3e-5 relative per product).  The features come
+// pre-split (SPLIT 2: the batch-shared table of k_split_features) or are split here (SPLIT 1:
+// per-frame features).
 #include <cstdlib>
 
 #include "gsr_internal.h"
@@ -28,6 +33,8 @@ namespace gsr {
 typedef float floatx16 __attribute__((ext_vector_type(16)));
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef unsigned uint4x __attribute__((ext_vector_type(4)));
+typedef unsigned uint2x __attribute__((ext_vector_type(2)));
+typedef short shortx4 __attribute__((ext_vector_type(4)));
 
 constexpr int kBwdBatch = 32;   // survivors per batch
 constexpr int kBwdPitch = 65;   // LDS row pitch (floats) of the [32][64] w / u tiles
@@ -57,7 +64,7 @@ __device__ __forceinline__ float add_halves(float x) {
 // ABL (timing ablations only, wrong gradients): 1 = no atomics, 2 = no serial replay, 3 = no
 // flush (colour MFMA, moments, atomics), 4 = no list walk beyond the ring fill (batches empty),
 // 5 / 6 = VALU stand-ins for the g / the colour contraction's MFMAs
-template <bool EXACT, bool INVD, int ABL = 0>
+template <bool EXACT, bool INVD, int SPLIT = 0, int ABL = 0>
 __global__ __launch_bounds__(GSR_TILE_PIX) __attribute__((amdgpu_waves_per_eu(2))) void k_render_bwd(
     Dims d, Inputs in, GeomArena g, ImageArena im, BinArena bn, Grads gr) {
     __shared__ float lds_all[(GSR_TILE_PIX / 64) * kBwdLdsWave];
@@ -106,7 +113,8 @@ __global__ __launch_bounds__(GSR_TILE_PIX) __attribute__((amdgpu_waves_per_eu(2)
         const uint2 range = im.ranges[tile_g];
         const uint32_t* __restrict__ plist = bn.point_list + range.x;
         const float4* __restrict__ rrec = g.rrec + (int64_t)b * d.P * 2;
-        const float* __restrict__ colors = in.colors + in.s_colors * b;
+        const float* __restrict__ colors = SPLIT == 2 ? reinterpret_cast<const float*>(g.fsplit)
+                                                      : in.colors + in.s_colors * b;
         const int64_t gbase = (int64_t)b * d.P;
         const int64_t cbase = gr.reduce ? 0 : gbase;  // frame-reduced colour gradients: one [P][C] block
 
@@ -146,12 +154,18 @@ __global__ __launch_bounds__(GSR_TILE_PIX) __attribute__((amdgpu_waves_per_eu(2)
         // g = f . dL contraction B operands: k-step k of pixel half h, lane l: dL[channel 16(l>>5) + k]
         // [pixel 32h + (l&31)] -- one swap per k turns (dL[k], dL[16+k]) into both halves' operands
         float bh0[16], bh1[16];
+        // SPLIT: the g contraction's dL operands as packed bf16 (hi | lo)
+        unsigned bp0[16], bp1[16];
 #pragma unroll
         for (int k = 0; k < 16; k++) {
             const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(dL[k]), __float_as_uint(dL[16 + k]),
                                                              false, false);
             bh0[k] = __uint_as_float(sw[0]);
             bh1[k] = __uint_as_float(sw[1]);
+            if (SPLIT) {
+                bp0[k] = split_hl(bh0[k]);
+                bp1[k] = split_hl(bh1[k]);
+            }
         }
 
         // ---- survivor stream: chunks of 64 list positions, last chunk first (the next lower chunk
@@ -235,6 +249,33 @@ __global__ __launch_bounds__(GSR_TILE_PIX) __attribute__((amdgpu_waves_per_eu(2)
             floatx16 gd0, gd1;
 #pragma unroll
             for (int r = 0; r < 16; r++) { gd0[r] = 0.f; gd1[r] = 0.f; }
+            if (SPLIT) {
+                // k-pairs (k, k+1): lane half h's four k-slots hold (d_hi, d_lo) of channels 16h + k and
+                // 16h + k + 1 (B, compact: one register per channel); A repeats f_hi (then f_lo) of
+                // the same channels, so two MFMAs give all four products of both channels
+#pragma unroll
+                for (int k = 0; k < 16; k += 2) {
+                    unsigned fh0, fl0, fh1, fl1;
+                    if (SPLIT == 2) {  // (hi | lo) table words -> (hi | hi), (lo | lo)
+                        const unsigned t0 = __float_as_uint(fr[k]), t1 = __float_as_uint(fr[k + 1]);
+                        fh0 = __builtin_amdgcn_perm(t0, t0, 0x01000100u);
+                        fl0 = __builtin_amdgcn_perm(t0, t0, 0x03020302u);
+                        fh1 = __builtin_amdgcn_perm(t1, t1, 0x01000100u);
+                        fl1 = __builtin_amdgcn_perm(t1, t1, 0x03020302u);
+                    } else {
+                        split_hh_ll(fr[k], fh0, fl0);
+                        split_hh_ll(fr[k + 1], fh1, fl1);
+                    }
+                    const shortx4 ah = __builtin_bit_cast(shortx4, (uint2x){fh0, fh1});
+                    const shortx4 al = __builtin_bit_cast(shortx4, (uint2x){fl0, fl1});
+                    const shortx4 b0 = __builtin_bit_cast(shortx4, (uint2x){bp0[k], bp0[k + 1]});
+                    const shortx4 b1 = __builtin_bit_cast(shortx4, (uint2x){bp1[k], bp1[k + 1]});
+                    gd0 = __builtin_amdgcn_mfma_f32_32x32x8bf16_1k(ah, b0, gd0, 0, 0, 0);
+                    gd1 = __builtin_amdgcn_mfma_f32_32x32x8bf16_1k(ah, b1, gd1, 0, 0, 0);
+                    gd0 = __builtin_amdgcn_mfma_f32_32x32x8bf16_1k(al, b0, gd0, 0, 0, 0);
+                    gd1 = __builtin_amdgcn_mfma_f32_32x32x8bf16_1k(al, b1, gd1, 0, 0, 0);
+                }
+            } else
 #pragma unroll
             for (int k = 0; k < 16; k++) {
                 if (ABL == 5) {  /* timing ablation: VALU stand-in for the g contraction */
@@ -256,7 +297,6 @@ __global__ __launch_bounds__(GSR_TILE_PIX) __attribute__((amdgpu_waves_per_eu(2)
             wave_lds_order();
 
             // ---- serial replay of the batch, slot by slot (static slots: g lives in registers)
-            uint32_t amask = 0;  // slots with an active pixel (the others add nothing)
 #pragma unroll
             for (int s = 0; s < kBwdBatch; s++) {
                 if ((uint32_t)s >= nb || ABL == 2) continue;  // (not break: the loop must unroll -- static slots)
@@ -278,7 +318,7 @@ __global__ __launch_bounds__(GSR_TILE_PIX) __attribute__((amdgpu_waves_per_eu(2)
                     G = expf_fast(power);
                     alpha = fminf(0.99f, ra.z * G);
                 }
-                const bool act = inside && contributor < last_contributor && !(power > 0.0f) &&
+                const bool act = contributor < last_contributor && !(power > 0.0f) &&  // (outside: last 0)
                                  !(power < -87.0f) && !(alpha < 1.0f / 255.0f);
                 const float one_m = 1.f - alpha;
                 const float rinv1m = __builtin_amdgcn_rcpf(one_m);
@@ -296,14 +336,13 @@ __global__ __launch_bounds__(GSR_TILE_PIX) __attribute__((amdgpu_waves_per_eu(2)
                     const float ai_n = fmaf(last_alpha, last_inv - accum_inv, accum_inv);
                     accum_inv = act ? ai_n : accum_inv;
                     last_inv = act ? ra.w : last_inv;
-                    dL_dalpha += (ra.w - accum_inv) * dL_inv;
+                    dL_dalpha = fmaf(ra.w - accum_inv, dL_inv, dL_dalpha);
                 }
                 dL_dalpha *= T;
                 last_alpha = act ? alpha : last_alpha;
                 dL_dalpha = fmaf(bg_term, rinv1m, dL_dalpha);  // + (-T_final / (1 - alpha)) bg . dL
                 // u = G dL/dalpha (0 where the pixel does not take the Gaussian; G may be inf there)
                 const float u = act ? G * dL_dalpha : 0.f;
-                amask |= __builtin_amdgcn_ballot_w64(act) ? (1u << s) : 0u;
                 wl[s * kBwdPitch + lane] = wgt;
                 ul[s * kBwdPitch + lane] = u;
                 __builtin_amdgcn_sched_barrier(0);  // slot by slot: no register build-up across slots
@@ -368,7 +407,9 @@ __global__ __launch_bounds__(GSR_TILE_PIX) __attribute__((amdgpu_waves_per_eu(2)
                     const uint32_t gsl = __builtin_amdgcn_readlane(bg_, (r & 3) + 8 * (r >> 2)) ;
                     const uint32_t gsh = __builtin_amdgcn_readlane(bg_, (r & 3) + 8 * (r >> 2) + 4);
                     const uint32_t gs = hi ? gsh : gsl;
-                    if ((amask >> sl) & 1u) atomicAdd(gr.dL_dcolors + (cbase + gs) * GSR_C + l32, acc[r]);
+                    // slots past the batch hold stale tiles; a zero sum (no pixel took the Gaussian,
+                    // or no gradient) adds nothing
+                    if (sl < nb && acc[r] != 0.f) atomicAdd(gr.dL_dcolors + (cbase + gs) * GSR_C + l32, acc[r]);
                 }
             }
             // the other terms of slot l&31, from the pixel moments of u about the Gaussian's centre
@@ -406,7 +447,7 @@ __global__ __launch_bounds__(GSR_TILE_PIX) __attribute__((amdgpu_waves_per_eu(2)
                     const uint32_t sl = (uint32_t)(8 * qq + (lane >> 3));
                     const uint32_t gs = (uint32_t)__shfl((int)bg_, (int)sl);
                     const float val = rows[8 * sl + (lane & 7)];
-                    if (((amask >> sl) & 1u) && (lane & 7) != 7 && (INVD || (lane & 7) != kGtInv))
+                    if (sl < nb && val != 0.f && (lane & 7) != 7 && (INVD || (lane & 7) != kGtInv))
                         atomicAdd(g.gterm + (gbase + gs) * kGtWords + (lane & 7), val);
                 }
             }
@@ -424,7 +465,7 @@ __global__ void k_zero_bwd_queues(uint32_t* ctrl) {
 }
 
 void launch_render_bwd(const Dims& d, const Inputs& in, const GeomArena& g, const ImageArena& im,
-                       const BinArena& b, const Grads& gr, bool exact, hipStream_t s) {
+                       const BinArena& b, const Grads& gr, bool exact, bool split, hipStream_t s) {
     const int nwaves = d.B * d.T * kStrips;  // upper bound of the work items
     if (nwaves == 0) return;
     hipLaunchKernelGGL(k_zero_bwd_queues, dim3(1), dim3(64), 0, s, g.ctrl);
@@ -433,20 +474,34 @@ void launch_render_bwd(const Dims& d, const Inputs& in, const GeomArena& g, cons
     const dim3 grid(min((nwaves + 3) / 4, persistent_grid(2))), blk(GSR_TILE_PIX);
     static const int ablate = [] { const char* e = getenv("GSR_BWD_ABLATE"); return e ? atoi(e) : 0; }();
     if (ablate >= 1 && ablate <= 6 && exact && invd) {
-        if (ablate == 1) hipLaunchKernelGGL((k_render_bwd<true, true, 1>), grid, blk, 0, s, d, in, g, im, b, gr);
-        if (ablate == 2) hipLaunchKernelGGL((k_render_bwd<true, true, 2>), grid, blk, 0, s, d, in, g, im, b, gr);
-        if (ablate == 3) hipLaunchKernelGGL((k_render_bwd<true, true, 3>), grid, blk, 0, s, d, in, g, im, b, gr);
-        if (ablate == 5) hipLaunchKernelGGL((k_render_bwd<true, true, 5>), grid, blk, 0, s, d, in, g, im, b, gr);
-        if (ablate == 6) hipLaunchKernelGGL((k_render_bwd<true, true, 6>), grid, blk, 0, s, d, in, g, im, b, gr);
+        if (ablate == 1) hipLaunchKernelGGL((k_render_bwd<true, true, 0, 1>), grid, blk, 0, s, d, in, g, im, b, gr);
+        if (ablate == 2) hipLaunchKernelGGL((k_render_bwd<true, true, 0, 2>), grid, blk, 0, s, d, in, g, im, b, gr);
+        if (ablate == 3) hipLaunchKernelGGL((k_render_bwd<true, true, 0, 3>), grid, blk, 0, s, d, in, g, im, b, gr);
+        if (ablate == 5) hipLaunchKernelGGL((k_render_bwd<true, true, 0, 5>), grid, blk, 0, s, d, in, g, im, b, gr);
+        if (ablate == 6) hipLaunchKernelGGL((k_render_bwd<true, true, 0, 6>), grid, blk, 0, s, d, in, g, im, b, gr);
         return;
     }
-    if (exact) {
-        if (invd) hipLaunchKernelGGL((k_render_bwd<true, true>), grid, blk, 0, s, d, in, g, im, b, gr);
-        else hipLaunchKernelGGL((k_render_bwd<true, false>), grid, blk, 0, s, d, in, g, im, b, gr);
-    } else {
-        if (invd) hipLaunchKernelGGL((k_render_bwd<false, true>), grid, blk, 0, s, d, in, g, im, b, gr);
-        else hipLaunchKernelGGL((k_render_bwd<false, false>), grid, blk, 0, s, d, in, g, im, b, gr);
+    // split-bf16 contractions; one feature table for the batch is split once (into the forward's
+    // fsplit rows, which this launch owns until it ends)
+    // GSR_BWD_SPLIT=0: f32 contractions even with the split switch on (A/B)
+    static const bool bwd_split = [] { const char* e = getenv("GSR_BWD_SPLIT"); return !(e && e[0] == '0'); }();
+    int sp = 0;
+    if (split && bwd_split) {
+        sp = 1;
+        if (in.s_colors == 0) {
+            launch_split_features(d.P, in.colors, g.fsplit, s);
+            sp = 2;
+        }
     }
+#define GSR_BWD(E, I, S) hipLaunchKernelGGL((k_render_bwd<E, I, S>), grid, blk, 0, s, d, in, g, im, b, gr)
+#define GSR_BWD_S(E, I) { if (sp == 2) GSR_BWD(E, I, 2); else if (sp == 1) GSR_BWD(E, I, 1); else GSR_BWD(E, I, 0); }
+    if (exact) {
+        if (invd) GSR_BWD_S(true, true) else GSR_BWD_S(true, false)
+    } else {
+        if (invd) GSR_BWD_S(false, true) else GSR_BWD_S(false, false)
+    }
+#undef GSR_BWD_S
+#undef GSR_BWD
 }
 
 }  // namespace gsr

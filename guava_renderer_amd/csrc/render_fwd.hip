@@ -244,6 +244,12 @@ __global__ __launch_bounds__(256) void k_refine_prepare(int n, const float* __re
     }
 }
 
+void launch_split_features(int P, const float* colors, uint32_t* out, hipStream_t s) {
+    if (P <= 0) return;
+    hipLaunchKernelGGL(k_split_features, dim3((P * GSR_C / 4 + 255) / 256), dim3(256), 0, s, P * GSR_C / 4,
+                       reinterpret_cast<const float4*>(colors), reinterpret_cast<uint4*>(out));
+}
+
 void launch_refine_prepare(int n, const float* in, const float* w, int n_out, int keep, float* out,
                            hipStream_t s) {
     if (n <= 0) return;

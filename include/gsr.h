@@ -59,7 +59,9 @@ int gsr_set_exact_exp(int on);
  * fmaf chain (default); 1 = split-bf16 MFMA (f = f_hi + f_lo, four exact bf16 products per
  * feature x weight, f32 accumulation): <= 3e-5 relative per product, colour L-inf within the
  * north_star's 1e-4; final_T, n_contrib and inverse depth stay bit-exact.  Returns the previous
- * setting.  No reference counterpart (forward.cu:371-372 accumulates in f32). */
+ * setting.  The same switch puts the backward's two contractions (g = f . dL/dpixel and
+ * dL/dcolor = sum_px w dL/dpixel) on split-bf16 MFMAs; gradients stay within 1e-4 of their scale.
+ * No reference counterpart (forward.cu:371-372 accumulates in f32). */
 int gsr_set_split_bf16(int on);
 
 /* Scratch sizes used by gsr_forward (the three resizer requests).  Unlike the reference's

@@ -72,6 +72,23 @@ def test_backward_matches_oracle(kind, P, W, H, seed):
     _check(_gpu_backward(d, dL, dLinv), _oracle_backward(d, dL, dLinv))
 
 
+@pytest.mark.parametrize("kind,P,W,H,seed", [("random", 2000, 96, 64, 1), ("avatar", 12000, 128, 128, 3)])
+def test_backward_split_bf16_matches_oracle(kind, P, W, H, seed):
+    """gsr_set_split_bf16(1): the backward's g = f . dL/dpixel contraction on split-bf16 MFMAs (the
+    single-frame feature table pre-split by k_split_features) -- same 1e-4 bar."""
+    from guava_renderer_amd import _lib
+    d = make_scene(kind, P, W, H, seed=seed)
+    rng = np.random.default_rng(seed)
+    dL = rng.normal(size=(32, H, W)).astype(np.float32)
+    dLinv = rng.normal(size=(1, H, W)).astype(np.float32)
+    prev = _lib.set_split_bf16(True)
+    try:
+        g = _gpu_backward(d, dL, dLinv)
+    finally:
+        _lib.set_split_bf16(bool(prev))
+    _check(g, _oracle_backward(d, dL, dLinv))
+
+
 def test_backward_no_invdepth_grad():
     d = make_scene("random", 3000, 96, 96, seed=4)
     rng = np.random.default_rng(4)

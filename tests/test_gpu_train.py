@@ -107,12 +107,15 @@ def test_config5_backward_single_frame():
             assert err <= TOL, f"{name}: {err:.3g}"
 
 
-def test_fullsize_backward_batch6():
+@pytest.mark.parametrize("split,per_frame_colors", [(False, False), (True, False), (True, True)])
+def test_fullsize_backward_batch6(split, per_frame_colors):
     """BatchRasterizer.backward at the training batch (6 per-frame views): frames 0 and 5 vs the
-    oracle, per-frame gradient tensors."""
+    oracle, per-frame gradient tensors.  split: the split-bf16 switch, whose g contraction takes the
+    batch-shared pre-split feature table, or splits per-frame features ([B, P, 32]) in the kernel."""
     from guava_renderer_amd import _lib
     from guava_renderer_amd.batch import BatchRasterizer
     _lib.set_exact_exp(True)
+    prev = _lib.set_split_bf16(split)
     sc, cams = _scene_c2(cams=6)
     cams = cams[:6]
     B = 6
@@ -122,13 +125,18 @@ def test_fullsize_backward_batch6():
     tanf = t(np.array([[c["tanfovx"], c["tanfovy"]] for c in cams], np.float32))
     bgs = torch.zeros((B, 32), device=DEV)
     args = [t(sc[k]) for k in ("means3D", "colors", "opacities", "scales", "rotations")]
+    if per_frame_colors:
+        args[1] = args[1][None].repeat(B, 1, 1).contiguous()
     r = BatchRasterizer(B, 100000, 512, 512, R_capacity=12 * 100000 * B, device=DEV)
-    r.forward(*args, views, projs, tanf, bgs)
-    rng = np.random.default_rng(12)
-    dL = rng.normal(size=(B, 32, 512, 512)).astype(np.float32)
-    dLinv = rng.normal(size=(B, 512, 512)).astype(np.float32)
-    g = r.backward(*args, views, projs, tanf, bgs, t(dL), t(dLinv))
-    torch.cuda.synchronize()
+    try:
+        r.forward(*args, views, projs, tanf, bgs)
+        rng = np.random.default_rng(12)
+        dL = rng.normal(size=(B, 32, 512, 512)).astype(np.float32)
+        dLinv = rng.normal(size=(B, 512, 512)).astype(np.float32)
+        g = r.backward(*args, views, projs, tanf, bgs, t(dL), t(dLinv))
+        torch.cuda.synchronize()
+    finally:
+        _lib.set_split_bf16(bool(prev))
     assert not r.status()[1]
     gpu = {k: v.cpu().numpy() for k, v in g.items() if v is not None}
     for f in (0, 5):
