@@ -318,7 +318,7 @@ def profile_read():
 
 
 COUNTERS = ("pairs_evaluated", "pairs_contributing", "strip_pairs_blended", "mfma_ksteps",
-            "gaussians_staged", "list_entries", "tiles_rendered")
+            "gaussians_staged", "list_entries", "tiles_rendered", "dead_ksteps")
 
 
 def render_counters(fn, device="cuda"):

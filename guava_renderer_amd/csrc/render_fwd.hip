@@ -40,6 +40,9 @@ namespace gsr {
 #ifndef GSR_MFMA_K8
 #define GSR_MFMA_K8 1  // split-bf16 products on v_mfma_f32_32x32x8_bf16 (0: 32x32x16 with k 4..7 zero)
 #endif
+#ifndef GSR_SPLIT_FIRST
+#define GSR_SPLIT_FIRST 1  // split-bf16: split both weights before the lane-half swap (two swaps, no copies)
+#endif
 #ifndef GSR_BATCH_NSLOT
 #define GSR_BATCH_NSLOT 3  // pipeline slots of the batched (throughput) kernels
 #endif
@@ -377,7 +380,7 @@ __device__ __forceinline__ void render_fwd_body(const Dims& d, const Inputs& in,
         uint4x sa_ = {0u, 0u, 0u, 0u}, sb0_ = {0u, 0u, 0u, 0u}, sb1_ = {0u, 0u, 0u, 0u};  // SPLIT operands, k 4..7 stay 0
 #pragma unroll
         for (int r = 0; r < 16; r++) { acc0[r] = 0.f; acc1[r] = 0.f; }
-        uint64_t n_surv = 0, n_steps = 0, n_contrib_pairs = 0, n_staged = 0;
+        uint64_t n_surv = 0, n_steps = 0, n_contrib_pairs = 0, n_staged = 0, n_dead = 0;
 
         // Survivor stream: wave-uniform state walking the list 64 entries at a time; the next
         // chunk's entries (index | strip mask << 28) are always in flight.
@@ -506,6 +509,7 @@ __device__ __forceinline__ void render_fwd_body(const Dims& d, const Inputs& in,
                 if (!was_done_ && done_a_) stop = (uint32_t)S##pa;                                  \
                 else if (!done_a_ && done) stop = (uint32_t)S##pb;                                  \
                 n_contrib_pairs += __popcll(__ballot(wa_ > 0.f)) + __popcll(__ballot(wb_ > 0.f));   \
+                n_dead += (S##v && __ballot(wa_ > 0.f || wb_ > 0.f) == 0ull) ? 1 : 0;               \
                 n_surv += S##v ? (S##hb ? 2 : 1) : 0;                                               \
             }                                                                                       \
             if (STATS || TL) n_steps += S##v ? 1 : 0;                                               \
@@ -526,7 +530,19 @@ __device__ __forceinline__ void render_fwd_body(const Dims& d, const Inputs& in,
                 unsigned h0_, l0_, h1_, l1_;                                                        \
                 split_hh_ll(__uint_as_float(sw_[0]), h0_, l0_);                                     \
                 split_hh_ll(__uint_as_float(sw_[1]), h1_, l1_);                                     \
-                if (GSR_MFMA_K8) {  /* k = 8: exactly the four products per lane half, no padding */ \
+                if (GSR_SPLIT_FIRST) {  /* split both weights, then swap the (hi, hi) and (lo, lo) words: */ \
+                    /* the swaps consume the split words, the weights stay for the inverse depth */ \
+                    unsigned ha_, la_, hb_, lb_;                                                    \
+                    split_hh_ll(wa_, ha_, la_);                                                     \
+                    split_hh_ll(wb_, hb_, lb_);                                                     \
+                    const auto sh_ = __builtin_amdgcn_permlane32_swap(ha_, hb_, false, false);      \
+                    const auto sl_ = __builtin_amdgcn_permlane32_swap(la_, lb_, false, false);      \
+                    const uint2x a2_ = {fp_, fp_}, b0_ = {sh_[0], sl_[0]}, b1_ = {sh_[1], sl_[1]};  \
+                    acc0 = __builtin_amdgcn_mfma_f32_32x32x8bf16_1k(__builtin_bit_cast(shortx4, a2_), \
+                                                                   __builtin_bit_cast(shortx4, b0_), acc0, 0, 0, 0); \
+                    acc1 = __builtin_amdgcn_mfma_f32_32x32x8bf16_1k(__builtin_bit_cast(shortx4, a2_), \
+                                                                   __builtin_bit_cast(shortx4, b1_), acc1, 0, 0, 0); \
+                } else if (GSR_MFMA_K8) {  /* k = 8: exactly the four products per lane half, no padding */ \
                     const uint2x a2_ = {fp_, fp_}, b0_ = {h0_, l0_}, b1_ = {h1_, l1_};              \
                     acc0 = __builtin_amdgcn_mfma_f32_32x32x8bf16_1k(__builtin_bit_cast(shortx4, a2_), \
                                                                    __builtin_bit_cast(shortx4, b0_), acc0, 0, 0, 0); \
@@ -617,6 +633,7 @@ __device__ __forceinline__ void render_fwd_body(const Dims& d, const Inputs& in,
                 atomicAdd(&cn[2], (unsigned long long)n_surv);
                 atomicAdd(&cn[3], (unsigned long long)n_steps);
                 atomicAdd(&cn[4], (unsigned long long)n_staged);
+                atomicAdd(&cn[7], (unsigned long long)n_dead);
                 if (strip == 0) {
                     atomicAdd(&cn[5], (unsigned long long)n);
                     atomicAdd(&cn[6], 1ull);
