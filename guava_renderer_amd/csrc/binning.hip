@@ -703,7 +703,7 @@ __host__ __device__ __forceinline__ uint32_t strip_mask(float4 co, float4 pre, f
 // 64-bit masks per column and per row, in LDS), and base[] advances by the pass's per-tile totals.
 // The (chunk x tile) table and the per-workgroup base[] load shrink with the chunk, not the pass.
 template <int ABL>  // timing ablations (GSR_SCATTER_ABLATE): 1 = no strip test, 2 = no list store
-__global__ __launch_bounds__(kSlots) __attribute__((amdgpu_waves_per_eu(6))) void k_ordered_scatter(Dims d, GeomArena g, ImageArena im, BinArena bn) {
+__global__ __launch_bounds__(kSlots) __attribute__((amdgpu_waves_per_eu(6))) void k_ordered_scatter(Dims d, GeomArena g, ImageArena im, BinArena bn, int xcd_order) {
     uint32_t sink = 0;
     extern __shared__ uint64_t masks[];  // colm[gx][4], rowm[gy][4], then uint32 tile bases[T]
     __shared__ uint32_t s_pref[kSlots];
@@ -714,7 +714,22 @@ __global__ __launch_bounds__(kSlots) __attribute__((amdgpu_waves_per_eu(6))) voi
     __shared__ float4 s_pre[kSlots];
     __shared__ float2 s_m[kSlots];
     if (g.ctrl[kCtrlOverflow]) return;
-    const int b = blockIdx.y, c = blockIdx.x;
+    // XCD-aware order (GSR_SCATTER_XCD, default on): workgroup L runs on XCD L % 8, and XCD x takes
+    // the x-th eighth of the (frame, chunk) items in chunk order, so consecutive chunks -- which
+    // write adjacent entries of every tile list -- meet in one L2 and leave it as whole lines
+    // instead of partial ones from eight L2s.  Off: blockIdx order (chunk-major per frame).
+    int b, c;
+    if (xcd_order) {
+        const uint32_t L = blockIdx.x, N = (uint32_t)d.nchunk * (uint32_t)d.B;
+        const uint32_t M = (N + 7u) / 8u;
+        const uint32_t item = (L & 7u) * M + (L >> 3);
+        if (item >= N) return;
+        b = (int)(item / (uint32_t)d.nchunk);
+        c = (int)(item - (uint32_t)b * (uint32_t)d.nchunk);
+    } else {
+        b = blockIdx.y;
+        c = blockIdx.x;
+    }
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     const uint32_t V = g.fstat[kFsWords * b + kFsVisible];
     if ((uint32_t)c * d.chunk >= V) return;
@@ -808,11 +823,13 @@ void launch_ordered_scatter(const Dims& d, const GeomArena& g, const ImageArena&
             hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     }
     static const int abl = [] { const char* e = getenv("GSR_SCATTER_ABLATE"); return e ? atoi(e) : 0; }();
-    const dim3 gr(d.nchunk, d.B), bl(kSlots);
-    if (abl == 1) hipLaunchKernelGGL(k_ordered_scatter<1>, gr, bl, lds, s, d, g, im, b);
-    else if (abl == 2) hipLaunchKernelGGL(k_ordered_scatter<2>, gr, bl, lds, s, d, g, im, b);
-    else if (abl == 3) hipLaunchKernelGGL(k_ordered_scatter<3>, gr, bl, lds, s, d, g, im, b);
-    else hipLaunchKernelGGL(k_ordered_scatter<0>, gr, bl, lds, s, d, g, im, b);
+    static const int xo = [] { const char* e = getenv("GSR_SCATTER_XCD"); return (e && e[0] == '0') ? 0 : 1; }();
+    const uint32_t N = (uint32_t)d.nchunk * (uint32_t)d.B;
+    const dim3 gr = xo ? dim3(8u * ((N + 7u) / 8u)) : dim3(d.nchunk, d.B), bl(kSlots);
+    if (abl == 1) hipLaunchKernelGGL(k_ordered_scatter<1>, gr, bl, lds, s, d, g, im, b, xo);
+    else if (abl == 2) hipLaunchKernelGGL(k_ordered_scatter<2>, gr, bl, lds, s, d, g, im, b, xo);
+    else if (abl == 3) hipLaunchKernelGGL(k_ordered_scatter<3>, gr, bl, lds, s, d, g, im, b, xo);
+    else hipLaunchKernelGGL(k_ordered_scatter<0>, gr, bl, lds, s, d, g, im, b, xo);
 }
 
 // ---------------------------------------------------------------- 6. strip work list
