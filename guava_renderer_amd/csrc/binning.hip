@@ -887,15 +887,18 @@ __device__ __forceinline__ uint32_t tile_strip_max(const ImageArena& im, int64_t
 
 // Per frame: histogram over the buckets of its non-empty tiles' strips (tile_major = 0) or of the
 // tiles themselves keyed by their longest strip (tile_major = 1).
-__global__ __launch_bounds__(1024) void k_strip_hist(Dims d, ImageArena im, int tile_major) {
-    __shared__ uint32_t h[kStripBuckets];
+__global__ __launch_bounds__(1024) void k_strip_hist(Dims d, ImageArena im, int tile_major, int map) {
+    __shared__ uint32_t h[8 * kStripBuckets];
     const int b = blockIdx.x;
-    for (int i = threadIdx.x; i < kStripBuckets; i += 1024) h[i] = 0;
+    const int nh = map == 2 ? 8 * kStripBuckets : kStripBuckets;
+    for (int i = threadIdx.x; i < nh; i += 1024) h[i] = 0;
     __syncthreads();
     for (int t = threadIdx.x; t < d.T; t += 1024) {
         const int64_t tg = (int64_t)b * d.T + t;
         if (!im.tile_count[tg]) continue;
-        if (tile_major) {
+        if (map == 2) {  // (tile-major by construction)
+            atomicAdd(&h[tile_queue(t, d.gx) * kStripBuckets + strip_bucket(tile_strip_max(im, tg))], 1u);
+        } else if (tile_major) {
             atomicAdd(&h[strip_bucket(tile_strip_max(im, tg))], 1u);
         } else {
 #pragma unroll
@@ -903,7 +906,46 @@ __global__ __launch_bounds__(1024) void k_strip_hist(Dims d, ImageArena im, int 
         }
     }
     __syncthreads();
-    for (int i = threadIdx.x; i < kStripBuckets; i += 1024) im.strip_hist[b * kStripBuckets + i] = h[i];
+    for (int i = threadIdx.x; i < nh; i += 1024) im.strip_hist[(int64_t)b * nh + i] = h[i];
+}
+
+// map 2: list offsets of every (frame, queue, bucket) run, in place of the histogram.  The list is
+// queue-major (queue q's tiles form one segment), bucket-major inside a segment (most survivors
+// first), frame-major inside a bucket; the segment bounds go to ctrl[kCtrlQStart..] for queue_item.
+__global__ __launch_bounds__(1024) void k_strip_qscan(Dims d, ImageArena im, uint32_t* ctrl) {
+    constexpr int kN = 8 * kStripBuckets;  // (queue, bucket) runs, queue-major
+    __shared__ uint32_t tot[kN + 1];
+    __shared__ uint32_t sh[1024 / 64 + 1];
+    for (int i = threadIdx.x; i < kN; i += 1024) {
+        uint32_t a = 0;
+        for (int f = 0; f < d.B; f++) a += im.strip_hist[(int64_t)f * kN + i];
+        tot[i] = a;
+    }
+    if (threadIdx.x == 0) tot[kN] = 0;
+    __syncthreads();
+    // exclusive scan over the runs, two per thread (kN <= 2048)
+    const int i0 = 2 * threadIdx.x;
+    const uint32_t a0 = i0 < kN ? tot[i0] : 0u, a1 = i0 + 1 < kN ? tot[i0 + 1] : 0u;
+    uint32_t total;
+    const uint32_t ex = block_excl_scan<uint32_t, 1024>(a0 + a1, &total, sh);  // (barriers inside)
+    if (i0 < kN) tot[i0] = ex;
+    if (i0 + 1 < kN) tot[i0 + 1] = ex + a0;
+    if (threadIdx.x == 0) tot[kN] = total;
+    __syncthreads();
+    for (int i = threadIdx.x; i < kN; i += 1024) {
+        uint32_t run = tot[i];
+        for (int f = 0; f < d.B; f++) {
+            uint32_t* h = im.strip_hist + (int64_t)f * kN + i;
+            const uint32_t c = *h;
+            *h = run;
+            run += c;
+        }
+    }
+    if (threadIdx.x < 8) {
+        const int q = threadIdx.x;
+        ctrl[kCtrlQStart + q] = tot[q * kStripBuckets];
+        ctrl[kCtrlQStart + 8 + q] = tot[(q + 1) * kStripBuckets] - tot[q * kStripBuckets];
+    }
 }
 
 // Per frame: place its strips into the batch-wide strip list, bucket-major (most survivors first);
@@ -911,11 +953,25 @@ __global__ __launch_bounds__(1024) void k_strip_hist(Dims d, ImageArena im, int 
 // places whole tiles (their 4 strips consecutive) by their longest strip, so the render's
 // tile-affine queues (queue_item) keep a tile's strips -- which read the same Gaussians -- on one
 // XCD and its L2.
-__global__ __launch_bounds__(1024) void k_strip_place(Dims d, ImageArena im, int tile_major) {
+__global__ __launch_bounds__(1024) void k_strip_place(Dims d, ImageArena im, int tile_major, int map) {
     extern __shared__ uint32_t hist[];  // [B][kStripBuckets]
-    __shared__ uint32_t cur[kStripBuckets];
+    __shared__ uint32_t cur[8 * kStripBuckets];
     __shared__ uint32_t before[kStripBuckets];
     const int b = blockIdx.x;
+    if (map == 2) {  // offsets from k_strip_qscan
+        for (int i = threadIdx.x; i < 8 * kStripBuckets; i += 1024)
+            cur[i] = im.strip_hist[(int64_t)b * 8 * kStripBuckets + i];
+        __syncthreads();
+        for (int t = threadIdx.x; t < d.T; t += 1024) {
+            const int64_t tg = (int64_t)b * d.T + t;
+            if (!im.tile_count[tg]) continue;
+            const uint32_t pos =
+                atomicAdd(&cur[tile_queue(t, d.gx) * kStripBuckets + strip_bucket(tile_strip_max(im, tg))], 1u);
+#pragma unroll
+            for (int s = 0; s < kStrips; s++) im.strip_list[kStrips * pos + s] = ((uint32_t)tg << 2) | (uint32_t)s;
+        }
+        return;
+    }
     for (int i = threadIdx.x; i < d.B * kStripBuckets; i += 1024) hist[i] = im.strip_hist[i];
     __syncthreads();
     for (int bk = threadIdx.x; bk < kStripBuckets; bk += 1024) {  // bucket totals; this frame's share before it
@@ -957,19 +1013,24 @@ __global__ __launch_bounds__(1024) void k_strip_place(Dims d, ImageArena im, int
 
 void launch_strip_order(const Dims& d, const GeomArena& g, const ImageArena& im, const BinArena& b,
                         hipStream_t s) {
-    (void)g;
     if (d.B == 0 || d.T == 0) return;
     const int nt = d.B * d.T;
     hipLaunchKernelGGL(k_strip_count, dim3((nt + 3) / 4), dim3(256), 0, s, d, im, b);
     const int tile_major = strip_order_tile_major();
-    hipLaunchKernelGGL(k_strip_hist, dim3(d.B), dim3(1024), 0, s, d, im, tile_major);
+    const int map = tile_major ? xcd_queue_map() : 0;
+    hipLaunchKernelGGL(k_strip_hist, dim3(d.B), dim3(1024), 0, s, d, im, tile_major, map);
+    if (map == 2) {
+        hipLaunchKernelGGL(k_strip_qscan, dim3(1), dim3(1024), 0, s, d, im, g.ctrl);
+        hipLaunchKernelGGL(k_strip_place, dim3(d.B), dim3(1024), 0, s, d, im, tile_major, map);
+        return;
+    }
     const size_t lds = (size_t)d.B * kStripBuckets * 4;
     static size_t attr = 0;
     if (lds > 65536 && attr < lds) {
         attr = lds;
         hipFuncSetAttribute((const void*)k_strip_place, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     }
-    hipLaunchKernelGGL(k_strip_place, dim3(d.B), dim3(1024), lds, s, d, im, tile_major);
+    hipLaunchKernelGGL(k_strip_place, dim3(d.B), dim3(1024), lds, s, d, im, tile_major, map);
 }
 
 }  // namespace gsr

@@ -90,7 +90,12 @@ namespace gsr {
 static void env_tuning(Inputs& in) {
     static const uint32_t prio = [] { const char* e = getenv("GSR_PRIO_ITEMS"); return e ? (uint32_t)atoi(e) : 0u; }();
     in.prio_items = prio;
-    in.xcd_map = (uint32_t)strip_order_tile_major();
+    in.xcd_map = strip_order_tile_major() ? (uint32_t)xcd_queue_map() : 0u;
+}
+
+int xcd_queue_map() {
+    static const int v = [] { const char* e = getenv("GSR_XCD_MAP"); return (e && e[0] == '1') ? 1 : 2; }();
+    return v;
 }
 
 int strip_order_tile_major() {
@@ -151,7 +156,7 @@ size_t carve_image(char* base, const Dims& d, ImageArena* im) {
     a.lpt_hist = take<uint32_t>(base, off, (size_t)d.B * kLptBuckets);
     a.strip_cnt = take<uint32_t>(base, off, (size_t)kStrips * nt);
     a.strip_list = take<uint32_t>(base, off, (size_t)kStrips * nt);
-    a.strip_hist = take<uint32_t>(base, off, (size_t)d.B * kStripBuckets);
+    a.strip_hist = take<uint32_t>(base, off, (size_t)d.B * 8 * kStripBuckets);
     if (im) *im = a;
     return align_up(off) + 256;
 }

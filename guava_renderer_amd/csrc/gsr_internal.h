@@ -43,6 +43,8 @@ enum Ctrl : int {
     kCtrlRenderHead = 4, // render worklist dequeue counter
     kCtrlBwdHead = 5,    // render-backward worklist dequeue counter
     kCtrlNonEmpty = 6,   // tiles of the batch with a non-empty list
+    kCtrlQStart = 16,    // queue map 2: first strip_list tile of each XCD queue (8 words), then
+                         // the queue's tile count (8 words)
     kCtrlXcdQueue = 1024,  // 8 per-XCD render dequeue counters, 4 KiB apart
     kCtrlXcdStride = 1024,
     kCtrlWords = 9216
@@ -104,7 +106,8 @@ struct ImageArena {
     uint32_t* lpt_hist;   // per frame: tiles per work-list bucket
     uint32_t* strip_cnt;  // per tile x 4 strips: list entries whose strip bit is set
     uint32_t* strip_list; // the strips of the non-empty tiles, most survivors first: tile << 2 | strip
-    uint32_t* strip_hist; // per frame: strips per kStripBuckets bucket
+    uint32_t* strip_hist; // per frame: strips per kStripBuckets bucket (map 2: per XCD queue x bucket,
+                          // then rewritten in place as list offsets)
 };
 
 struct BinArena {
@@ -218,19 +221,37 @@ int persistent_grid(int per_cu);
 // GSR_STRIP_ORDER: "strip" orders the render work by each strip's survivors; "tile" (default) by
 // tile (its longest strip), the 4 strips consecutive and dealt to one XCD queue (L2 reuse).
 int strip_order_tile_major();
+// GSR_XCD_MAP: the render work-queue map (queue_item) -- 1 tile-affine, 2 block-affine (default)
+int xcd_queue_map();
+// map 2: the XCD queue of tile t -- 4x4-tile blocks (64x64 pixels) dealt over the eight queues,
+// shifted by 3 per block row, so every queue holds a spread of blocks (balanced) and neighbouring
+// tiles, which share Gaussians, read them through one L2
+__host__ __device__ __forceinline__ uint32_t tile_queue(int t, int gx) {
+    const int tx = t % gx, ty = t / gx;
+    return (uint32_t)((tx >> 2) + 3 * (ty >> 2)) & 7u;
+}
 
 // Render work items (render_fwd / render_bwd): the 4 strips of each of the ne non-empty tiles in
 // strip_list order (items [0, 4 ne)), then nempty whole empty tiles (items [4 ne, 4 ne + nempty)).
 // Eight per-XCD queues; the k-th dequeue of queue q returns:
 //  * map 0: item q + 8k;
 //  * map 1 (tile-affine): queue q owns list tiles q, q+8, q+16, ... with their 4 strips consecutive,
-//    then the empty tiles e = q (mod 8): a tile's strips read the same Gaussians from one L2.
+//    then the empty tiles e = q (mod 8): a tile's strips read the same Gaussians from one L2;
+//  * map 2 (block-affine): queue q owns its segment of the strip list (the tiles of its blocks,
+//    tile_queue, most survivors first; bounds in ctrl[kCtrlQStart..]), 4 strips per tile
+//    consecutive, then the empty tiles e = q (mod 8).
 // 0xFFFFFFFF when queue q is drained.
 __device__ __forceinline__ uint32_t queue_item(uint32_t q, uint32_t k, uint32_t ne, uint32_t nempty,
-                                               uint32_t map) {
+                                               uint32_t map, const uint32_t* ctrl) {
     if (map == 0) {
         const uint32_t item = q + 8u * k;
         return item < 4u * ne + nempty ? item : 0xFFFFFFFFu;
+    }
+    if (map == 2) {
+        const uint32_t nq = ctrl[kCtrlQStart + 8 + q];
+        if (k < 4u * nq) return 4u * (ctrl[kCtrlQStart + q] + (k >> 2)) + (k & 3u);
+        const uint32_t e = q + 8u * (k - 4u * nq);
+        return e < nempty ? 4u * ne + e : 0xFFFFFFFFu;
     }
     const uint32_t ntq = ne > q ? (ne - q + 7u) >> 3 : 0u;  // tiles owned by queue q
     if (k < 4u * ntq) return 4u * (q + 8u * (k >> 2)) + (k & 3u);
@@ -239,7 +260,7 @@ __device__ __forceinline__ uint32_t queue_item(uint32_t q, uint32_t k, uint32_t 
 }
 
 // The same mapping with every strip split into two work items (half-strip render waves): 8 items
-// per non-empty tile, then the empty tiles.
+// per non-empty tile, then the empty tiles (map 2 lists are walked as map 1: every item once).
 __device__ __forceinline__ uint32_t queue_item_half(uint32_t q, uint32_t k, uint32_t ne, uint32_t nempty,
                                                     uint32_t map) {
     if (map == 0) {

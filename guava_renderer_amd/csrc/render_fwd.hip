@@ -310,7 +310,7 @@ __device__ __forceinline__ void render_fwd_body(const Dims& d, const Inputs& in,
             if (lane == 0) k = atomicAdd(&g.ctrl[kCtrlXcdQueue + kCtrlXcdStride * q], 1u);
             k = __builtin_amdgcn_readfirstlane(k);
             item = HALF ? queue_item_half(q, k, ne, nitems - nstrip, in.xcd_map)
-                        : queue_item(q, k, ne, nitems - nstrip, in.xcd_map);
+                        : queue_item(q, k, ne, nitems - nstrip, in.xcd_map, g.ctrl);
             if (item != 0xFFFFFFFFu) break;
             q = (q + 1) & 7u;
             q_left--;
