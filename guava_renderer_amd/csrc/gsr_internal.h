@@ -226,9 +226,12 @@ int xcd_queue_map();
 // map 2: the XCD queue of tile t -- 4x4-tile blocks (64x64 pixels) dealt over the eight queues,
 // shifted by 3 per block row, so every queue holds a spread of blocks (balanced) and neighbouring
 // tiles, which share Gaussians, read them through one L2
+#ifndef GSR_XCD_BLOCK_SHIFT
+#define GSR_XCD_BLOCK_SHIFT 2  // log2 of the block side in tiles
+#endif
 __host__ __device__ __forceinline__ uint32_t tile_queue(int t, int gx) {
     const int tx = t % gx, ty = t / gx;
-    return (uint32_t)((tx >> 2) + 3 * (ty >> 2)) & 7u;
+    return (uint32_t)((tx >> GSR_XCD_BLOCK_SHIFT) + 3 * (ty >> GSR_XCD_BLOCK_SHIFT)) & 7u;
 }
 
 // Render work items (render_fwd / render_bwd): the 4 strips of each of the ne non-empty tiles in

@@ -93,8 +93,9 @@ __global__ __launch_bounds__(GSR_TILE_PIX) __attribute__((amdgpu_waves_per_eu(2)
             uint32_t k = 0;
             if (lane == 0) k = atomicAdd(&g.ctrl[kCtrlXcdQueue + kCtrlXcdStride * q + kBwdQueueOffset], 1u);
             k = __builtin_amdgcn_readfirstlane(k);
-            // (the block-affine map measured +2% here: the backward walks the list tile-affine)
-            item = queue_item(q, k, ne, 0u, in.xcd_map == 2u ? 1u : in.xcd_map, g.ctrl);
+            // (map 2's list is longest-first per queue segment only: walked round-robin, the long
+            // strips of the last segments would start last)
+            item = queue_item(q, k, ne, 0u, in.xcd_map, g.ctrl);
             if (item != 0xFFFFFFFFu) break;
             q = (q + 1) & 7u;
             q_left--;
