@@ -1017,7 +1017,8 @@ void launch_strip_order(const Dims& d, const GeomArena& g, const ImageArena& im,
     const int nt = d.B * d.T;
     hipLaunchKernelGGL(k_strip_count, dim3((nt + 3) / 4), dim3(256), 0, s, d, im, b);
     const int tile_major = strip_order_tile_major();
-    const int map = tile_major ? xcd_queue_map() : 0;
+    // (one frame: the tile-affine walk of one longest-first list, measured 1.5% faster there)
+    const int map = tile_major ? (d.B == 1 ? 1 : xcd_queue_map()) : 0;
     hipLaunchKernelGGL(k_strip_hist, dim3(d.B), dim3(1024), 0, s, d, im, tile_major, map);
     if (map == 2) {
         hipLaunchKernelGGL(k_strip_qscan, dim3(1), dim3(1024), 0, s, d, im, g.ctrl);

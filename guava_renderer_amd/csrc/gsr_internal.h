@@ -263,12 +263,18 @@ __device__ __forceinline__ uint32_t queue_item(uint32_t q, uint32_t k, uint32_t 
 }
 
 // The same mapping with every strip split into two work items (half-strip render waves): 8 items
-// per non-empty tile, then the empty tiles (map 2 lists are walked as map 1: every item once).
+// per non-empty tile, then the empty tiles.
 __device__ __forceinline__ uint32_t queue_item_half(uint32_t q, uint32_t k, uint32_t ne, uint32_t nempty,
-                                                    uint32_t map) {
+                                                    uint32_t map, const uint32_t* ctrl) {
     if (map == 0) {
         const uint32_t item = q + 8u * k;
         return item < 8u * ne + nempty ? item : 0xFFFFFFFFu;
+    }
+    if (map == 2) {
+        const uint32_t nq = ctrl[kCtrlQStart + 8 + q];
+        if (k < 8u * nq) return 8u * (ctrl[kCtrlQStart + q] + (k >> 3)) + (k & 7u);
+        const uint32_t e = q + 8u * (k - 8u * nq);
+        return e < nempty ? 8u * ne + e : 0xFFFFFFFFu;
     }
     const uint32_t ntq = ne > q ? (ne - q + 7u) >> 3 : 0u;
     if (k < 8u * ntq) return 8u * (q + 8u * (k >> 3)) + (k & 7u);

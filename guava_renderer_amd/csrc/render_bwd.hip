@@ -479,8 +479,10 @@ __global__ void k_zero_bwd_queues(uint32_t* ctrl) {
     if (threadIdx.x < 8) ctrl[kCtrlXcdQueue + kCtrlXcdStride * threadIdx.x + kBwdQueueOffset] = 0u;
 }
 
-void launch_render_bwd(const Dims& d, const Inputs& in, const GeomArena& g, const ImageArena& im,
+void launch_render_bwd(const Dims& d, const Inputs& in_, const GeomArena& g, const ImageArena& im,
                        const BinArena& b, const Grads& gr, bool exact, bool split, hipStream_t s) {
+    Inputs in = in_;  // one frame: strip_list is one longest-first list (launch_strip_order)
+    if (d.B == 1 && in.xcd_map == 2u) in.xcd_map = 1u;
     const int nwaves = d.B * d.T * kStrips;  // upper bound of the work items
     if (nwaves == 0) return;
     hipLaunchKernelGGL(k_zero_bwd_queues, dim3(1), dim3(64), 0, s, g.ctrl);

@@ -309,7 +309,7 @@ __device__ __forceinline__ void render_fwd_body(const Dims& d, const Inputs& in,
             uint32_t k = 0;
             if (lane == 0) k = atomicAdd(&g.ctrl[kCtrlXcdQueue + kCtrlXcdStride * q], 1u);
             k = __builtin_amdgcn_readfirstlane(k);
-            item = HALF ? queue_item_half(q, k, ne, nitems - nstrip, in.xcd_map)
+            item = HALF ? queue_item_half(q, k, ne, nitems - nstrip, in.xcd_map, g.ctrl)
                         : queue_item(q, k, ne, nitems - nstrip, in.xcd_map, g.ctrl);
             if (item != 0xFFFFFFFFu) break;
             q = (q + 1) & 7u;
@@ -687,8 +687,10 @@ __global__ __launch_bounds__(GSR_TILE_PIX) __attribute__((amdgpu_waves_per_eu(4)
     render_fwd_body<EXACT, false, false, true>(d, in, g, im, bn, o);
 }
 
-void launch_render_fwd(const Dims& d, const Inputs& in, const GeomArena& g, const ImageArena& im,
+void launch_render_fwd(const Dims& d, const Inputs& in_, const GeomArena& g, const ImageArena& im,
                        const BinArena& b, const Outputs& o, bool exact, bool split, hipStream_t s) {
+    Inputs in = in_;  // one frame: strip_list is one longest-first list (launch_strip_order)
+    if (d.B == 1 && in.xcd_map == 2u) in.xcd_map = 1u;
     static const int ablate = [] { const char* e = getenv("GSR_RENDER_ABLATE"); return e ? atoi(e) : 0; }();
     const int nwaves = d.B * d.T * kStrips;  // upper bound of the work items
     if (nwaves == 0) return;

@@ -46,7 +46,7 @@ def image_layout(W, H):
     return _carve([("final_T", np.float32, W * H), ("n_contrib", np.uint32, W * H),
                    ("ranges", np.uint32, 2 * T), ("tile_count", np.uint32, T), ("work_list", np.uint32, T),
                    ("lpt_hist", np.uint32, 34), ("strip_cnt", np.uint32, 4 * T),
-                   ("strip_list", np.uint32, 4 * T), ("strip_hist", np.uint32, 129)])
+                   ("strip_list", np.uint32, 4 * T), ("strip_hist", np.uint32, 8 * 129)])
 
 
 def bin_layout(R):

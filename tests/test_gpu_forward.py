@@ -5,8 +5,6 @@ means2D, depth, conic/opacity, the sorted per-tile lists and ranges, n_contrib, 
 feature channels and the inverse depth.  Fast-exp mode (hardware v_exp_f32): integers exact,
 colours within 1e-4 L_inf except on the rare pixels where an alpha threshold flips.
 """
-import os
-
 import numpy as np
 import pytest
 
@@ -142,9 +140,8 @@ def test_render_counters_match_oracle(kind, P, W, H):
 def test_strip_work_list():
     """k_strip_count / k_strip_place: survivors per 64-pixel strip equal the popcount of that strip's
     bit over the tile's list, and the strip work list holds every strip of every non-empty tile
-    exactly once, tile-major (GSR_STRIP_ORDER default): a tile's 4 strips consecutive, grouped by
-    XCD queue, and inside a queue's segment tiles in non-increasing order of their longest strip up
-    to the 4-buckets-per-octave granularity."""
+    exactly once, tile-major (GSR_STRIP_ORDER default): a tile's 4 strips consecutive, tiles in
+    non-increasing order of their longest strip up to the 4-buckets-per-octave granularity."""
     _lib().set_exact_exp(True)
     d = make_scene("avatar", 20000, 200, 136, seed=3)
     _, _, _, gs = gpu_forward(d)
@@ -167,16 +164,10 @@ def test_strip_work_list():
         return 127 - (4 * e + sub)
     groups = lst.reshape(-1, 4)
     assert (groups >> 2 == (groups[:, :1] >> 2)).all() and ((groups & 3) == np.arange(4)).all()
-    # block-affine queue map (GSR_XCD_MAP default 2): the list is one segment per XCD queue in queue
-    # order (4x4-tile blocks dealt as tile_queue in gsr_internal.h), longest-first inside a segment
-    gx = (d["image_width"] + 15) // 16
-    tiles = groups[:, 0] >> 2  # (one frame: tile index == global tile)
-    q = (((tiles % gx) >> 2) + 3 * ((tiles // gx) >> 2)) & 7
-    if os.environ.get("GSR_XCD_MAP", "2")[:1] == "1":  # tile-affine map: one longest-first list
-        q = np.zeros_like(q)
-    assert all(q[i] <= q[i + 1] for i in range(len(q) - 1))
+    # one frame: one longest-first list (batches of 2+ frames use per-XCD segments, each
+    # longest-first: queue_item map 2; every batch test's bit-exact frames cover that walk)
     b = [bucket(int(cnt[x >> 2].max())) for x in groups[:, 0]]
-    assert all(b[i] <= b[i + 1] for i in range(len(b) - 1) if q[i] == q[i + 1])
+    assert all(b[i] <= b[i + 1] for i in range(len(b) - 1))
 
 
 def test_refine_epilogue_matches_conv():

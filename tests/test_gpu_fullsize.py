@@ -121,3 +121,20 @@ def test_full_batch_invariants():
         final_T = decode(ib.cpu().numpy(), image_layout(512, 512))["final_T"].reshape(512, 512)
         assert (final_T >= 0).all() and (final_T <= 1).all()
         np.testing.assert_allclose(acc[k], 1.0 - final_T, atol=2e-5)
+
+
+def test_block_affine_queue_segments():
+    """Batches (B >= 2) deal the strips over the eight per-XCD queues by 4x4-tile block
+    (queue_item map 2): the control words hold each queue's segment of the strip list, and the
+    segments tile the non-empty tiles exactly (start = exclusive sum of the counts); the frames
+    themselves are pinned bit-exactly by the other batch tests."""
+    from guava_renderer_amd import scenes
+    sc = scenes.avatar_cloud(20000, seed=3)
+    cams = scenes.frame_cameras(3, 256, 256, seed=1000)
+    r, _, _, _ = _batch_render(sc, cams)
+    ctrl = r.workspace[:4 * 64].view(torch.int32).cpu().numpy()
+    ne, qstart, qcount = int(ctrl[6]), ctrl[16:24], ctrl[24:32]
+    assert ne > 0 and int(qcount.sum()) == ne
+    np.testing.assert_array_equal(qstart, np.concatenate([[0], np.cumsum(qcount)[:-1]]))
+    assert (qcount > 0).sum() >= 4  # the blocks spread over the queues
+
