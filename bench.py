@@ -418,13 +418,18 @@ def main():
     bytes_launch = _render_alg_bytes(P_vis / B, W, H) * frames_per_launch
     achieved = bytes_launch / (render_ms * 1e-3) / 1e9 if render_ms > 0 else None
     traffic = issue = None
-    pmc_path = os.path.join(ROOT, "profiles", "pmc_render_fwd.json")
+    # HBM traffic per launch from the committed PMC summaries (tools/pmc_summary.py): the contract
+    # workload's (pmc_render_fwd.json) and the training batch's (pmc_train.json: render_fwd and
+    # render_bwd of `--pipeline train --batch 6`)
+    pmc_path = os.path.join(ROOT, "profiles", "pmc_train.json" if a.pipeline == "train" else "pmc_render_fwd.json")
+    bwd_traffic = None
     if os.path.exists(pmc_path):
         try:
             pm = json.load(open(pmc_path))
             if pm.get("config") == workload and pm.get("batch") == B:
                 traffic = pm.get("hbm_bytes_per_launch")
                 issue = pm.get("render_fwd_issue")
+                bwd_traffic = (pm.get("kernels", {}).get("k_render_bwd") or {}).get("hbm_bytes")
         except Exception:  # noqa: BLE001
             traffic = None
 
@@ -498,7 +503,7 @@ def main():
         out["roofline_bwd"] = {"bound": "hbm", "kernel": "render_bwd",
                                "achieved": round(bwd_ach, 1) if bwd_ach else None, "peak": HBM_PEAK_GBS,
                                "unit": "GB/s", "frac": round(bwd_ach / HBM_PEAK_GBS, 4) if bwd_ach else None,
-                               "traffic": None, "alg_bytes_per_launch": bwd_bytes,
+                               "traffic": bwd_traffic, "alg_bytes_per_launch": bwd_bytes,
                                "avg_launch_ms": round(bwd_ms, 4), "us_per_frame": round(1000 * bwd_ms / B, 2)}
     if a.pipeline == "frame":
         out["latency_ms_per_frame"] = round(1000.0 * el / (a.steps * B), 4)
