@@ -1011,6 +1011,20 @@ __global__ __launch_bounds__(1024) void k_strip_place(Dims d, ImageArena im, int
     }
 }
 
+void launch_strip_list_tile(const Dims& d, const ImageArena& im, uint32_t* out, hipStream_t s) {
+    if (d.B == 0 || d.T == 0) return;
+    ImageArena i2 = im;
+    i2.strip_list = out;
+    hipLaunchKernelGGL(k_strip_hist, dim3(d.B), dim3(1024), 0, s, d, i2, 1, 1);
+    const size_t lds = (size_t)d.B * kStripBuckets * 4;
+    static size_t attr = 0;
+    if (lds > 65536 && attr < lds) {
+        attr = lds;
+        hipFuncSetAttribute((const void*)k_strip_place, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    }
+    hipLaunchKernelGGL(k_strip_place, dim3(d.B), dim3(1024), lds, s, d, i2, 1, 1);
+}
+
 void launch_strip_order(const Dims& d, const GeomArena& g, const ImageArena& im, const BinArena& b,
                         hipStream_t s) {
     if (d.B == 0 || d.T == 0) return;

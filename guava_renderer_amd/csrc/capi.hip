@@ -157,6 +157,7 @@ size_t carve_image(char* base, const Dims& d, ImageArena* im) {
     a.strip_cnt = take<uint32_t>(base, off, (size_t)kStrips * nt);
     a.strip_list = take<uint32_t>(base, off, (size_t)kStrips * nt);
     a.strip_hist = take<uint32_t>(base, off, (size_t)d.B * 8 * kStripBuckets);
+    a.strip_list_bwd = take<uint32_t>(base, off, (size_t)kStrips * nt);
     if (im) *im = a;
     return align_up(off) + 256;
 }

@@ -108,6 +108,7 @@ struct ImageArena {
     uint32_t* strip_list; // the strips of the non-empty tiles, most survivors first: tile << 2 | strip
     uint32_t* strip_hist; // per frame: strips per kStripBuckets bucket (map 2: per XCD queue x bucket,
                           // then rewritten in place as list offsets)
+    uint32_t* strip_list_bwd;  // the backward's list: one longest-first list, tile-major (map 1)
 };
 
 struct BinArena {
@@ -295,6 +296,8 @@ void launch_tile_scan(const Dims& d, const GeomArena& g, const ImageArena& im, h
 // survivors per strip -> strip_cnt; strips of the non-empty tiles, most survivors first -> strip_list
 void launch_strip_order(const Dims& d, const GeomArena& g, const ImageArena& im, const BinArena& b,
                         hipStream_t s);
+// the strip list of queue map 1 (one longest-first list, tile-major) into `out` (render_bwd)
+void launch_strip_list_tile(const Dims& d, const ImageArena& im, uint32_t* out, hipStream_t s);
 void launch_ordered_scatter(const Dims& d, const GeomArena& g, const ImageArena& im,
                             const BinArena& b, hipStream_t s);
 void launch_render_fwd(const Dims& d, const Inputs& in, const GeomArena& g, const ImageArena& im,

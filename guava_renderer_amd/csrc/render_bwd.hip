@@ -93,8 +93,6 @@ __global__ __launch_bounds__(GSR_TILE_PIX) __attribute__((amdgpu_waves_per_eu(2)
             uint32_t k = 0;
             if (lane == 0) k = atomicAdd(&g.ctrl[kCtrlXcdQueue + kCtrlXcdStride * q + kBwdQueueOffset], 1u);
             k = __builtin_amdgcn_readfirstlane(k);
-            // (map 2's list is longest-first per queue segment only: walked round-robin, the long
-            // strips of the last segments would start last)
             item = queue_item(q, k, ne, 0u, in.xcd_map, g.ctrl);
             if (item != 0xFFFFFFFFu) break;
             q = (q + 1) & 7u;
@@ -479,10 +477,20 @@ __global__ void k_zero_bwd_queues(uint32_t* ctrl) {
     if (threadIdx.x < 8) ctrl[kCtrlXcdQueue + kCtrlXcdStride * threadIdx.x + kBwdQueueOffset] = 0u;
 }
 
-void launch_render_bwd(const Dims& d, const Inputs& in_, const GeomArena& g, const ImageArena& im,
+void launch_render_bwd(const Dims& d, const Inputs& in_, const GeomArena& g, const ImageArena& im_,
                        const BinArena& b, const Grads& gr, bool exact, bool split, hipStream_t s) {
     Inputs in = in_;  // one frame: strip_list is one longest-first list (launch_strip_order)
     if (d.B == 1 && in.xcd_map == 2u) in.xcd_map = 1u;
+    // The forward's block-affine segments cost the backward 8%: it walks a tile-affine list of its
+    // own (one longest-first list, built here from the forward's strip counts, ~10 us);
+    // GSR_BWD_TILE_LIST=0 walks the forward's segments
+    static const bool own_list = [] { const char* e = getenv("GSR_BWD_TILE_LIST"); return !(e && e[0] == '0'); }();
+    ImageArena im = im_;
+    if (in.xcd_map == 2u && own_list) {
+        launch_strip_list_tile(d, im_, im_.strip_list_bwd, s);
+        im.strip_list = im_.strip_list_bwd;
+        in.xcd_map = 1u;
+    }
     const int nwaves = d.B * d.T * kStrips;  // upper bound of the work items
     if (nwaves == 0) return;
     hipLaunchKernelGGL(k_zero_bwd_queues, dim3(1), dim3(64), 0, s, g.ctrl);
