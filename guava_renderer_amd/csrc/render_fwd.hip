@@ -43,6 +43,9 @@ namespace gsr {
 #ifndef GSR_SPLIT_FIRST
 #define GSR_SPLIT_FIRST 1  // split-bf16: split both weights before the lane-half swap (two swaps, no copies)
 #endif
+#ifndef GSR_SKIP_DEAD
+#define GSR_SKIP_DEAD 0  // 1: skip the blend + MFMAs of a k-step no live pixel takes (measured +2%: off)
+#endif
 #ifndef GSR_BATCH_NSLOT
 #define GSR_BATCH_NSLOT 3  // pipeline slots of the batched (throughput) kernels
 #endif
@@ -499,7 +502,9 @@ __device__ __forceinline__ void render_fwd_body(const Dims& d, const Inputs& in,
             } else {                                                                                \
                 acc0 = __builtin_amdgcn_mfma_f32_32x32x2f32(S##f, w_, acc0, 0, 0, 0);               \
             }                                                                                       \
-        } else {                                                                                    \
+        } else if (!GSR_SKIP_DEAD || STATS || TL ||  /* a k-step no live pixel takes: skipped (exact) */ \
+                   __builtin_amdgcn_ballot_w64(!done && (!(S##al < 1.0f / 255.0f) ||                \
+                                                         !(S##bl < 1.0f / 255.0f))) != 0ull) {       \
             const float f_ = S##f;                                                                  \
             const bool was_done_ = done;                                                            \
             const float wa_ = take_step(S##al, S##ai, (uint32_t)S##pa, T, invd, last, done);        \
