@@ -1,26 +1,47 @@
 #!/usr/bin/env python
 """Headline benchmark: rendered frames/sec at 512x512 with ~100k Gaussians (BASELINE.json).
 
-One step = one pass of GUAVA's per-frame animation path over a batch of `--batch` tracked frames
+One step = one pass of GUAVA's per-frame animation path over a batch of tracked frames
 (config 2 "self-reenactment": main/test.py:70-76 times Ubody_Gaussian.forward + render per frame):
   --pipeline avatar (default): EHM deformation (FLAME head LBS + SMPL-X body LBS, per-frame pose,
       expression, eyelids), vertex + UV Gaussian assembly, then the rasterizer hot path
       (preprocess -> tile binning -> per-tile depth order -> 32-channel compositing);
-  --pipeline raster: the rasterizer alone over one static cloud seen by a camera per frame.
+      --config c5: 300k Gaussians (3 per UV texel), 1024x1024, cross-reenactment poses
+      (main/test.py:96-139: target poses with the source identity);
+  --pipeline raster: the rasterizer alone over one static cloud seen by a camera per frame;
+  --pipeline train: BASELINE config 4 (raster fwd + fused-SSIM/L1 loss + raster bwd + Adam);
+  --pipeline frame: GUAVA's unchanged caller, GaussianRasterizer_32 once per frame.
 Synthetic avatar: P=100,000 Gaussians (10,475 SMPL-X vertex Gaussians + UV Gaussians), 512x512,
-one camera and one pose per frame; every input resident in HBM before the timed region.  N GPUs: one process per GPU, each renders its
-own `--batch` frames (frames are independent -> weak scaling, no collective in the data path;
-torch.distributed is used only for the barrier and the max-over-ranks time).
+one camera and one pose per frame; every input resident in HBM before the timed region.
+
+Numerics: the headline is the bit-exact f32 path (colour accumulation on f32 MFMAs, identical to
+the CPU oracle); --split-bf16 measures the tolerance mode instead (the line then carries the f32
+number under `exact_accum`); by default the split-bf16 number is an extra key (`split_bf16`).
+
+N GPUs: one process per GPU.  `--gpus N` starts the N ranks itself (torch.distributed.run, before
+anything touches the GPU) unless it already runs under a launcher (WORLD_SIZE set, which must
+equal N).  Frames are sharded over ranks: by default each rank renders its own `--batch` frames
+("scaling": "weak"); `--global-batch G` splits G frames over the ranks instead ("strong"; config 3
+is G=32 over 8 GPUs).  Every step ends with the consumer exchange: the rendered frames are encoded
+as GUAVA's 8-bit RGB (to8b, main/test.py:85) and all-gathered over RCCL/xGMI to every rank,
+overlapped with the next step's rendering (the timed region ends after the last exchange).  The
+line's time is the max over ranks.
 
 Prints ONE JSON line (rank 0) with the contract fields plus:
-  roofline      -- render_fwd kernel: algorithmic bytes per launch / average launch time from HIP
-                   events recorded on the launch stream inside the timed region;
-  cpu_baseline  -- the CPU oracle (a port of the reference algorithm) timed on a bounded sample of
-                   the same workload on this host's cores (rank 0, N=1 only).
+  roofline        -- render_fwd kernel: algorithmic bytes per launch / average launch time from HIP
+                     events recorded on the launch stream inside the timed region; `traffic` from the
+                     committed PMC summary only when it was measured on this build (source hash);
+  cpu_baseline    -- the CPU oracle (a port of the reference algorithm) timed on a bounded sample of
+                     the same workload on this host's cores (rank 0, N=1 only);
+  per_frame_dropin-- GUAVA's own fps definition (main/test.py:70-76,90): deform + one
+                     GaussianRasterizer_32 call per frame, B=1 (N=1 only);
+  config3_strong  -- at N>1: config 3 itself, 32 frames per step split over the N ranks.
 """
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -40,27 +61,52 @@ def _args():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=400)
     ap.add_argument("--warmup", type=int, default=20)
-    ap.add_argument("--batch", type=int, default=32, help="frames per step per GPU")
+    ap.add_argument("--batch", type=int, default=None,
+                    help="frames per step per GPU (weak scaling; default 32, 6 for --pipeline train)")
+    ap.add_argument("--global-batch", type=int, default=None,
+                    help="frames per step over ALL ranks (strong scaling; config 3 = 32 over 8 GPUs)")
     ap.add_argument("--config", default="c2", choices=["c2", "c5"])
     ap.add_argument("--pipeline", default="avatar", choices=["avatar", "raster", "train", "frame"],
                     help="train = BASELINE config 4: raster fwd + fused-SSIM/L1 loss + raster bwd + "
-                         "gradient all-reduce + Adam (use --batch 6); frame = GUAVA's unchanged caller: "
+                         "gradient all-reduce + Adam; frame = GUAVA's unchanged caller: "
                          "one GaussianRasterizer_32 call per frame as gaussian_render.py:37-67 does")
     ap.add_argument("--inflight", type=int, default=1,
-                    help="batches in flight on separate HIP streams (avatar/raster pipelines): the deform "
-                         "and binning of one batch overlap the compositing of the others (3: +4%% frames/s "
-                         "over 1); kernel times for the roofline then come from an isolated pass")
+                    help="batches in flight on separate HIP streams (avatar/raster pipelines); kernel "
+                         "times for the roofline then come from an isolated pass")
     ap.add_argument("--refine", action="store_true",
                     help="fuse the refiner's first 1x1 conv 32->16 + leaky ReLU into the render "
                          "epilogue (inference output: 16 refiner features + 4 raw channels)")
     ap.add_argument("--fast-exp", action="store_true", help="hardware exp (not bit-exact)")
-    ap.add_argument("--exact-accum", action="store_true",
-                    help="f32 MFMA colour accumulation, bit-identical to the oracle (default: split-bf16 "
-                         "MFMA accumulation, colour within the north_star's 1e-4 L_inf, include/gsr.h)")
+    ap.add_argument("--split-bf16", action="store_true",
+                    help="headline in the split-bf16 colour-accumulation mode (tolerance, include/gsr.h)")
+    ap.add_argument("--gather", default="u8", choices=["u8", "f32", "none"],
+                    help="N>1 consumer exchange: 8-bit RGB (to8b, default), f32 RGB, or none")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-extras", action="store_true",
+                    help="only the contract measurement (no split-bf16 / per-frame / config-3 extras)")
     ap.add_argument("--stages", action="store_true", help="also time every stage (extra events)")
-    return ap.parse_args()
+    a = ap.parse_args()
+    if a.batch is None:
+        a.batch = 6 if a.pipeline == "train" else 32
+    return a
+
+
+def _free_port():
+    s = socket.socket(socket.AF_INET, socket.SOCK_STREAM)
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def _launch_ranks(n):
+    """`bench.py --gpus N` without a launcher: start N ranks (one process per GPU) under
+    torch.distributed.run as a CHILD process -- nothing here has touched the GPU -- and exit with
+    its status.  Rank 0's JSON line reaches stdout through the child."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr=127.0.0.1", f"--master-port={_free_port()}", os.path.abspath(__file__)] + sys.argv[1:]
+    return subprocess.run(cmd).returncode
 
 
 def _workload(cfg):
@@ -136,10 +182,216 @@ def cpu_baseline(scene, cams, W, H, budget_s, avatar_inputs=None):
                        f"({what}, OpenMP {threads} threads on {model}) in {el:.1f}s")
 
 
+class Workload:
+    """The synthetic inputs and the per-step callable of one pipeline for B frames of this rank
+    (frames [lo, hi) of n_total), resident in HBM."""
+
+    def __init__(self, a, wl, B, lo, n_total, dev, numerics):
+        import torch
+        from guava_renderer_amd import scenes
+        from guava_renderer_amd.batch import BatchRasterizer
+        self.a, self.B, self.dev = a, B, dev
+        P, W, H = wl["P"], wl["W"], wl["H"]
+        self.W, self.H = W, H
+        cams_all = scenes.frame_cameras(n_total, W, H, seed=1000)
+        self.cams = cams = cams_all[lo:lo + B]
+        t = lambda x: torch.tensor(np.ascontiguousarray(x), device=dev)  # noqa: E731
+        self.t = t
+        views = t(np.stack([c["viewmatrix"].reshape(16) for c in cams]))
+        projs = t(np.stack([c["projmatrix"].reshape(16) for c in cams]))
+        tanf = t(np.array([[c["tanfovx"], c["tanfovy"]] for c in cams], np.float32))
+        self.views, self.projs, self.tanf = views, projs, tanf
+        bgs = torch.zeros((B, C), dtype=torch.float32, device=dev)
+        self.avatar_inputs = None
+        self.rasts = []
+        self.pipes = []
+        self.trainer = None
+        if a.pipeline in ("avatar", "frame"):
+            from guava_renderer_amd import avatar
+            from guava_renderer_amd.pipeline import AvatarPipeline
+            body, flame, extra = avatar.ehm_assets(seed=0)
+            verts, faces, tex = avatar.template_mesh()
+            g = avatar.gaussians(verts, faces, tex * wl["gpt"], P=P, seed=0)
+            bp_all, fp_all = avatar.ehm_params(n_total, seed=1000)
+            if a.config == "c5":  # cross-reenactment: target poses on the source identity
+                src_b, src_f = avatar.ehm_params(1, seed=77)
+                bp_all, fp_all = avatar.change_id_info(bp_all, fp_all, src_b, src_f)
+            bp = {k: v[lo:lo + B] for k, v in bp_all.items()}
+            fp = {k: v[lo:lo + B] for k, v in fp_all.items()}
+            self.bpt = {k: t(v) for k, v in bp.items()}
+            self.fpt = {k: t(v) for k, v in fp.items()}
+            self.avatar_assets = (body, flame, extra, g)
+            self.avatar_inputs = (body, flame, extra, g, bp, fp)
+            self.scene = {"colors": g["colors"], "opacities": g["opacities"]}
+            probe = AvatarPipeline(body, flame, extra, g, B, W, H, R_capacity=24 * P * B, device=dev)
+            self.P = probe.P
+            if a.pipeline == "avatar":
+                probe.render(self.bpt, self.fpt, views, projs, tanf)
+                R_probe, ovf = probe.rast.status()
+                assert not ovf, "probe overflow"
+                del probe
+                torch.cuda.empty_cache()
+                self.pipes = [AvatarPipeline(body, flame, extra, g, B, W, H, R_capacity=int(R_probe * 1.25) + 1024,
+                                             device=dev) for _ in range(max(1, a.inflight))]
+                for p in self.pipes:
+                    p.rast.numerics = numerics
+                self.rasts = [p.rast for p in self.pipes]
+                head = None
+                if a.refine:
+                    from guava_renderer_amd.batch import RefineHead
+                    rng = np.random.default_rng(5)  # random-init conv_body_first (nn.Conv2d(32, 16, 1))
+                    head = RefineHead(t(rng.uniform(-0.18, 0.18, (16, 32)).astype(np.float32)),
+                                      t(rng.uniform(-0.18, 0.18, 16).astype(np.float32)), keep_channels=4)
+                pipes = self.pipes
+                self.step_on = lambda i: pipes[i].render(self.bpt, self.fpt, views, projs, tanf, refine=head)
+            else:
+                self._frame_pipeline(probe, numerics)
+        elif a.pipeline == "train":
+            from guava_renderer_amd.train import SplatTrainer
+            scene = scenes.avatar_cloud(P, seed=0, gaussians_per_texel=wl["gpt"])
+            self.scene = scene
+            self.P = P = scene["means3D"].shape[0]
+            params = {k: t(scene[k]) for k in ("means3D", "colors", "opacities", "scales", "rotations")}
+            probe = BatchRasterizer(B, P, W, H, R_capacity=24 * P * B, device=dev)
+            probe.forward(params["means3D"], params["colors"], params["opacities"], params["scales"],
+                          params["rotations"], views, projs, tanf, bgs)
+            R_probe, ovf = probe.status()
+            assert not ovf, "probe overflow"
+            del probe
+            torch.cuda.empty_cache()
+            # the trainable parameters are the raw attributes (SURVEY.md 8(d) C4): a small learning
+            # rate keeps the per-step work at the avatar's distribution over the timed steps;
+            # capacity with headroom for the drift (an overflowing step is skipped on the device)
+            self.trainer = SplatTrainer(params, B, W, H, R_capacity=int(R_probe * 2) + 1024, device=dev, lr=1e-5,
+                                        numerics=numerics)
+            self.rasts = [self.trainer.rast]
+            target = torch.rand((B, 3, H, W), device=dev, generator=torch.Generator(device=dev).manual_seed(lo))
+            self.step_on = lambda i: self.trainer.step(views, projs, tanf, target)
+        else:
+            scene = scenes.avatar_cloud(P, seed=0, gaussians_per_texel=wl["gpt"])
+            self.scene = scene
+            self.P = P = scene["means3D"].shape[0]
+            means, colors = t(scene["means3D"]), t(scene["colors"])
+            opac, scales, rots = t(scene["opacities"]), t(scene["scales"]), t(scene["rotations"])
+            probe = BatchRasterizer(B, P, W, H, R_capacity=24 * P * B, device=dev)
+            probe.forward(means, colors, opac, scales, rots, views, projs, tanf, bgs)
+            R_probe, ovf = probe.status()
+            assert not ovf, "probe overflow"
+            del probe
+            torch.cuda.empty_cache()
+            self.rasts = [BatchRasterizer(B, P, W, H, R_capacity=int(R_probe * 1.25) + 1024, device=dev,
+                                          numerics=numerics) for _ in range(max(1, a.inflight))]
+            rasts = self.rasts
+            self.step_on = lambda i: rasts[i].forward(means, colors, opac, scales, rots, views, projs, tanf, bgs)
+        self.rast = self.rasts[0] if self.rasts else None
+
+    def _frame_pipeline(self, dpipe, numerics):
+        """GUAVA's unchanged caller (models/UbodyAvatar/gaussian_render.py:19-67, the refiner aside):
+        one GaussianRasterizationSettings + GaussianRasterizer_32 call per frame, camera fields read
+        per frame with int()/float() from device tensors, outputs stacked.  The deformed assets of
+        the B frames come from the deform kernels, outside the timed region."""
+        import torch
+        from diff_gaussian_rasterization_32 import GaussianRasterizationSettings, GaussianRasterizer_32
+        B, dev, H, W = self.B, self.dev, self.H, self.W
+        dg = dpipe.deform(self.bpt, self.fpt)
+        assets = {"xyz": dg["xyz"], "rotation": dg["rotation"], "scaling": dg["scaling"],
+                  "opacity": dpipe.gauss.opacity.unsqueeze(0).expand(B, -1, -1),
+                  "features_color": dpipe.gauss.colors.unsqueeze(0).expand(B, -1, -1)}
+        cam_params = _cam_params(self, B)
+        self.last_radii = [None]
+
+        def step_on(i):
+            with torch.no_grad():
+                out, radii, depths = _render_model(assets, cam_params, B, dev, GaussianRasterizationSettings,
+                                                   GaussianRasterizer_32)
+                self.last_radii[0] = radii
+                return out, depths, radii
+        self.step_on = step_on
+
+
+def _cam_params(w, B, lo=0):
+    """render_cam_params of B frames as GUAVA's data loader hands them to GaussianRenderer
+    (dataset/data_loader.py:232-251): device tensors, one row per frame."""
+    import torch
+    sl = slice(lo, lo + B)
+    return {"image_height": torch.full((B,), w.H, device=w.dev), "image_width": torch.full((B,), w.W, device=w.dev),
+            "tanfovx": w.tanf[sl, 0].contiguous(), "tanfovy": w.tanf[sl, 1].contiguous(),
+            "world_view_transform": w.views[sl].view(B, 4, 4), "full_proj_transform": w.projs[sl].view(B, 4, 4),
+            "camera_center": w.t(np.stack([c["campos"] for c in w.cams[sl]]))}
+
+
+def _render_model(assets, cam_params, B, dev, Settings, Rasterizer):
+    """GaussianRenderer.forward's rasterizer loop (gaussian_render.py:19-67) as GUAVA runs it."""
+    import torch
+    mean_3d = assets["xyz"]
+    features_color = assets["features_color"].clone()
+    mean_2d = torch.zeros_like(mean_3d, dtype=torch.float32, requires_grad=True, device=dev)
+    bg = torch.ones((B, features_color.shape[-1]), dtype=torch.float32, device=dev) * 0.0
+    imgs, radiis, depths = [], [], []
+    for bi in range(B):
+        rs = Settings(
+            image_height=int(cam_params["image_height"][bi]), image_width=int(cam_params["image_width"][bi]),
+            tanfovx=float(cam_params["tanfovx"][bi]), tanfovy=float(cam_params["tanfovy"][bi]),
+            bg=bg[bi], scale_modifier=1.0, viewmatrix=cam_params["world_view_transform"][bi],
+            projmatrix=cam_params["full_proj_transform"][bi], sh_degree=0,
+            campos=cam_params["camera_center"][bi], prefiltered=False, debug=False, antialiasing=False)
+        img, rad, dep = Rasterizer(raster_settings=rs)(
+            means3D=mean_3d[bi], means2D=mean_2d[bi], shs=None, colors_precomp=features_color[bi],
+            opacities=assets["opacity"][bi], scales=assets["scaling"][bi],
+            rotations=assets["rotation"][bi], cov3D_precomp=None)
+        imgs.append(img)
+        radiis.append(rad)
+        depths.append(dep)
+    return torch.stack(imgs, 0), torch.stack(radiis, 0), torch.stack(depths, 0)
+
+
+def per_frame_dropin(w, dev, n_frames=256, warmup=16):
+    """GUAVA's own fps (main/test.py:70-76,90): per frame, Ubody_Gaussian.forward (here the deform
+    kernels at B=1) then GaussianRenderer's rasterizer call through the unchanged drop-in API
+    (GaussianRasterizer_32, gaussian_render.py:37-67), B=1, under no_grad as render_set runs.
+    fps = frames / wall time of the loop (the int()/float() camera reads serialise the frames as
+    they do in the reference); the loop ends with a device synchronisation."""
+    import torch
+    from diff_gaussian_rasterization_32 import GaussianRasterizationSettings, GaussianRasterizer_32
+    from guava_renderer_amd.pipeline import AvatarPipeline
+    body, flame, extra, g = w.avatar_assets
+    pipe = AvatarPipeline(body, flame, extra, g, 1, w.W, w.H, R_capacity=1024, device=dev)
+    frames = [({k: v[i:i + 1] for k, v in w.bpt.items()}, {k: v[i:i + 1] for k, v in w.fpt.items()},
+               _cam_params(w, 1, lo=i)) for i in range(w.B)]
+    opacity = pipe.gauss.opacity.unsqueeze(0)
+    colors = pipe.gauss.colors.unsqueeze(0)
+
+    def frame(k):
+        bp, fp, cam = frames[k % len(frames)]
+        dg = pipe.deform(bp, fp)  # Ubody_Gaussian.forward (ubody_gaussian.py:245-289)
+        assets = {"xyz": dg["xyz"], "rotation": dg["rotation"], "scaling": dg["scaling"],
+                  "opacity": opacity, "features_color": colors}
+        return _render_model(assets, cam, 1, dev, GaussianRasterizationSettings, GaussianRasterizer_32)
+
+    with torch.no_grad():
+        for k in range(warmup):
+            frame(k)
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        for k in range(n_frames):
+            frame(k)
+        torch.cuda.synchronize(dev)
+        el = time.perf_counter() - t0
+    return {"value": round(n_frames / el, 2), "unit": "frames/s", "latency_ms_per_frame": round(1e3 * el / n_frames, 4),
+            "frames": n_frames, "batch": 1,
+            "path": "deform (B=1) + GaussianRasterizer_32 per frame, no_grad (main/test.py:70-76)"}
+
+
 def main():
     a = _args()
+    ws = os.environ.get("WORLD_SIZE")
+    if ws is None and a.gpus > 1:
+        sys.exit(_launch_ranks(a.gpus))
+    world = int(ws or "1")
+    if world != a.gpus:
+        print(f"bench.py: --gpus {a.gpus} but the launcher started WORLD_SIZE={world} ranks", file=sys.stderr)
+        sys.exit(2)
     import torch
-    world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None
@@ -156,191 +408,90 @@ def main():
             dist.init_process_group(backend)
     torch.cuda.set_device(dev)
 
-    from guava_renderer_amd import _lib, parallel, scenes
-    from guava_renderer_amd.batch import BatchRasterizer, profile_enable, profile_read, render_counters
-    _lib.set_exact_exp(not a.fast_exp)
-    _lib.set_split_bf16(not a.exact_accum)
+    from guava_renderer_amd import _lib, parallel
+    from guava_renderer_amd.batch import profile_enable, profile_read, render_counters
 
+    numerics = _lib.numerics(fast_exp=a.fast_exp, split_bf16=a.split_bf16)
     wl = _workload(a.config)
-    P, W, H, B = wl["P"], wl["W"], wl["H"], a.batch
-    cams_all = scenes.frame_cameras(B * world, W, H, seed=1000)
-    cams = parallel.shard_frames(cams_all, rank, world)  # B frames per rank, no data-path collective
-    t = lambda x: torch.tensor(np.ascontiguousarray(x), device=dev)  # noqa: E731
-    views = t(np.stack([c["viewmatrix"].reshape(16) for c in cams]))
-    projs = t(np.stack([c["projmatrix"].reshape(16) for c in cams]))
-    tanf = t(np.array([[c["tanfovx"], c["tanfovy"]] for c in cams], np.float32))
-    bgs = torch.zeros((B, C), dtype=torch.float32, device=dev)
-    avatar_inputs = None
-    workload = wl["name"] + {"avatar": "-deform+raster", "raster": "-raster", "train": "-train",
-                             "frame": "-per-frame-dropin"}[a.pipeline]
-
-    if a.pipeline == "avatar":
-        from guava_renderer_amd import avatar
-        from guava_renderer_amd.pipeline import AvatarPipeline
-        body, flame, extra = avatar.ehm_assets(seed=0)
-        verts, faces, tex = avatar.template_mesh()
-        g = avatar.gaussians(verts, faces, tex, P=P, seed=0)
-        bp_all, fp_all = avatar.ehm_params(B * world, seed=1000)
-        lo, hi = parallel.shard_range(B * world, rank, world)
-        bp = {k: v[lo:hi] for k, v in bp_all.items()}
-        fp = {k: v[lo:hi] for k, v in fp_all.items()}
-        bpt = {k: t(v) for k, v in bp.items()}
-        fpt = {k: t(v) for k, v in fp.items()}
-        probe = AvatarPipeline(body, flame, extra, g, B, W, H, R_capacity=24 * P * B, device=dev)
-        probe.render(bpt, fpt, views, projs, tanf)
-        R_probe, ovf = probe.rast.status()
-        assert not ovf, "probe overflow"
-        del probe
-        torch.cuda.empty_cache()
-        pipes = [AvatarPipeline(body, flame, extra, g, B, W, H, R_capacity=int(R_probe * 1.25) + 1024, device=dev)
-                 for _ in range(max(1, a.inflight))]
-        pipe = pipes[0]
-        P = pipe.P
-        rast = pipe.rast
-        rasts = [p.rast for p in pipes]
-        scene = {"colors": g["colors"], "opacities": g["opacities"]}
-        avatar_inputs = (body, flame, extra, g, bp, fp)
-
-        head = None
-        if a.refine:
-            from guava_renderer_amd.batch import RefineHead
-            rng = np.random.default_rng(5)  # random-init conv_body_first (nn.Conv2d(32, 16, 1))
-            head = RefineHead(t(rng.uniform(-0.18, 0.18, (16, 32)).astype(np.float32)),
-                              t(rng.uniform(-0.18, 0.18, 16).astype(np.float32)), keep_channels=4)
-
-        def step_on(i):
-            return pipes[i].render(bpt, fpt, views, projs, tanf, refine=head)
-    elif a.pipeline == "train":
-        from guava_renderer_amd.train import SplatTrainer
-        scene = scenes.avatar_cloud(P, seed=0, gaussians_per_texel=wl["gpt"])
-        P = scene["means3D"].shape[0]
-        params = {k: t(scene[k]) for k in ("means3D", "colors", "opacities", "scales", "rotations")}
-        probe = BatchRasterizer(B, P, W, H, R_capacity=24 * P * B, device=dev)
-        probe.forward(params["means3D"], params["colors"], params["opacities"], params["scales"],
-                      params["rotations"], views, projs, tanf, bgs)
-        R_probe, ovf = probe.status()
-        assert not ovf, "probe overflow"
-        del probe
-        torch.cuda.empty_cache()
-        # the trainable parameters are the raw attributes: a small learning rate
-        # keeps the per-step work at the avatar's distribution over the timed steps; capacity with
-        # headroom for the drift (an overflowing step is skipped on the device and counted)
-        trainer = SplatTrainer(params, B, W, H, R_capacity=int(R_probe * 2) + 1024, device=dev, lr=1e-5)
-        rast = trainer.rast
-        target = torch.rand((B, 3, H, W), device=dev, generator=torch.Generator(device=dev).manual_seed(rank))
-
-        rasts = [rast]
-
-        def step_on(i):
-            return trainer.step(views, projs, tanf, target)
-    elif a.pipeline == "frame":
-        # GUAVA's unchanged caller (models/UbodyAvatar/gaussian_render.py:19-67, the refiner aside):
-        # one GaussianRasterizationSettings + GaussianRasterizer_32 call per frame, camera fields
-        # read per frame with int()/float() from device tensors, outputs stacked.  The deformed
-        # assets of the B frames come from the deform kernels, outside the timed region.
-        from diff_gaussian_rasterization_32 import GaussianRasterizationSettings, GaussianRasterizer_32
-        from guava_renderer_amd import avatar
-        from guava_renderer_amd.pipeline import AvatarPipeline
-        body, flame, extra = avatar.ehm_assets(seed=0)
-        verts, faces, tex = avatar.template_mesh()
-        g = avatar.gaussians(verts, faces, tex, P=P, seed=0)
-        bp_all, fp_all = avatar.ehm_params(B * world, seed=1000)
-        lo, hi = parallel.shard_range(B * world, rank, world)
-        bpt = {k: t(v[lo:hi]) for k, v in bp_all.items()}
-        fpt = {k: t(v[lo:hi]) for k, v in fp_all.items()}
-        dpipe = AvatarPipeline(body, flame, extra, g, B, W, H, R_capacity=24 * P * B, device=dev)
-        dg = dpipe.deform(bpt, fpt)
-        P = dpipe.P
-        assets = {"xyz": dg["xyz"], "rotation": dg["rotation"], "scaling": dg["scaling"],
-                  "opacity": dpipe.gauss.opacity.unsqueeze(0).expand(B, -1, -1),
-                  "features_color": dpipe.gauss.colors.unsqueeze(0).expand(B, -1, -1)}
-        cam_params = {"image_height": torch.full((B,), H, device=dev), "image_width": torch.full((B,), W, device=dev),
-                      "tanfovx": tanf[:, 0].contiguous(), "tanfovy": tanf[:, 1].contiguous(),
-                      "world_view_transform": views.view(B, 4, 4), "full_proj_transform": projs.view(B, 4, 4),
-                      "camera_center": t(np.stack([c["campos"] for c in cams]))}
-        scene = {"colors": g["colors"], "opacities": g["opacities"]}
-        avatar_inputs = (body, flame, extra, g, {k: v[lo:hi] for k, v in bp_all.items()},
-                         {k: v[lo:hi] for k, v in fp_all.items()})
-        rasts = []
-        last_radii = [None]
-
-        def step_on(i):
-            with torch.no_grad():
-                mean_3d = assets["xyz"]
-                features_color = assets["features_color"].clone()
-                mean_2d = torch.zeros_like(mean_3d, dtype=torch.float32, requires_grad=True, device=dev)
-                bg = torch.ones((B, features_color.shape[-1]), dtype=torch.float32, device=dev) * 0.0
-                imgs, radiis, depths = [], [], []
-                for bi in range(B):
-                    rs = GaussianRasterizationSettings(
-                        image_height=int(cam_params["image_height"][bi]), image_width=int(cam_params["image_width"][bi]),
-                        tanfovx=float(cam_params["tanfovx"][bi]), tanfovy=float(cam_params["tanfovy"][bi]),
-                        bg=bg[bi], scale_modifier=1.0, viewmatrix=cam_params["world_view_transform"][bi],
-                        projmatrix=cam_params["full_proj_transform"][bi], sh_degree=0,
-                        campos=cam_params["camera_center"][bi], prefiltered=False, debug=False, antialiasing=False)
-                    img, rad, dep = GaussianRasterizer_32(raster_settings=rs)(
-                        means3D=mean_3d[bi], means2D=mean_2d[bi], shs=None, colors_precomp=features_color[bi],
-                        opacities=assets["opacity"][bi], scales=assets["scaling"][bi],
-                        rotations=assets["rotation"][bi], cov3D_precomp=None)
-                    imgs.append(img)
-                    radiis.append(rad)
-                    depths.append(dep)
-                out = torch.stack(imgs, 0)
-                last_radii[0] = torch.stack(radiis, 0)
-                return out, torch.stack(depths, 0), last_radii[0]
+    W, H = wl["W"], wl["H"]
+    if a.global_batch is not None:
+        if a.global_batch % world:
+            print(f"bench.py: --global-batch {a.global_batch} does not split over {world} ranks", file=sys.stderr)
+            sys.exit(2)
+        B, scaling, n_total = a.global_batch // world, "strong", a.global_batch
     else:
-        scene = scenes.avatar_cloud(P, seed=0, gaussians_per_texel=wl["gpt"])
-        P = scene["means3D"].shape[0]
-        means, colors = t(scene["means3D"]), t(scene["colors"])
-        opac, scales, rots = t(scene["opacities"]), t(scene["scales"]), t(scene["rotations"])
-        # size the instance capacity from one probe batch
-        probe = BatchRasterizer(B, P, W, H, R_capacity=24 * P * B, device=dev)
-        probe.forward(means, colors, opac, scales, rots, views, projs, tanf, bgs)
-        R_probe, ovf = probe.status()
-        assert not ovf, "probe overflow"
-        del probe
-        torch.cuda.empty_cache()
-        rasts = [BatchRasterizer(B, P, W, H, R_capacity=int(R_probe * 1.25) + 1024, device=dev)
-                 for _ in range(max(1, a.inflight))]
-        rast = rasts[0]
-
-        def step_on(i):
-            return rasts[i].forward(means, colors, opac, scales, rots, views, projs, tanf, bgs)
+        B, scaling, n_total = a.batch, "weak", a.batch * world
+    lo = rank * B
+    w = Workload(a, wl, B, lo, n_total, dev, numerics)
+    P = w.P
+    workload = wl["name"] + {"avatar": "-deform+raster" + ("-cross" if a.config == "c5" else ""),
+                             "raster": "-raster", "train": "-train", "frame": "-per-frame-dropin"}[a.pipeline]
 
     # batches in flight: step k runs on stream k mod n with its own pipeline / workspace (each
     # batch is complete work -- deform, binning, compositing; only consecutive batches overlap)
-    n_inflight = max(1, len(rasts))
+    n_inflight = max(1, len(w.rasts))
     streams = [torch.cuda.current_stream(dev)] + [torch.cuda.Stream(dev) for _ in range(n_inflight - 1)]
-    step_count = [0]
 
-    gather = dist is not None and a.pipeline != "train"
-    # consumer boundary: every rank receives all ranks' RGB frames (RCCL all-gather over xGMI),
-    # each batch's exchange overlapped with the next batch's rendering on a side stream
-    gatherer = None
-    if gather:
+    # consumer boundary at N>1: every rank receives all ranks' frames as the consumer writes them
+    # (8-bit RGB, main/test.py:85) over RCCL/xGMI, each batch's exchange overlapped with the next
+    # batch's rendering on a side stream
+    def make_gatherer(b):
+        if dist is None or a.pipeline == "train" or a.gather == "none":
+            return None
         gdev = dev if backend == "nccl" else torch.device("cpu")
-        gatherer = parallel.FrameGather(B, (3, H, W), torch.float32, gdev)
+        return parallel.FrameGather(b, (3, H, W), torch.uint8 if a.gather == "u8" else torch.float32, gdev)
 
-    def step():
-        i = step_count[0] % n_inflight
-        step_count[0] += 1
-        with torch.cuda.stream(streams[i]):
-            res = step_on(i)
-            if gatherer is not None:
-                rgb = res[0][:, :3]
-                gatherer.push(rgb if backend == "nccl" else rgb.cpu())
-            return res
+    def make_step(wk, gatherer):
+        cnt = [0]
 
+        def step():
+            i = cnt[0] % n_inflight
+            cnt[0] += 1
+            with torch.cuda.stream(streams[i]):
+                res = wk.step_on(i)
+                if gatherer is not None:
+                    frames = res[0]
+                    if backend != "nccl":  # gloo rehearsal: encode on the GPU, exchange on the host
+                        frames = parallel.frames_to8b(frames).cpu() if a.gather == "u8" else frames[:, :3].cpu()
+                    elif a.gather == "f32":
+                        frames = frames[:, :3]
+                    gatherer.push(frames)
+                return res
+        return step
+
+    def timed(step, gatherer, steps, warmup):
+        for _ in range(warmup):
+            step()
+        torch.cuda.synchronize(dev)
+        if dist is not None:
+            dist.barrier()
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            step()
+        if gatherer is not None:
+            gatherer.wait()
+        torch.cuda.synchronize(dev)
+        el = time.perf_counter() - t0
+        if dist is not None:
+            dist.barrier()
+            tt = torch.tensor([el], dtype=torch.float64, device=dev if backend == "nccl" else "cpu")
+            dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+            el = float(tt.item())
+        return el
+
+    gatherer = make_gatherer(B)
+    step = make_step(w, gatherer)
     for _ in range(a.warmup):
         step()
     torch.cuda.synchronize(dev)
-    if rasts:
-        R_total, ovf = rast.status()
-        assert not any(r.status()[1] for r in rasts)
-        P_vis = int((rast.radii > 0).sum().item())
-    else:  # per-frame drop-in path: the _C calls size their own buffers (exact R, host sync)
+    if w.rast is not None:
+        R_total, ovf = w.rast.status()
+        assert not any(r.status()[1] for r in w.rasts)
+        P_vis = int((w.rast.radii > 0).sum().item())
+    else:  # per-frame drop-in path: the _C calls size their own buffers
         R_total = None
-        P_vis = int((last_radii[0] > 0).sum().item())
+        P_vis = int((w.last_radii[0] > 0).sum().item())
     profile_read()  # reset accumulators
     stage_set = (("preprocess", "scan", "depth_sort", "chunk_count", "tile_scan", "ordered_scatter",
                   "render_fwd", "render_bwd", "preprocess_bwd") if a.stages else
@@ -350,64 +501,57 @@ def main():
     # isolated pass afterwards, one batch at a time
     isolated = n_inflight > 1
     profile_enable(() if isolated else stage_set)
-    if dist is not None:
-        dist.barrier()
-    torch.cuda.synchronize(dev)
-    t0 = time.perf_counter()
-    for _ in range(a.steps):
-        step()
-    if gatherer is not None:
-        gatherer.wait()
-    torch.cuda.synchronize(dev)
-    el = time.perf_counter() - t0
-    if dist is not None:
-        dist.barrier()
+    el = timed(step, gatherer, a.steps, 0)
     prof = profile_read()
     profile_enable(())
     if isolated:
         profile_enable(stage_set)
         for _ in range(max(20, a.steps // 4)):
             with torch.cuda.stream(streams[0]):
-                step_on(0)
+                w.step_on(0)
         torch.cuda.synchronize(dev)
         prof = profile_read()
         profile_enable(())
+    if a.pipeline == "train":
+        assert w.trainer.skipped_steps == 0 and not w.trainer.rast.status()[1], \
+            "capacity overflow inside the timed region"
+    else:
+        assert not any(r.status()[1] for r in w.rasts), "capacity overflow inside the timed region"
+    extras = not a.no_extras
     deform_ms = None
     if a.pipeline == "avatar":  # deformation alone (EHM + Gaussian assembly), outside the timed region
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record()
         for _ in range(a.steps):
-            pipe.deform(bpt, fpt)
+            w.pipes[0].deform(w.bpt, w.fpt)
         e1.record()
         torch.cuda.synchronize(dev)
         deform_ms = e0.elapsed_time(e1) / a.steps
-    # the bit-exact colour accumulation on the same workload (split-bf16 off), a shorter run after
-    # the timed region: the line's `exact_accum` (N=1 avatar / raster pipelines, default mode only)
-    exact_line = None
-    if dist is None and not a.exact_accum and a.pipeline in ("avatar", "raster"):
-        _lib.set_split_bf16(False)
-        n_ex = max(20, a.steps // 4)
-        for _ in range(3):
-            step()
-        torch.cuda.synchronize(dev)
-        t_ex = time.perf_counter()
-        for _ in range(n_ex):
-            step()
-        torch.cuda.synchronize(dev)
-        ms_ex = (time.perf_counter() - t_ex) / n_ex * 1e3
-        _lib.set_split_bf16(True)
-        exact_line = {"value": round(1e3 * B / ms_ex, 2), "ms_per_step": round(ms_ex, 4), "steps": n_ex,
-                      "colour_accum": "f32 mfma (bit-exact with the oracle)"}
+    # the other colour-accumulation mode on the same workload, a shorter run after the timed region
+    other_line = None
+    if extras and dist is None and a.pipeline in ("avatar", "raster"):
+        other = numerics ^ _lib.NUMERICS_SPLIT_BF16
+        for r in w.rasts:
+            r.numerics = other
+        n_o = max(20, a.steps // 4)
+        el_o = timed(step, None, n_o, 3)
+        for r in w.rasts:
+            r.numerics = numerics
+        other_line = {"value": round(B * n_o / el_o, 2), "ms_per_step": round(1e3 * el_o / n_o, 4), "steps": n_o,
+                      "colour_accum": "split-bf16 mfma (<=1e-4 L_inf)" if other & _lib.NUMERICS_SPLIT_BF16
+                      else "f32 mfma (bit-exact with the oracle)"}
     # work counters of one extra (instrumented, untimed) step: which wall the render kernel hits
     work = render_counters(step, device=dev)
-    if a.pipeline == "train":
-        assert trainer.skipped_steps == 0 and not trainer.rast.status()[1], "capacity overflow inside the timed region"
-    else:
-        assert not any(r.status()[1] for r in rasts), "capacity overflow inside the timed region"
-    if dist is not None:
-        tt = torch.tensor([el], dtype=torch.float64, device=dev if backend == "nccl" else "cpu")
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        el = float(tt.item())
+    # config 3 at N>1: the 32-frame batch split over the ranks (strong scaling) beside the weak line
+    strong_line = None
+    if extras and dist is not None and scaling == "weak" and a.pipeline == "avatar" and 32 % world == 0:
+        w3 = Workload(a, wl, 32 // world, rank * (32 // world), 32, dev, numerics)
+        g3 = make_gatherer(32 // world)
+        n3 = max(20, a.steps // 4)
+        el3 = timed(make_step(w3, g3), g3, n3, 5)
+        strong_line = {"value": round(32 * n3 / el3, 2), "ms_per_step": round(1e3 * el3 / n3, 4), "steps": n3,
+                       "global_batch": 32, "frames_per_gpu": 32 // world, "scaling": "strong"}
+        del w3, g3
 
     frames = world * B * a.steps
     fps = frames / el
@@ -417,22 +561,27 @@ def main():
     frames_per_launch = 1 if a.pipeline == "frame" else B
     bytes_launch = _render_alg_bytes(P_vis / B, W, H) * frames_per_launch
     achieved = bytes_launch / (render_ms * 1e-3) / 1e9 if render_ms > 0 else None
-    traffic = issue = None
-    # HBM traffic per launch from the committed PMC summaries (tools/pmc_summary.py): the contract
-    # workload's (pmc_render_fwd.json) and the training batch's (pmc_train.json: render_fwd and
-    # render_bwd of `--pipeline train --batch 6`)
+    traffic = issue = bwd_traffic = None
+    traffic_note = "no PMC summary for this workload"
+    # HBM traffic per launch from the committed PMC summaries (tools/pmc_summary.py), used only when
+    # they were measured on the library built from these sources (their source hash)
     pmc_path = os.path.join(ROOT, "profiles", "pmc_train.json" if a.pipeline == "train" else "pmc_render_fwd.json")
-    bwd_traffic = None
     if os.path.exists(pmc_path):
         try:
+            from guava_renderer_amd import build as _build
             pm = json.load(open(pmc_path))
             if pm.get("config") == workload and pm.get("batch") == B:
-                traffic = pm.get("hbm_bytes_per_launch")
-                issue = pm.get("render_fwd_issue")
-                bwd_traffic = (pm.get("kernels", {}).get("k_render_bwd") or {}).get("hbm_bytes")
-        except Exception:  # noqa: BLE001
-            traffic = None
+                if pm.get("source_hash") == _build.source_hash():
+                    traffic = pm.get("hbm_bytes_per_launch")
+                    issue = pm.get("render_fwd_issue")
+                    bwd_traffic = (pm.get("kernels", {}).get("k_render_bwd") or {}).get("hbm_bytes")
+                    traffic_note = f"PMC FETCH_SIZE+WRITE_SIZE, {os.path.basename(pmc_path)} (this build)"
+                else:
+                    traffic_note = f"{os.path.basename(pmc_path)} was measured on another build: not used"
+        except Exception as e:  # noqa: BLE001
+            traffic_note = f"PMC summary unreadable: {e}"
 
+    split_head = bool(numerics & _lib.NUMERICS_SPLIT_BF16)
     out = {
         "metric": ("training frames/sec (raster fwd+bwd + fused-SSIM loss) @512x512, ~100k Gaussians"
                    if a.pipeline == "train" else
@@ -445,12 +594,13 @@ def main():
         "warmup": a.warmup,
         "ms_per_step": round(ms_step, 4),
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": scaling,
         "vs_baseline": None,
-        "dtype": "f32" if a.exact_accum else "f32 (colour products in split-bf16: f = f_hi + f_lo, f32 accumulation)",
+        "dtype": "f32 (colour products in split-bf16: f = f_hi + f_lo, f32 accumulation)" if split_head else "f32",
         "data": ("synthetic avatar (SMPL-X template mesh + UV-texel Gaussians, synthetic LBS bases, "
                  "GUAVA attribute distributions), one pose + one orbit camera per frame"
-                 if a.pipeline == "avatar" else
+                 + (", cross-reenactment (target poses, source identity)" if a.config == "c5" else "")
+                 if a.pipeline in ("avatar", "frame") else
                  "synthetic (SMPL-X-template avatar cloud, GUAVA attribute distributions, "
                  "one orbit camera per frame)"),
         "config": {"workload": workload,
@@ -460,18 +610,22 @@ def main():
                                          "(all 32 channels carry gradient) -> frame-reduced raster bwd -> "
                                          "grad all-reduce -> Adam",
                                 "frame": "deformed frames -> GaussianRasterizer_32 once per frame (gaussian_render.py:37-67)"
-                                }[a.pipeline] + (" + fused refiner conv_body_first" if a.refine else ""), "gaussians": P, "image": [W, H], "channels": C,
+                                }[a.pipeline] + (" + fused refiner conv_body_first" if a.refine else ""),
+                   "gaussians": P, "image": [W, H], "channels": C,
                    "frames_per_step_per_gpu": B, "global_batch": B * world,
-                   "parallelism": f"frame-sharded x{world}" + (", RGB all-gather per step (overlapped with the next step)" if world > 1 and a.pipeline != "train" else ""),
+                   "parallelism": f"frame-sharded x{world}" + (
+                       f", {a.gather} RGB all-gather per step (overlapped with the next step)"
+                       if world > 1 and a.pipeline != "train" and a.gather != "none" else
+                       ", gradient all-reduce per step" if world > 1 and a.pipeline == "train" else ""),
                    "batches_in_flight": n_inflight,
                    "exp": "hw" if a.fast_exp else "exact-poly",
-                   "colour_accum": "f32 mfma (bit-exact)" if a.exact_accum else "split-bf16 mfma (<=1e-4)",
+                   "colour_accum": "split-bf16 mfma (<=1e-4)" if split_head else "f32 mfma (bit-exact)",
                    "instances_per_step": R_total, "visible_gaussians_per_frame": P_vis / B},
         "roofline": {"bound": "hbm", "kernel": "render_fwd",
                      "achieved": round(achieved, 1) if achieved else None,
                      "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 4) if achieved else None,
-                     "traffic": traffic, "alg_bytes_per_launch": bytes_launch,
+                     "traffic": traffic, "traffic_source": traffic_note, "alg_bytes_per_launch": bytes_launch,
                      "avg_launch_ms": round(render_ms, 4),
                      "timing": "isolated pass, one batch in flight" if isolated else "timed region"},
         "path_roofline": {"alg_bytes_per_frame": _path_alg_bytes(P, W, H),
@@ -480,19 +634,19 @@ def main():
     }
     # per-frame work of the render kernel and its matrix-core utilisation (dense peak of the MFMA used)
     ksteps = work["mfma_ksteps"]
-    if a.exact_accum:
+    if not split_head:
         mfma_flops = ksteps * 2 * (2 * 32 * 32 * 2)  # two v_mfma_f32_32x32x2f32 per wave k-step
     else:  # two v_mfma_f32_32x32x8_bf16 per wave k-step (every k-slot carries a split product)
         mfma_flops = ksteps * 2 * (2 * 32 * 32 * 8)
     out["render_work_per_frame"] = {k: round(v / B, 1) for k, v in work.items()}
     out["render_mfma"] = {"issued_tflops": round(mfma_flops / (render_ms * 1e-3) / 1e12, 2) if render_ms else None,
-                          "peak_tflops": F32_MFMA_PEAK_TFLOPS if a.exact_accum else BF16_MFMA_PEAK_TFLOPS,
-                          "instruction": "v_mfma_f32_32x32x2_f32" if a.exact_accum else "v_mfma_f32_32x32x8_bf16",
+                          "peak_tflops": BF16_MFMA_PEAK_TFLOPS if split_head else F32_MFMA_PEAK_TFLOPS,
+                          "instruction": "v_mfma_f32_32x32x8_bf16" if split_head else "v_mfma_f32_32x32x2_f32",
                           "useful_frac": round(work["pairs_contributing"] / max(64 * work["strip_pairs_blended"], 1), 4)}
-    if issue is not None and not a.exact_accum:
+    if issue is not None:
         # the compute wall beside the HBM one: per-launch instruction counts and per-SIMD pipe busy
-        # of the contract kernel, from the committed PMC passes (profiles/pmc_render_fwd.json)
-        out["render_issue"] = dict(issue, source="profiles/pmc_render_fwd.json (tools/gpu_pmc_fwd.sh)",
+        # of the contract kernel, from the committed PMC passes of this build
+        out["render_issue"] = dict(issue, source="profiles/pmc_render_fwd.json (tools/gpu_pmc.sh)",
                                    valu_per_kstep=round(issue["valu_insts"] / max(ksteps, 1), 1)
                                    if issue.get("valu_insts") else None)
     if a.pipeline == "train":
@@ -509,12 +663,16 @@ def main():
         out["latency_ms_per_frame"] = round(1000.0 * el / (a.steps * B), 4)
     if deform_ms is not None:
         out["deform_ms_per_step"] = round(deform_ms, 4)
-    if exact_line is not None:
-        out["exact_accum"] = exact_line
+    if other_line is not None:
+        out["split_bf16" if not split_head else "exact_accum"] = other_line
+    if strong_line is not None:
+        out["config3_strong"] = strong_line
     if a.stages:
         out["stage_ms_per_step"] = {k: round(v[0] / max(v[1], 1), 4) for k, v in prof.items()}
+    if extras and world == 1 and a.pipeline == "avatar":
+        out["per_frame_dropin"] = per_frame_dropin(w, dev)
     if rank == 0 and world == 1 and not a.no_cpu_baseline and a.pipeline != "train":
-        out["cpu_baseline"] = cpu_baseline(scene, cams, W, H, a.cpu_seconds, avatar_inputs)
+        out["cpu_baseline"] = cpu_baseline(w.scene, w.cams, W, H, a.cpu_seconds, w.avatar_inputs)
     if rank == 0:
         print(json.dumps(out), flush=True)
     if dist is not None:

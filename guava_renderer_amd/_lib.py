@@ -9,18 +9,29 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "lib", "libgsr.so")
 
 # every symbol declared in include/*.h
-EXPORTS = ("gsr_version", "gsr_last_error", "gsr_set_exact_exp", "gsr_set_split_bf16", "gsr_geometry_bytes",
-           "gsr_image_bytes", "gsr_binning_bytes", "gsr_mark_visible", "gsr_forward",
+EXPORTS = ("gsr_version", "gsr_last_error", "gsr_geometry_bytes",
+           "gsr_image_bytes", "gsr_binning_bytes", "gsr_mark_visible", "gsr_forward", "gsr_forward_ex",
            "gsr_forward_async_bound", "gsr_forward_async",
-           "gsr_backward", "gsr_batch_workspace_bytes", "gsr_forward_batch",
+           "gsr_backward", "gsr_backward_ex", "gsr_batch_workspace_bytes", "gsr_forward_batch",
            "gsr_backward_batch", "gsr_backward_batch_shared", "gsr_batch_status", "gsr_profile_enable", "gsr_profile_read",
            "gsr_render_counters", "gsr_render_timeline", "gsr_forward_batch_refine",
-           "gsr_refine_prepare", "gsr_batch_status_offset",
+           "gsr_refine_prepare", "gsr_batch_status_offset", "gsr_frames_to8b",
            # include/gsr_deform.h
            "gsr_lbs_workspace_bytes", "gsr_lbs", "gsr_blend_joints", "gsr_splice_head",
            "gsr_pack_rows", "gsr_deform_gaussians",
            # include/gsr_ssim.h
            "gsr_fused_ssim", "gsr_fused_ssim_backward", "gsr_image_loss_partials", "gsr_image_loss")
+
+# per-call numerics flags (include/gsr.h GSR_NUMERICS_*); 0 = bit-identical to the CPU oracle
+NUMERICS_EXACT = 0
+NUMERICS_FAST_EXP = 1
+NUMERICS_SPLIT_BF16 = 2
+
+
+def numerics(fast_exp=False, split_bf16=False):
+    """The `numerics` flag word of one call (include/gsr.h)."""
+    return (NUMERICS_FAST_EXP if fast_exp else 0) | (NUMERICS_SPLIT_BF16 if split_bf16 else 0)
+
 
 ALLOC_FN = ctypes.CFUNCTYPE(ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t)
 
@@ -29,6 +40,7 @@ _i = ctypes.c_int
 _i64 = ctypes.c_int64
 _f = ctypes.c_float
 _sz = ctypes.c_size_t
+_u32 = ctypes.c_uint32
 
 _lib = None
 
@@ -80,10 +92,6 @@ def load(path=None):
             raise GsrError(f"{path} was built from other sources (hash {built}, tree {_build.source_hash()}): "
                            "rebuild with `python -m guava_renderer_amd.build` (GSR_ALLOW_STALE=1 overrides)")
     L.gsr_last_error.restype = ctypes.c_char_p
-    L.gsr_set_exact_exp.argtypes = [_i]
-    L.gsr_set_exact_exp.restype = _i
-    L.gsr_set_split_bf16.argtypes = [_i]
-    L.gsr_set_split_bf16.restype = _i
     L.gsr_geometry_bytes.argtypes = [_i, _i, _i]
     L.gsr_geometry_bytes.restype = _sz
     L.gsr_image_bytes.argtypes = [_i, _i]
@@ -96,33 +104,37 @@ def load(path=None):
                               _vp, _vp, _vp, _f, _vp, _vp, _vp, _vp, _vp, _f, _f, _i, _vp, _vp, _i,
                               _vp, _i, _vp]
     L.gsr_forward.restype = _i
+    L.gsr_forward_ex.argtypes = list(L.gsr_forward.argtypes[:-1]) + [_u32, _vp]
+    L.gsr_forward_ex.restype = _i
     L.gsr_forward_async_bound.argtypes = [_i, _i, _i]
     L.gsr_forward_async_bound.restype = _i64
-    L.gsr_forward_async.argtypes = list(L.gsr_forward.argtypes[:-1]) + [_vp, _vp]
+    L.gsr_forward_async.argtypes = list(L.gsr_forward.argtypes[:-1]) + [_vp, _u32, _vp]
     L.gsr_forward_async.restype = _i
     L.gsr_backward.argtypes = [_i, _i, _i, _i, _vp, _i, _i, _vp, _vp, _vp, _vp, _vp, _f, _vp, _vp,
                                _vp, _vp, _vp, _f, _f, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp,
                                _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i, _i, _vp]
     L.gsr_backward.restype = _i
+    L.gsr_backward_ex.argtypes = list(L.gsr_backward.argtypes[:-1]) + [_u32, _vp]
+    L.gsr_backward_ex.restype = _i
     L.gsr_batch_workspace_bytes.argtypes = [_i, _i, _i, _i, _i64]
     L.gsr_batch_workspace_bytes.restype = _sz
     L.gsr_batch_status_offset.argtypes = [_i, _i, _i, _i, _i64]
     L.gsr_batch_status_offset.restype = _sz
     L.gsr_forward_batch.argtypes = [_i, _i, _i, _i, _vp, _i64, _vp, _i64, _vp, _i64, _vp, _i64, _vp,
                                     _i64, _f, _vp, _vp, _vp, _vp, _i64, _vp, _i64, _vp, _vp, _vp, _i,
-                                    _vp]
+                                    _u32, _vp]
     L.gsr_forward_batch.restype = _i
-    L.gsr_forward_batch_refine.argtypes = list(L.gsr_forward_batch.argtypes[:-1]) + [
-        ctypes.POINTER(RefineEpilogue), _vp]
+    L.gsr_forward_batch_refine.argtypes = list(L.gsr_forward_batch.argtypes[:-2]) + [
+        ctypes.POINTER(RefineEpilogue), _u32, _vp]
     L.gsr_forward_batch_refine.restype = _i
     L.gsr_refine_prepare.argtypes = [_i, _vp, _vp, _i, _i, _vp, _vp]
     L.gsr_refine_prepare.restype = _i
     L.gsr_backward_batch.argtypes = [_i, _i, _i, _i, _vp, _i64, _vp, _i64, _vp, _i64, _vp, _i64, _vp,
                                      _i64, _f, _vp, _vp, _vp, _vp, _i64, _vp, _i64, _vp, _vp, _vp, _vp,
-                                     _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i, _vp]
+                                     _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i, _u32, _vp]
     L.gsr_backward_batch.restype = _i
     L.gsr_backward_batch_shared.argtypes = list(L.gsr_backward_batch.argtypes[:24]) + [_vp, _vp, _vp, _vp, _vp,
-                                                                                       _i, _vp]
+                                                                                       _i, _u32, _vp]
     L.gsr_backward_batch_shared.restype = _i
     L.gsr_batch_status.argtypes = [_vp, _i, _i, ctypes.POINTER(_i64), ctypes.POINTER(_i), _vp]
     L.gsr_batch_status.restype = _i
@@ -134,6 +146,8 @@ def load(path=None):
     L.gsr_render_counters.restype = _i
     L.gsr_render_timeline.argtypes = [_vp, ctypes.c_uint32]
     L.gsr_render_timeline.restype = _i
+    L.gsr_frames_to8b.argtypes = [_i, _i, _i, _i, _vp, _i64, _vp, _vp]
+    L.gsr_frames_to8b.restype = _i
     L.gsr_lbs_workspace_bytes.argtypes = [_i, _i, _i, _i]
     L.gsr_lbs_workspace_bytes.restype = _sz
     L.gsr_lbs.argtypes = [_i, _i, _i, _i, _vp, _i64, _vp, _vp, _vp, _i, _vp, _vp, _vp, _vp, _vp, _vp,
@@ -168,11 +182,3 @@ def check(rc, what):
         raise GsrError(f"{what} failed ({-rc}): {msg}")
     return rc
 
-
-def set_exact_exp(on=True):
-    return load().gsr_set_exact_exp(1 if on else 0)
-
-
-def set_split_bf16(on=True):
-    """Split-bf16 MFMA colour accumulation (tolerance mode, include/gsr.h); returns the previous setting."""
-    return load().gsr_set_split_bf16(1 if on else 0)

@@ -156,3 +156,19 @@ def ehm_params(B, seed=1000, n_shape=300, n_exp=50, body_sigma=0.15):
                  eye_pose_params=0.05 * f(B, 6),
                  eyelid_params=np.clip(0.5 + 0.2 * f(B, 2), 0.0, 1.0).astype(np.float32))
     return body, flame
+
+
+def change_id_info(target_body, target_flame, source_body, source_flame):
+    """Cross-reenactment inputs (main/test.py:21-28 change_id_info): the target frames' pose and
+    expression with the SOURCE identity -- shape, joints_offset, head_scale and the FLAME shape come
+    from the source (its first frame, broadcast over the target's B frames).  hand_scale is not part
+    of these assets (EHMDeformer rejects it: the MANO vertex map is not bundled)."""
+    B = target_flame["shape_params"].shape[0]
+    body = dict(target_body)
+    flame = dict(target_flame)
+    for k in ("shape", "joints_offset", "head_scale"):
+        if source_body.get(k) is not None:
+            body[k] = np.ascontiguousarray(np.broadcast_to(source_body[k][:1], (B,) + source_body[k].shape[1:]))
+    flame["shape_params"] = np.ascontiguousarray(
+        np.broadcast_to(source_flame["shape_params"][:1], (B,) + source_flame["shape_params"].shape[1:]))
+    return body, flame

@@ -66,14 +66,19 @@ class BatchRasterizer:
     images are NaN) and sets the workspace's sticky overflow word.  No host synchronisation is
     needed to notice it: after every forward the sticky words are copied asynchronously to pinned
     memory, and the next forward/backward (or poll()) raises CapacityError once that copy has
-    landed; poll(wait=True) or status() check at once."""
+    landed; poll(wait=True) or status() check at once.
 
-    def __init__(self, B, P, W, H, R_capacity=None, device="cuda"):
+    numerics: the flag word of this rasterizer's calls (include/gsr.h GSR_NUMERICS_*, built by
+    _lib.numerics()); 0, the default, is bit-identical to the CPU oracle.  A call may override it
+    (forward / backward `numerics=`); nothing is process-wide."""
+
+    def __init__(self, B, P, W, H, R_capacity=None, device="cuda", numerics=0):
         self.B, self.P, self.W, self.H = int(B), int(P), int(W), int(H)
         self.device = torch.device(device)
         if self.device.type == "cuda" and self.device.index is None:
             self.device = torch.device("cuda", torch.cuda.current_device())
         self.R_capacity = int(R_capacity if R_capacity is not None else 16 * P * B)
+        self.numerics = int(numerics)
         self.L = _lib.load()
         nbytes = self.L.gsr_batch_workspace_bytes(self.B, self.P, self.W, self.H, self.R_capacity)
         soff = self.L.gsr_batch_status_offset(self.B, self.P, self.W, self.H, self.R_capacity)
@@ -154,18 +159,19 @@ class BatchRasterizer:
         return self._overflow
 
     def forward(self, means3D, colors, opacities, scales, rotations, viewmatrices, projmatrices,
-                tanfov, backgrounds, scale_modifier=1.0, antialiasing=False, refine=None):
+                tanfov, backgrounds, scale_modifier=1.0, antialiasing=False, refine=None, numerics=None):
         """Render B frames.  refine: optional RefineHead -- the refiner's first 1x1 conv + leaky ReLU
         fused into the render epilogue (include/gsr.h gsr_refine_epilogue); its output is
         refine.out [B,n_out,H,W] and only out_color[:, :refine.keep_channels] is written."""
         self.poll()
+        nm = self.numerics if numerics is None else int(numerics)
         keep, head, (v, pm, tf, bg, bs) = self._inputs(means3D, colors, opacities, scales, rotations,
                                                        viewmatrices, projmatrices, tanfov, backgrounds)
         args = head + (float(scale_modifier), v, pm, tf, bg, bs, self.workspace.data_ptr(), self.R_capacity,
                        self.out_color.data_ptr(), self.out_invdepth.data_ptr(), self.radii.data_ptr(),
                        int(bool(antialiasing)))
         if refine is None:
-            _lib.check(self.L.gsr_forward_batch(*args, self._stream()), "gsr_forward_batch")
+            _lib.check(self.L.gsr_forward_batch(*args, nm, self._stream()), "gsr_forward_batch")
         else:
             # composite the pre-contracted rows (include/gsr.h gsr_refine_prepare): features and
             # backgrounds both go through the head's 32 -> keep + n_out map
@@ -176,7 +182,7 @@ class BatchRasterizer:
             args[6] = pc.data_ptr()
             args[18] = pb.data_ptr()
             ep = refine.epilogue(self.B, self.H, self.W)
-            _lib.check(self.L.gsr_forward_batch_refine(*args, ctypes.byref(ep), self._stream()),
+            _lib.check(self.L.gsr_forward_batch_refine(*args, ctypes.byref(ep), nm, self._stream()),
                        "gsr_forward_batch_refine")
         del keep
         self._after_forward()
@@ -184,13 +190,14 @@ class BatchRasterizer:
 
     def backward(self, means3D, colors, opacities, scales, rotations, viewmatrices, projmatrices,
                  tanfov, backgrounds, dL_dcolor, dL_dinvdepth=None, scale_modifier=1.0,
-                 antialiasing=False, shared=False):
+                 antialiasing=False, shared=False, numerics=None):
         """Gradients of the last forward, per frame: dict of [B,P,k] tensors (all zero when that
         forward overflowed the capacity; the overflow is reported by the next forward / poll).
         shared=True (attributes shared by every frame, e.g. one avatar under B cameras): the
         attribute gradients summed over the frames instead, dict of [P,k] tensors (means3D, colors,
         opacity, scales, rotations) -- gsr_backward_batch_shared, no [B,P,k] buffers."""
         B, P = self.B, self.P
+        nm = self.numerics if numerics is None else int(numerics)
         o = dict(dtype=torch.float32, device=self.device)
         keep, head, (v, pm, tf, bg, bs) = self._inputs(means3D, colors, opacities, scales, rotations,
                                                        viewmatrices, projmatrices, tanfov, backgrounds)
@@ -210,7 +217,7 @@ class BatchRasterizer:
                 *head, float(scale_modifier), v, pm, tf, bg, bs, self.workspace.data_ptr(), self.R_capacity,
                 dLc.data_ptr(), dLi.data_ptr() if dLi is not None else None, g["opacity"].data_ptr(),
                 g["colors"].data_ptr(), g["means3D"].data_ptr(), g["scales"].data_ptr(),
-                g["rotations"].data_ptr(), int(bool(antialiasing)), self._stream())
+                g["rotations"].data_ptr(), int(bool(antialiasing)), nm, self._stream())
             _lib.check(rc, "gsr_backward_batch_shared")
             del keep
             return g
@@ -225,7 +232,7 @@ class BatchRasterizer:
             g["mean2D"].data_ptr(), g["conic"].data_ptr(), g["opacity"].data_ptr(),
             g["colors"].data_ptr(), g["invdepth"].data_ptr() if g["invdepth"] is not None else None,
             g["means3D"].data_ptr(), g["cov3D"].data_ptr(), g["scales"].data_ptr(),
-            g["rotations"].data_ptr(), int(bool(antialiasing)), self._stream())
+            g["rotations"].data_ptr(), int(bool(antialiasing)), nm, self._stream())
         _lib.check(rc, "gsr_backward_batch")
         del keep
         return g

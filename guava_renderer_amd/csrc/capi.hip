@@ -16,8 +16,6 @@ using namespace gsr;
 namespace {
 
 thread_local std::string g_err;
-int g_exact_exp = 1;
-int g_split_bf16 = 0;
 uint64_t* g_render_counters = nullptr;  // gsr_render_counters
 uint32_t* g_timeline = nullptr;         // gsr_render_timeline
 uint32_t g_timeline_cap = 0;
@@ -69,6 +67,11 @@ struct StageTimer {
         if (p) hipEventRecord(p->b, s);
     }
 };
+
+// per-call numerics flags (include/gsr.h GSR_NUMERICS_*)
+inline bool exact_exp(uint32_t numerics) { return (numerics & GSR_NUMERICS_FAST_EXP) == 0; }
+inline bool split_bf16(uint32_t numerics) { return (numerics & GSR_NUMERICS_SPLIT_BF16) != 0; }
+constexpr uint32_t kNumericsKnown = GSR_NUMERICS_FAST_EXP | GSR_NUMERICS_SPLIT_BF16;
 
 inline size_t align_up(size_t x) { return (x + 255) & ~(size_t)255; }
 inline size_t ctrl_words(const Dims& d) { return (size_t)kCtrlWords + (size_t)kFsWords * d.B; }
@@ -177,7 +180,7 @@ namespace {
 
 // Shared forward sequence once R is known and the binning arena exists.
 int run_binning_and_render(const Dims& d, const Inputs& in, const GeomArena& g, const ImageArena& im,
-                           const BinArena& bn, const Outputs& o, int debug, hipStream_t s) {
+                           const BinArena& bn, const Outputs& o, uint32_t numerics, int debug, hipStream_t s) {
     { StageTimer st_(2, s); launch_depth_sort(d, g, s); }
     STAGE(debug, s, "depth_sort");
     { StageTimer st_(3, s); launch_chunk_count(d, g, im, s); }
@@ -190,7 +193,7 @@ int run_binning_and_render(const Dims& d, const Inputs& in, const GeomArena& g, 
         launch_strip_order(d, g, im, bn, s);
     }
     STAGE(debug, s, "ordered_scatter");
-    { StageTimer st_(6, s); launch_render_fwd(d, in, g, im, bn, o, g_exact_exp != 0, g_split_bf16 != 0, s); }
+    { StageTimer st_(6, s); launch_render_fwd(d, in, g, im, bn, o, exact_exp(numerics), split_bf16(numerics), s); }
     STAGE(debug, s, "render_fwd");
     return 0;
 }
@@ -209,17 +212,6 @@ extern "C" {
 // (guava_renderer_amd/build.py source_hash), checked against the tree by the Python loader
 const char* gsr_version(void) { return "gsr-gfx950 0.2 " GSR_SRC_HASH; }
 const char* gsr_last_error(void) { return g_err.c_str(); }
-int gsr_set_exact_exp(int on) {
-    int prev = g_exact_exp;
-    g_exact_exp = on ? 1 : 0;
-    return prev;
-}
-
-int gsr_set_split_bf16(int on) {
-    int prev = g_split_bf16;
-    g_split_bf16 = on ? 1 : 0;
-    return prev;
-}
 
 size_t gsr_geometry_bytes(int P, int width, int height) {
     return carve_geom(nullptr, make_dims(1, P, width, height), nullptr);
@@ -256,9 +248,10 @@ static int forward_single(gsr_alloc_fn geometryBuffer, gsr_alloc_fn binningBuffe
                           const float* rotations, const float* cov3D_precomp, const float* viewmatrix,
                           const float* projmatrix, const float* cam_pos, float tan_fovx, float tan_fovy,
                           int prefiltered, float* out_color, float* depth, int antialiasing, int* radii,
-                          int debug, uint32_t* status_host, hipStream_t s) {
+                          int debug, uint32_t* status_host, uint32_t numerics, hipStream_t s) {
     (void)D; (void)M; (void)shs; (void)cam_pos;
     if (P < 0 || width <= 0 || height <= 0) return fail(GSR_ERR_ARG, "bad P/width/height");
+    if (numerics & ~kNumericsKnown) return fail(GSR_ERR_ARG, "unknown numerics flags");
     if (P >= kMaxGaussians) return fail(GSR_ERR_ARG, "P must be < 2^24");
     if ((int64_t)((width + 15) / 16) * ((height + 15) / 16) > kMaxTiles) return fail(GSR_ERR_ARG, "image too large");
     const Dims d = make_dims(1, P, width, height);
@@ -303,7 +296,7 @@ static int forward_single(gsr_alloc_fn geometryBuffer, gsr_alloc_fn binningBuffe
         if (!bb) return fail(GSR_ERR_ALLOC, "binningBuffer allocation failed");
         BinArena bn;
         carve_bin(bb, cap, &bn);
-        int rc = run_binning_and_render(d, in, g, im, bn, o, debug, s);
+        int rc = run_binning_and_render(d, in, g, im, bn, o, numerics, debug, s);
         if (rc < 0) return rc;
         HIP_TRY(hipMemcpyAsync(status_host, g.ctrl, 4 * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
         return 0;
@@ -322,7 +315,7 @@ static int forward_single(gsr_alloc_fn geometryBuffer, gsr_alloc_fn binningBuffe
     if (!bb) return fail(GSR_ERR_ALLOC, "binningBuffer allocation failed");
     BinArena bn;
     carve_bin(bb, R, &bn);
-    int rc = run_binning_and_render(d, in, g, im, bn, o, debug, s);
+    int rc = run_binning_and_render(d, in, g, im, bn, o, numerics, debug, s);
     if (rc < 0) return rc;
     return (int)R;
 }
@@ -338,7 +331,22 @@ int gsr_forward(gsr_alloc_fn geometryBuffer, gsr_alloc_fn binningBuffer, gsr_all
     return forward_single(geometryBuffer, binningBuffer, imageBuffer, alloc_ctx, P, D, M, background, width,
                           height, means3D, shs, colors_precomp, opacities, scales, scale_modifier, rotations,
                           cov3D_precomp, viewmatrix, projmatrix, cam_pos, tan_fovx, tan_fovy, prefiltered,
-                          out_color, depth, antialiasing, radii, debug, nullptr, (hipStream_t)stream);
+                          out_color, depth, antialiasing, radii, debug, nullptr, GSR_NUMERICS_EXACT,
+                          (hipStream_t)stream);
+}
+
+int gsr_forward_ex(gsr_alloc_fn geometryBuffer, gsr_alloc_fn binningBuffer, gsr_alloc_fn imageBuffer,
+                   void* alloc_ctx, int P, int D, int M, const float* background, int width, int height,
+                   const float* means3D, const float* shs, const float* colors_precomp,
+                   const float* opacities, const float* scales, float scale_modifier,
+                   const float* rotations, const float* cov3D_precomp, const float* viewmatrix,
+                   const float* projmatrix, const float* cam_pos, float tan_fovx, float tan_fovy,
+                   int prefiltered, float* out_color, float* depth, int antialiasing, int* radii,
+                   int debug, uint32_t numerics, void* stream) {
+    return forward_single(geometryBuffer, binningBuffer, imageBuffer, alloc_ctx, P, D, M, background, width,
+                          height, means3D, shs, colors_precomp, opacities, scales, scale_modifier, rotations,
+                          cov3D_precomp, viewmatrix, projmatrix, cam_pos, tan_fovx, tan_fovy, prefiltered,
+                          out_color, depth, antialiasing, radii, debug, nullptr, numerics, (hipStream_t)stream);
 }
 
 int64_t gsr_forward_async_bound(int P, int width, int height) {
@@ -353,27 +361,28 @@ int gsr_forward_async(gsr_alloc_fn geometryBuffer, gsr_alloc_fn binningBuffer, g
                       const float* rotations, const float* cov3D_precomp, const float* viewmatrix,
                       const float* projmatrix, const float* cam_pos, float tan_fovx, float tan_fovy,
                       int prefiltered, float* out_color, float* depth, int antialiasing, int* radii,
-                      int debug, uint32_t* status_host, void* stream) {
+                      int debug, uint32_t* status_host, uint32_t numerics, void* stream) {
     if (!status_host) return fail(GSR_ERR_ARG, "gsr_forward_async: null status_host");
     if (debug) return fail(GSR_ERR_ARG, "gsr_forward_async: debug mode synchronises; use gsr_forward");
     return forward_single(geometryBuffer, binningBuffer, imageBuffer, alloc_ctx, P, D, M, background, width,
                           height, means3D, shs, colors_precomp, opacities, scales, scale_modifier, rotations,
                           cov3D_precomp, viewmatrix, projmatrix, cam_pos, tan_fovx, tan_fovy, prefiltered,
-                          out_color, depth, antialiasing, radii, debug, status_host, (hipStream_t)stream);
+                          out_color, depth, antialiasing, radii, debug, status_host, numerics, (hipStream_t)stream);
 }
 
-int gsr_backward(int P, int D, int M, int R, const float* background, int width, int height,
-                 const float* means3D, const float* shs, const float* colors_precomp,
-                 const float* opacities, const float* scales, float scale_modifier,
-                 const float* rotations, const float* cov3D_precomp, const float* viewmatrix,
-                 const float* projmatrix, const float* campos, float tan_fovx, float tan_fovy,
-                 const int* radii, char* geom_buffer, char* binning_buffer, char* image_buffer,
-                 const float* dL_dpix, const float* dL_invdepths, float* dL_dmean2D,
-                 float* dL_dconic, float* dL_dopacity, float* dL_dcolor, float* dL_dinvdepth,
-                 float* dL_dmean3D, float* dL_dcov3D, float* dL_dsh, float* dL_dscale,
-                 float* dL_drot, int antialiasing, int debug, void* stream) {
+int gsr_backward_ex(int P, int D, int M, int R, const float* background, int width, int height,
+                    const float* means3D, const float* shs, const float* colors_precomp,
+                    const float* opacities, const float* scales, float scale_modifier,
+                    const float* rotations, const float* cov3D_precomp, const float* viewmatrix,
+                    const float* projmatrix, const float* campos, float tan_fovx, float tan_fovy,
+                    const int* radii, char* geom_buffer, char* binning_buffer, char* image_buffer,
+                    const float* dL_dpix, const float* dL_invdepths, float* dL_dmean2D,
+                    float* dL_dconic, float* dL_dopacity, float* dL_dcolor, float* dL_dinvdepth,
+                    float* dL_dmean3D, float* dL_dcov3D, float* dL_dsh, float* dL_dscale,
+                    float* dL_drot, int antialiasing, int debug, uint32_t numerics, void* stream) {
     (void)D; (void)M; (void)shs; (void)campos; (void)radii; (void)dL_dsh;
     hipStream_t s = (hipStream_t)stream;
+    if (numerics & ~kNumericsKnown) return fail(GSR_ERR_ARG, "unknown numerics flags");
     if (P <= 0) return 0;
     if (colors_precomp == nullptr)
         return fail(GSR_ERR_NO_COLORS, "For non-RGB, provide precomputed Gaussian colors!");
@@ -410,11 +419,29 @@ int gsr_backward(int P, int D, int M, int R, const float* background, int width,
     gr.dL_dcov3D = dL_dcov3D;
     gr.dL_dscale = (cov3D_precomp == nullptr) ? dL_dscale : nullptr;
     gr.dL_drot = (cov3D_precomp == nullptr) ? dL_drot : nullptr;
-    { StageTimer st_(7, s); launch_render_bwd(d, in, g, im, bn, gr, g_exact_exp != 0, g_split_bf16 != 0, s); }
+    { StageTimer st_(7, s); launch_render_bwd(d, in, g, im, bn, gr, exact_exp(numerics), split_bf16(numerics), s); }
     STAGE(debug, s, "render_bwd");
     { StageTimer st_(8, s); launch_preprocess_bwd(d, in, g, gr, s); }
     STAGE(debug, s, "preprocess_bwd");
     return 0;
+}
+
+int gsr_backward(int P, int D, int M, int R, const float* background, int width, int height,
+                 const float* means3D, const float* shs, const float* colors_precomp,
+                 const float* opacities, const float* scales, float scale_modifier,
+                 const float* rotations, const float* cov3D_precomp, const float* viewmatrix,
+                 const float* projmatrix, const float* campos, float tan_fovx, float tan_fovy,
+                 const int* radii, char* geom_buffer, char* binning_buffer, char* image_buffer,
+                 const float* dL_dpix, const float* dL_invdepths, float* dL_dmean2D,
+                 float* dL_dconic, float* dL_dopacity, float* dL_dcolor, float* dL_dinvdepth,
+                 float* dL_dmean3D, float* dL_dcov3D, float* dL_dsh, float* dL_dscale,
+                 float* dL_drot, int antialiasing, int debug, void* stream) {
+    return gsr_backward_ex(P, D, M, R, background, width, height, means3D, shs, colors_precomp, opacities,
+                           scales, scale_modifier, rotations, cov3D_precomp, viewmatrix, projmatrix, campos,
+                           tan_fovx, tan_fovy, radii, geom_buffer, binning_buffer, image_buffer, dL_dpix,
+                           dL_invdepths, dL_dmean2D, dL_dconic, dL_dopacity, dL_dcolor, dL_dinvdepth,
+                           dL_dmean3D, dL_dcov3D, dL_dsh, dL_dscale, dL_drot, antialiasing, debug,
+                           GSR_NUMERICS_EXACT, stream);
 }
 
 // Batch workspace: geometry | image | binning arenas, then 256 bytes of sticky status words
@@ -447,12 +474,12 @@ int gsr_forward_batch(int B, int P, int width, int height, const float* means3D,
                       float scale_modifier, const float* viewmatrices, const float* projmatrices,
                       const float* tanfov, const float* backgrounds, int64_t bg_stride,
                       char* workspace, int64_t R_capacity, float* out_color, float* out_invdepth,
-                      int* radii, int antialiasing, void* stream) {
+                      int* radii, int antialiasing, uint32_t numerics, void* stream) {
     return gsr_forward_batch_refine(B, P, width, height, means3D, means_stride, colors, colors_stride,
                                     opacities, opac_stride, scales, scales_stride, rotations, rot_stride,
                                     scale_modifier, viewmatrices, projmatrices, tanfov, backgrounds,
                                     bg_stride, workspace, R_capacity, out_color, out_invdepth, radii,
-                                    antialiasing, nullptr, stream);
+                                    antialiasing, nullptr, numerics, stream);
 }
 
 int gsr_forward_batch_refine(int B, int P, int width, int height, const float* means3D,
@@ -463,8 +490,9 @@ int gsr_forward_batch_refine(int B, int P, int width, int height, const float* m
                              const float* tanfov, const float* backgrounds, int64_t bg_stride,
                              char* workspace, int64_t R_capacity, float* out_color, float* out_invdepth,
                              int* radii, int antialiasing, const gsr_refine_epilogue* refine,
-                             void* stream) {
+                             uint32_t numerics, void* stream) {
     hipStream_t s = (hipStream_t)stream;
+    if (numerics & ~kNumericsKnown) return fail(GSR_ERR_ARG, "unknown numerics flags");
     if (refine) {
         if (!refine->out_refine || refine->n_out < 1 || refine->keep_channels < 0 ||
             refine->keep_channels + refine->n_out > GSR_C)
@@ -508,7 +536,7 @@ int gsr_forward_batch_refine(int B, int P, int width, int height, const float* m
     HIP_TRY(hipMemsetAsync(g.bstart, 0, (size_t)d.B * (d.NB + 1) * 4, s));
     { StageTimer st_(0, s); launch_preprocess(d, in, g, o, s); }
     { StageTimer st_(1, s); launch_scan_blocksums(d, g, R_capacity, s); }
-    int rc = run_binning_and_render(d, in, g, im, bn, o, 0, s);
+    int rc = run_binning_and_render(d, in, g, im, bn, o, numerics, 0, s);
     if (rc < 0) return rc;
     return 0;
 }
@@ -531,8 +559,10 @@ static int backward_batch(int B, int P, int width, int height, const float* mean
                           const float* scales, int64_t scales_stride, const float* rotations, int64_t rot_stride,
                           float scale_modifier, const float* viewmatrices, const float* projmatrices,
                           const float* tanfov, const float* backgrounds, int64_t bg_stride, char* workspace,
-                          int64_t R_capacity, const Grads& grads, int antialiasing, hipStream_t s) {
+                          int64_t R_capacity, const Grads& grads, int antialiasing, uint32_t numerics,
+                          hipStream_t s) {
     if (B <= 0 || P <= 0 || !workspace || !tanfov) return fail(GSR_ERR_ARG, "bad batch arguments");
+    if (numerics & ~kNumericsKnown) return fail(GSR_ERR_ARG, "unknown numerics flags");
     if (P >= kMaxGaussians) return fail(GSR_ERR_ARG, "P must be < 2^24");
     const Dims d = make_dims(B, P, width, height);
     GeomArena g;
@@ -551,7 +581,7 @@ static int backward_batch(int B, int P, int width, int height, const float* mean
     in.bg = backgrounds; in.s_bg = bg_stride;
     in.scale_mod = scale_modifier;
     in.antialiasing = antialiasing;
-    { StageTimer st_(7, s); launch_render_bwd(d, in, g, im, bn, grads, g_exact_exp != 0, g_split_bf16 != 0, s); }
+    { StageTimer st_(7, s); launch_render_bwd(d, in, g, im, bn, grads, exact_exp(numerics), split_bf16(numerics), s); }
     { StageTimer st_(8, s); launch_preprocess_bwd(d, in, g, grads, s); }
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return fail(GSR_ERR_HIP, std::string("backward_batch: ") + hipGetErrorString(e));
@@ -568,7 +598,7 @@ int gsr_backward_batch(int B, int P, int width, int height, const float* means3D
                        const float* dL_dinvdepth, float* dL_dmean2D, float* dL_dconic,
                        float* dL_dopacity, float* dL_dcolor, float* dL_dinvdepth_g,
                        float* dL_dmean3D, float* dL_dcov3D, float* dL_dscale, float* dL_drot,
-                       int antialiasing, void* stream) {
+                       int antialiasing, uint32_t numerics, void* stream) {
     if (!dL_dpix || !dL_dmean2D || !dL_dconic || !dL_dopacity || !dL_dcolor || !dL_dmean3D || !dL_dcov3D)
         return fail(GSR_ERR_ARG, "backward_batch: null gradient buffer");
     Grads gr{};
@@ -587,7 +617,7 @@ int gsr_backward_batch(int B, int P, int width, int height, const float* means3D
     return backward_batch(B, P, width, height, means3D, means_stride, colors, colors_stride, opacities,
                           opac_stride, scales, scales_stride, rotations, rot_stride, scale_modifier,
                           viewmatrices, projmatrices, tanfov, backgrounds, bg_stride, workspace, R_capacity, gr,
-                          antialiasing, (hipStream_t)stream);
+                          antialiasing, numerics, (hipStream_t)stream);
 }
 
 int gsr_backward_batch_shared(int B, int P, int width, int height, const float* means3D,
@@ -599,7 +629,7 @@ int gsr_backward_batch_shared(int B, int P, int width, int height, const float* 
                               char* workspace, int64_t R_capacity, const float* dL_dpix,
                               const float* dL_dinvdepth, float* dL_dopacity, float* dL_dcolor,
                               float* dL_dmean3D, float* dL_dscale, float* dL_drot, int antialiasing,
-                              void* stream) {
+                              uint32_t numerics, void* stream) {
     if (!dL_dpix || !dL_dopacity || !dL_dcolor || !dL_dmean3D || !dL_dscale || !dL_drot)
         return fail(GSR_ERR_ARG, "backward_batch_shared: null gradient buffer");
     if (!scales || !rotations) return fail(GSR_ERR_ARG, "backward_batch_shared: needs scales and rotations");
@@ -616,7 +646,7 @@ int gsr_backward_batch_shared(int B, int P, int width, int height, const float* 
     return backward_batch(B, P, width, height, means3D, means_stride, colors, colors_stride, opacities,
                           opac_stride, scales, scales_stride, rotations, rot_stride, scale_modifier,
                           viewmatrices, projmatrices, tanfov, backgrounds, bg_stride, workspace, R_capacity, gr,
-                          antialiasing, (hipStream_t)stream);
+                          antialiasing, numerics, (hipStream_t)stream);
 }
 
 int gsr_render_counters(uint64_t* device_counters) {

@@ -19,7 +19,10 @@ from .. import _lib
 
 NUM_CHANNELS = 32
 # binning buffers up to this size take the no-sync forward (gsr_forward_async); larger ones (big
-# images x many Gaussians) size the buffer from the synchronous R read-back as the reference does
+# images x many Gaussians) size the buffer from the synchronous R read-back as the reference does.
+# The no-sync forward's buffer is the P x tiles bound, so it is only used when nobody keeps the
+# buffer (exact_binning=False: inference -- GaussianRasterizer_32 under no_grad drops it with the
+# call); a forward whose buffers autograd saves for backward sizes it to the exact R.
 ASYNC_BINNING_MB = int(os.environ.get("GSR_ASYNC_BINNING_MB", "512"))
 
 
@@ -27,20 +30,28 @@ class PendingCount:
     """num_rendered of a forward that did not wait for the device (gsr_forward_async): reading it
     (int(), comparisons, arithmetic, printing) waits for that forward and raises the reference's
     errors (a culled point with prefiltered set, an instance count beyond 2^31 - 1) then."""
-    __slots__ = ("_status", "_event", "_value", "__weakref__")
+    __slots__ = ("_status", "_event", "_value", "_error", "__weakref__")
 
     def __init__(self, status, event):
-        self._status, self._event, self._value = status, event, None
+        self._status, self._event, self._value, self._error = status, event, None, None
 
-    def __int__(self):
-        if self._value is None:
+    def _resolve(self):
+        """Wait for the forward and take its status out of the (reused) pinned slot; an error is
+        kept for THIS count's readers, never raised into whoever triggered the resolution."""
+        if self._value is None and self._error is None:
             self._event.synchronize()
             r, ovf, err = (int(x) for x in self._status[:3].tolist())
             if err & 1:
-                raise RuntimeError("Point is filtered although prefiltered is set. This shouldn't happen!")
-            if ovf:
-                raise _lib.CapacityError("instance count exceeds 2^31 - 1 (num_rendered is an int)")
-            self._value = r
+                self._error = RuntimeError("Point is filtered although prefiltered is set. This shouldn't happen!")
+            elif ovf:
+                self._error = _lib.CapacityError("instance count exceeds 2^31 - 1 (num_rendered is an int)")
+            else:
+                self._value = r
+
+    def __int__(self):
+        self._resolve()
+        if self._error is not None:
+            raise self._error
         return self._value
 
     __index__ = __int__
@@ -118,7 +129,7 @@ class _StatusRing:
             ev, ref = prev
             pc = ref()
             if pc is not None:
-                int(pc)  # resolve it from this slot before the slot is rewritten
+                pc._resolve()  # take its status out of this slot before the slot is rewritten
             else:
                 ev.synchronize()
         ev = torch.cuda.Event()
@@ -168,9 +179,16 @@ class _Resizer:
 
 def rasterize_gaussians(background, means3D, colors, opacity, scales, rotations, scale_modifier,
                         cov3D_precomp, viewmatrix, projmatrix, tan_fovx, tan_fovy, image_height,
-                        image_width, sh, degree, campos, prefiltered, antialiasing, debug):
+                        image_width, sh, degree, campos, prefiltered, antialiasing, debug, *, numerics=0,
+                        exact_binning=False):
     """RasterizeGaussiansCUDA (rasterize_points.cu:36-124).  Returns
-    (num_rendered, color[32,H,W], radii[P] int32, geomBuffer, binningBuffer, imgBuffer, invdepth[1,H,W])."""
+    (num_rendered, color[32,H,W], radii[P] int32, geomBuffer, binningBuffer, imgBuffer, invdepth[1,H,W]).
+    numerics (keyword only, not in the reference): the call's GSR_NUMERICS_* flags (_lib.numerics());
+    the default 0 is bit-identical to the CPU oracle.
+    exact_binning (keyword only): size binningBuffer to the exact instance count after a host read-back
+    of num_rendered (the reference's behaviour, rasterizer_impl.cu:279-291) -- for buffers kept until
+    backward.  Otherwise (default) the forward does not wait for the device: binningBuffer is the
+    P x tiles bound (4 B per possible instance; R cannot exceed it) and num_rendered a PendingCount."""
     if means3D.ndimension() != 2 or means3D.size(1) != 3:
         raise RuntimeError("means3D must have dimensions (num_points, 3)")
     P = int(means3D.size(0))
@@ -211,26 +229,28 @@ def rasterize_gaussians(background, means3D, colors, opacity, scales, rotations,
                 int(bool(antialiasing)), radii.data_ptr(), int(bool(debug)))
         bound = L.gsr_forward_async_bound(P, W, H)
         with torch.cuda.device(dev):
-            if not debug and bound < 0x7FFFFFFF and 4 * bound <= ASYNC_BINNING_MB << 20:
+            if not debug and not exact_binning and bound < 0x7FFFFFFF and 4 * bound <= ASYNC_BINNING_MB << 20:
                 ring = _RINGS.get(dev)
                 if ring is None:
                     ring = _RINGS[dev] = _StatusRing()
                 status, ev, k = ring.take(dev)
-                _lib.check(L.gsr_forward_async(*args, status.data_ptr(), _stream(dev)), "rasterize_gaussians")
+                _lib.check(L.gsr_forward_async(*args, status.data_ptr(), int(numerics), _stream(dev)),
+                           "rasterize_gaussians")
                 ev.record(torch.cuda.current_stream(dev))
                 rendered = PendingCount(status, ev)
                 ring.bind(k, ev, rendered)
             else:
-                rendered = _lib.check(L.gsr_forward(*args, _stream(dev)), "rasterize_gaussians")
+                rendered = _lib.check(L.gsr_forward_ex(*args, int(numerics), _stream(dev)), "rasterize_gaussians")
     return rendered, out_color, radii, geom.t, binning.t, img.t, out_invdepth
 
 
 def rasterize_gaussians_backward(background, means3D, radii, colors, opacities, scales, rotations,
                                  scale_modifier, cov3D_precomp, viewmatrix, projmatrix, tan_fovx,
                                  tan_fovy, dL_dout_color, dL_dout_invdepth, sh, degree, campos,
-                                 geomBuffer, R, binningBuffer, imageBuffer, antialiasing, debug):
+                                 geomBuffer, R, binningBuffer, imageBuffer, antialiasing, debug, *, numerics=0):
     """RasterizeGaussiansBackwardCUDA (rasterize_points.cu:127-223).  Returns
-    (dL_dmeans2D, dL_dcolors, dL_dopacity, dL_dmeans3D, dL_dcov3D, dL_dsh, dL_dscales, dL_drotations)."""
+    (dL_dmeans2D, dL_dcolors, dL_dopacity, dL_dmeans3D, dL_dcov3D, dL_dsh, dL_dscales, dL_drotations).
+    numerics: as rasterize_gaussians."""
     P = int(means3D.size(0))
     H = int(dL_dout_color.size(1))
     W = int(dL_dout_color.size(2))
@@ -266,7 +286,7 @@ def rasterize_gaussians_backward(background, means3D, radii, colors, opacities, 
         viewmatrix = _dev_f32(viewmatrix, dev, "viewmatrix")
         projmatrix = _dev_f32(projmatrix, dev, "projmatrix")
         with torch.cuda.device(dev):
-            rc = L.gsr_backward(
+            rc = L.gsr_backward_ex(
                 P, int(degree), M, int(R), _ptr(background), W, H, _ptr(means3D), _ptr(sh),
                 _ptr(colors), _ptr(opacities), _ptr(scales), float(scale_modifier), _ptr(rotations),
                 _ptr(cov3D_precomp), _ptr(viewmatrix), _ptr(projmatrix), _ptr(campos),
@@ -275,7 +295,7 @@ def rasterize_gaussians_backward(background, means3D, radii, colors, opacities, 
                 dL_dconic.data_ptr(), dL_dopacity.data_ptr(), dL_dcolors.data_ptr(),
                 _ptr(dL_dinvdepths), dL_dmeans3D.data_ptr(), dL_dcov3D.data_ptr(), _ptr(dL_dsh),
                 dL_dscales.data_ptr(), dL_drotations.data_ptr(), int(bool(antialiasing)),
-                int(bool(debug)), _stream(dev))
+                int(bool(debug)), int(numerics), _stream(dev))
         _lib.check(rc, "rasterize_gaussians_backward")
     return (dL_dmeans2D, dL_dcolors, dL_dopacity, dL_dmeans3D, dL_dcov3D, dL_dsh, dL_dscales,
             dL_drotations)

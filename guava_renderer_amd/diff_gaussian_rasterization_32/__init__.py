@@ -37,14 +37,20 @@ def cpu_deep_copy_tuple(input_tuple):
 
 def rasterize_gaussians(means3D, means2D, sh, colors_precomp, opacities, scales, rotations,
                         cov3Ds_precomp, raster_settings):
+    # whether autograd will keep this call's scratch buffers for backward (known only here: the
+    # Function's forward runs with grad mode off): then the binning buffer is sized to the exact
+    # instance count (the reference's host read-back of num_rendered), otherwise the forward runs
+    # without a host synchronisation and its transient buffer is released with the call
+    inputs = (means3D, means2D, sh, colors_precomp, opacities, scales, rotations, cov3Ds_precomp)
+    record = torch.is_grad_enabled() and any(isinstance(t, torch.Tensor) and t.requires_grad for t in inputs)
     return _RasterizeGaussians.apply(means3D, means2D, sh, colors_precomp, opacities, scales,
-                                     rotations, cov3Ds_precomp, raster_settings)
+                                     rotations, cov3Ds_precomp, raster_settings, record)
 
 
 class _RasterizeGaussians(torch.autograd.Function):
     @staticmethod
     def forward(ctx, means3D, means2D, sh, colors_precomp, opacities, scales, rotations,
-                cov3Ds_precomp, raster_settings):
+                cov3Ds_precomp, raster_settings, _for_backward=True):
         # argument order of the native call (reference __init__.py:60-81)
         args = (
             raster_settings.bg,
@@ -69,7 +75,7 @@ class _RasterizeGaussians(torch.autograd.Function):
             raster_settings.debug,
         )
         num_rendered, color, radii, geomBuffer, binningBuffer, imgBuffer, invdepths = \
-            _C.rasterize_gaussians(*args)
+            _C.rasterize_gaussians(*args, exact_binning=bool(_for_backward))
         ctx.raster_settings = raster_settings
         ctx.num_rendered = num_rendered
         ctx.save_for_backward(colors_precomp, means3D, scales, rotations, cov3Ds_precomp, radii, sh,
@@ -117,6 +123,7 @@ class _RasterizeGaussians(torch.autograd.Function):
             grad_scales,
             grad_rotations,
             grad_cov3Ds_precomp,
+            None,
             None,
         )
         return grads

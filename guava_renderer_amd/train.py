@@ -3,12 +3,14 @@
 One step over the B frames of this rank (main/trainer.py:82-102 does, per iteration: render the
 batch, Optimization_Loss, fabric.backward -> DDP gradient all-reduce, Adam step):
   1. BatchRasterizer.forward of the shared Gaussian attributes for B cameras (one launch set);
-  2. loss = (1 - lambda) * L1 + lambda * (1 - fused_ssim) of the raw RGB channels (the reference's
-     raw_renders term, utils/loss_utils.py:116-119; fused_ssim HIP kernels) + L1 of a refined image
+  2. loss = (1 - lambda) * L1 + lambda * (1 - fused_ssim) of the raw RGB channels + L1 of a refined image
      made from ALL 32 channels (the reference's `renders` term, :92; its StyleUNet refiner is out
      of scope, so a fixed random 1x1 conv 32 -> 3 stands in), so every feature channel carries a
      gradient into the rasterizer backward as in the reference's training; the L1 terms and the
-     gradient assembly are one gfx950 pass (gsr_image_loss);
+     gradient assembly are one gfx950 pass (gsr_image_loss).  The reference's raw_renders term
+     (utils/loss_utils.py:116-119) is lambda_l1 * L1 + an LPIPS perceptual term; LPIPS (AlexNet with
+     weights fetched from a URL) is out of scope, and fused-SSIM -- the reference's own native loss
+     kernel, BASELINE config 4 -- stands in for that perceptual term;
   3. BatchRasterizer.backward(shared=True) (render_bwd + cov/preprocess backward kernels) -> the
      shared attributes' gradients [P,k], summed over the frames inside the kernels (no [B,P,k]
      buffers);
@@ -40,14 +42,16 @@ C = 32
 
 
 class SplatTrainer:
-    def __init__(self, params, B, W, H, R_capacity, device="cuda", lr=1e-3, lambda_ssim=0.2, refine_head=True):
+    def __init__(self, params, B, W, H, R_capacity, device="cuda", lr=1e-3, lambda_ssim=0.2, refine_head=True,
+                 numerics=0):
         """params: dict of float32 device tensors means3D [P,3], colors [P,32], opacities [P,1],
         scales [P,3], rotations [P,4] (made leaves with requires_grad).  refine_head=False: the loss
-        sees the RGB channels only."""
+        sees the RGB channels only.  numerics: the rasterizer calls' GSR_NUMERICS_* flags."""
         self.dev = torch.device(device)
         self.p = {k: v.detach().clone().contiguous().requires_grad_(True) for k, v in params.items()}
         P = self.p["means3D"].shape[0]
-        self.rast = BatchRasterizer(B, P, W, H, R_capacity=R_capacity, device=self.dev)
+        self.numerics = int(numerics)
+        self.rast = BatchRasterizer(B, P, W, H, R_capacity=R_capacity, device=self.dev, numerics=self.numerics)
         self.opt = torch.optim.Adam(list(self.p.values()), lr=lr, fused=True)
         self.skipped_steps = 0
         self.B, self.W, self.H = B, W, H
@@ -66,12 +70,16 @@ class SplatTrainer:
         old = self.rast
         cap = max(int(old.max_instances_seen() * 1.5), 2 * old.R_capacity) + 1024
         warnings.warn(f"SplatTrainer: {err}; step skipped, R capacity {old.R_capacity} -> {cap}")
-        self.rast = BatchRasterizer(old.B, old.P, old.W, old.H, R_capacity=cap, device=self.dev)
+        self.rast = BatchRasterizer(old.B, old.P, old.W, old.H, R_capacity=cap, device=self.dev,
+                                    numerics=self.numerics)
         del old
 
     def gradients(self, views, projs, tanf, target):
         """Forward + loss + backward of one step: (loss, dict of the attributes' gradients summed
         over this rank's frames), before any all-reduce or update."""
+        want = (self.B, 3, self.H, self.W)
+        if tuple(target.shape) != want or target.device != self.dev:
+            raise ValueError(f"target: expected {list(want)} on {self.dev}, got {list(target.shape)} on {target.device}")
         try:
             self.rast.poll()
         except _lib.CapacityError as e:

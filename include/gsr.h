@@ -51,18 +51,22 @@ typedef char* (*gsr_alloc_fn)(void* ctx, size_t bytes);
 const char* gsr_version(void);
 const char* gsr_last_error(void);
 
-/* Blend exponent: 1 = deterministic polynomial exp, bit-identical to the CPU oracle (default);
- * 0 = hardware v_exp_f32.  Returns the previous setting. */
-int gsr_set_exact_exp(int on);
-
-/* Colour accumulation of the forward blend: 0 = f32 MFMA, bit-identical to the reference's
- * fmaf chain (default); 1 = split-bf16 MFMA (f = f_hi + f_lo, four exact bf16 products per
- * feature x weight, f32 accumulation): <= 3e-5 relative per product, colour L-inf within the
- * north_star's 1e-4; final_T, n_contrib and inverse depth stay bit-exact.  Returns the previous
- * setting.  The same switch puts the backward's two contractions (g = f . dL/dpixel and
- * dL/dcolor = sum_px w dL/dpixel) on split-bf16 MFMAs; gradients stay within 1e-4 of their scale.
- * No reference counterpart (forward.cu:371-372 accumulates in f32). */
-int gsr_set_split_bf16(int on);
+/* Numerics of ONE call (bit flags, the `numerics` argument of the *_ex / async / batch entry points;
+ * there is no process-wide mode).  GSR_NUMERICS_EXACT (0) is what the reference-signature entry
+ * points gsr_forward / gsr_backward use: bit-identical to the CPU oracle.
+ *   GSR_NUMERICS_FAST_EXP: the blend exponent on the hardware v_exp_f32 instead of the
+ *     deterministic polynomial (alpha thresholds can flip on rare pixels).
+ *   GSR_NUMERICS_SPLIT_BF16: colour accumulation of the forward blend as split-bf16 MFMAs
+ *     (f = f_hi + f_lo, four exact bf16 products per feature x weight, f32 accumulation):
+ *     <= 3e-5 relative per product, colour L-inf within the north_star's 1e-4; final_T,
+ *     n_contrib and inverse depth stay bit-exact.  In the backward the same flag puts the two
+ *     contractions (g = f . dL/dpixel, dL/dcolor = sum_px w dL/dpixel) on split-bf16 MFMAs;
+ *     gradients stay within 1e-4 of their scale.  No reference counterpart (forward.cu:371-372
+ *     accumulates in f32).
+ * Unknown bits are rejected (GSR_ERR_ARG). */
+#define GSR_NUMERICS_EXACT 0u
+#define GSR_NUMERICS_FAST_EXP 1u
+#define GSR_NUMERICS_SPLIT_BF16 2u
 
 /* Scratch sizes used by gsr_forward (the three resizer requests).  Unlike the reference's
  * GeometryState, the geometry arena also holds the per-frame depth sort and the (depth chunk x tile)
@@ -86,6 +90,15 @@ int gsr_forward(gsr_alloc_fn geometryBuffer, gsr_alloc_fn binningBuffer, gsr_all
                 const float* projmatrix, const float* cam_pos, float tan_fovx, float tan_fovy,
                 int prefiltered, float* out_color, float* depth, int antialiasing, int* radii,
                 int debug, void* stream);
+/* gsr_forward with explicit per-call numerics (GSR_NUMERICS_*). */
+int gsr_forward_ex(gsr_alloc_fn geometryBuffer, gsr_alloc_fn binningBuffer, gsr_alloc_fn imageBuffer,
+                   void* alloc_ctx, int P, int D, int M, const float* background, int width, int height,
+                   const float* means3D, const float* shs, const float* colors_precomp,
+                   const float* opacities, const float* scales, float scale_modifier,
+                   const float* rotations, const float* cov3D_precomp, const float* viewmatrix,
+                   const float* projmatrix, const float* cam_pos, float tan_fovx, float tan_fovy,
+                   int prefiltered, float* out_color, float* depth, int antialiasing, int* radii,
+                   int debug, uint32_t numerics, void* stream);
 
 /* gsr_forward without the host synchronisation after the scan (the reference reads num_rendered
  * back before sizing the binning buffer, rasterizer_impl.cu:279-291 of the reference driver):
@@ -103,7 +116,7 @@ int gsr_forward_async(gsr_alloc_fn geometryBuffer, gsr_alloc_fn binningBuffer, g
                       const float* rotations, const float* cov3D_precomp, const float* viewmatrix,
                       const float* projmatrix, const float* cam_pos, float tan_fovx, float tan_fovy,
                       int prefiltered, float* out_color, float* depth, int antialiasing, int* radii,
-                      int debug, uint32_t* status_host, void* stream);
+                      int debug, uint32_t* status_host, uint32_t numerics, void* stream);
 
 /* Rasterizer::backward.  Gradient buffers are accumulated into and must be zeroed by the caller
  * (the reference's torch::zeros, rasterize_points.cu:163-179): dL_dmean2D [P,3], dL_dconic [P,4],
@@ -120,6 +133,17 @@ int gsr_backward(int P, int D, int M, int R, const float* background, int width,
                  float* dL_dconic, float* dL_dopacity, float* dL_dcolor, float* dL_dinvdepth,
                  float* dL_dmean3D, float* dL_dcov3D, float* dL_dsh, float* dL_dscale,
                  float* dL_drot, int antialiasing, int debug, void* stream);
+/* gsr_backward with explicit per-call numerics (GSR_NUMERICS_*). */
+int gsr_backward_ex(int P, int D, int M, int R, const float* background, int width, int height,
+                    const float* means3D, const float* shs, const float* colors_precomp,
+                    const float* opacities, const float* scales, float scale_modifier,
+                    const float* rotations, const float* cov3D_precomp, const float* viewmatrix,
+                    const float* projmatrix, const float* campos, float tan_fovx, float tan_fovy,
+                    const int* radii, char* geom_buffer, char* binning_buffer, char* image_buffer,
+                    const float* dL_dpix, const float* dL_invdepths, float* dL_dmean2D,
+                    float* dL_dconic, float* dL_dopacity, float* dL_dcolor, float* dL_dinvdepth,
+                    float* dL_dmean3D, float* dL_dcov3D, float* dL_dsh, float* dL_dscale,
+                    float* dL_drot, int antialiasing, int debug, uint32_t numerics, void* stream);
 
 /* ---- batched multi-frame path (B frames, one launch per stage, capture-safe) ----
  * Per-frame inputs use an element stride between frames (0 = shared by every frame).
@@ -137,7 +161,7 @@ int gsr_forward_batch(int B, int P, int width, int height, const float* means3D,
                       float scale_modifier, const float* viewmatrices, const float* projmatrices,
                       const float* tanfov, const float* backgrounds, int64_t bg_stride,
                       char* workspace, int64_t R_capacity, float* out_color, float* out_invdepth,
-                      int* radii, int antialiasing, void* stream);
+                      int* radii, int antialiasing, uint32_t numerics, void* stream);
 int gsr_backward_batch(int B, int P, int width, int height, const float* means3D,
                        int64_t means_stride, const float* colors, int64_t colors_stride,
                        const float* opacities, int64_t opac_stride, const float* scales,
@@ -148,7 +172,7 @@ int gsr_backward_batch(int B, int P, int width, int height, const float* means3D
                        const float* dL_dinvdepth, float* dL_dmean2D, float* dL_dconic,
                        float* dL_dopacity, float* dL_dcolor, float* dL_dinvdepth_g,
                        float* dL_dmean3D, float* dL_dcov3D, float* dL_dscale, float* dL_drot,
-                       int antialiasing, void* stream);
+                       int antialiasing, uint32_t numerics, void* stream);
 
 /* gsr_backward_batch for Gaussian attributes SHARED by the B frames (one avatar seen from B
  * cameras, the training batch of main/trainer.py:82-102): the attribute gradients come back summed
@@ -165,7 +189,7 @@ int gsr_backward_batch_shared(int B, int P, int width, int height, const float* 
                               char* workspace, int64_t R_capacity, const float* dL_dpix,
                               const float* dL_dinvdepth, float* dL_dopacity, float* dL_dcolor,
                               float* dL_dmean3D, float* dL_dscale, float* dL_drot, int antialiasing,
-                              void* stream);
+                              uint32_t numerics, void* stream);
 /* Refiner-head epilogue: GaussianRenderer feeds the 32-channel render to the
  * StyleUNet refiner (gaussian_render.py:73), whose first layer is a 1x1 conv 32 -> 16 + leaky ReLU
  * (styleunet.py:110,178).  The conv is linear in the features, so it commutes with compositing:
@@ -199,7 +223,7 @@ int gsr_forward_batch_refine(int B, int P, int width, int height, const float* m
                              const float* tanfov, const float* backgrounds, int64_t bg_stride,
                              char* workspace, int64_t R_capacity, float* out_color, float* out_invdepth,
                              int* radii, int antialiasing, const gsr_refine_epilogue* refine,
-                             void* stream);
+                             uint32_t numerics, void* stream);
 /* Stage timing with HIP events recorded on the launch stream around each stage whose bit is set in
  * `stage_mask` (bit i = stage i: 0 preprocess, 1 block scan, 2 depth sort, 3 chunk count,
  * 4 tile scan, 5 ordered scatter, 6 render fwd, 7 render bwd, 8 preprocess bwd); 0 disables.
@@ -234,6 +258,13 @@ size_t gsr_batch_status_offset(int B, int P, int width, int height, int64_t R_ca
 /* Synchronises `stream`; writes the batch's instance count and overflow flag. */
 int gsr_batch_status(const char* workspace, int B, int P, int64_t* R_total, int* overflow,
                      void* stream);
+
+/* Consumer-side frame encoding for the multi-GPU frame exchange: the first
+ * `channels` planes of B frames [.., H, W] (frame i at src + i * frame_stride floats) ->
+ * dst [B][channels][H][W] uint8 = (uint8)(255 * clip(x, 0, 1)), GUAVA's to8b
+ * (utils/general_utils.py:316-317, applied to every rendered frame at main/test.py:85); NaN -> 0. */
+int gsr_frames_to8b(int B, int channels, int height, int width, const float* src, int64_t frame_stride,
+                    uint8_t* dst, void* stream);
 
 #ifdef __cplusplus
 }

@@ -101,7 +101,7 @@ def torch_inputs(d, device="cuda", requires_grad=False):
     return t
 
 
-def gpu_forward(d, antialiasing=False, use_cov=None, debug=False):
+def gpu_forward(d, antialiasing=False, use_cov=None, debug=False, numerics=0):
     """Runs _C.rasterize_gaussians; returns numpy outputs plus decoded scratch state."""
     import torch
     from guava_renderer_amd.diff_gaussian_rasterization_32 import _C
@@ -113,7 +113,7 @@ def gpu_forward(d, antialiasing=False, use_cov=None, debug=False):
     R, color, radii, gb, bb, ib, invd = _C.rasterize_gaussians(
         t["bg"], t["means3D"], t["colors"], t["opacities"], scales, rots, 1.0, cov,
         t["viewmatrix"], t["projmatrix"], d["tanfovx"], d["tanfovy"], d["image_height"],
-        d["image_width"], empty, 0, t["campos"], False, antialiasing, debug)
+        d["image_width"], empty, 0, t["campos"], False, antialiasing, debug, numerics=numerics)
     torch.cuda.synchronize()
     P = d["means3D"].shape[0]
     W, H = d["image_width"], d["image_height"]

@@ -85,11 +85,10 @@ def test_rejects_malformed(tmp_path):
 def test_ply_avatar_renders_like_oracle(tmp_path):
     import torch
 
-    from guava_renderer_amd import _lib, camera
+    from guava_renderer_amd import camera
     from guava_renderer_amd.batch import BatchRasterizer
     from helpers import oracle_forward
 
-    _lib.set_exact_exp(True)
     d = scenes.avatar_cloud(6000, 1)
     p = tmp_path / "GS_canonical.ply"
     avatar_io.write_gaussian_ply(p, d["means3D"], d["colors"][:, :3], d["opacities"], d["scales"], d["rotations"])

@@ -38,11 +38,16 @@ def test_scratch_sizes_grow_with_work():
     assert L.gsr_batch_workspace_bytes(4, 1000, 64, 64, 10 ** 4) > L.gsr_batch_workspace_bytes(1, 1000, 64, 64, 10 ** 4)
 
 
-def test_exact_exp_toggle():
+def test_numerics_flags():
+    """Numerics are per call (include/gsr.h GSR_NUMERICS_*): no process-wide setter exists."""
     from guava_renderer_amd import _lib
-    prev = _lib.set_exact_exp(False)
-    assert _lib.set_exact_exp(True) == 0
-    _lib.set_exact_exp(bool(prev) or True)
+    assert _lib.numerics() == _lib.NUMERICS_EXACT == 0
+    assert _lib.numerics(fast_exp=True) == 1 and _lib.numerics(split_bf16=True) == 2
+    assert _lib.numerics(True, True) == 3
+    L = _lib.load()
+    for name in ("gsr_set_exact_exp", "gsr_set_split_bf16"):
+        with pytest.raises(AttributeError):
+            getattr(L, name)
 
 
 def test_python_surface_matches_reference():
@@ -57,8 +62,16 @@ def test_python_surface_matches_reference():
     assert list(inspect.signature(m.rasterize_gaussians).parameters) == [
         "means3D", "means2D", "sh", "colors_precomp", "opacities", "scales", "rotations",
         "cov3Ds_precomp", "raster_settings"]
-    assert len(inspect.signature(_C.rasterize_gaussians).parameters) == 20
-    assert len(inspect.signature(_C.rasterize_gaussians_backward).parameters) == 24
+    def positional(f):
+        return [p for p in inspect.signature(f).parameters.values() if p.kind != p.KEYWORD_ONLY]
+
+    def keyword_only(f):
+        return [p.name for p in inspect.signature(f).parameters.values() if p.kind == p.KEYWORD_ONLY]
+    assert len(positional(_C.rasterize_gaussians)) == 20
+    assert len(positional(_C.rasterize_gaussians_backward)) == 24
+    # extensions beyond the reference are keyword-only with defaults (reference callers unaffected)
+    assert keyword_only(_C.rasterize_gaussians) == ["numerics", "exact_binning"]
+    assert keyword_only(_C.rasterize_gaussians_backward) == ["numerics"]
     assert len(inspect.signature(_C.mark_visible).parameters) == 3
 
 

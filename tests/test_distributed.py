@@ -63,6 +63,14 @@ def _worker(rank, world, port, n_frames, q):
                 got = fg.wait()
                 want = _fake_render([step * n_frames + f for f in range(n_frames)])
                 ok_stream = ok_stream and torch.equal(got, want)
+            # the 8-bit exchange (bench.py's default at N>1): uint8 frames as the consumer writes them
+            f8 = parallel.FrameGather(len(frames), (3, 4, 4), torch.uint8, torch.device("cpu"))
+            for step in range(3):
+                ids = [step * n_frames + f for f in frames]
+                f8.push((_fake_render(ids)[:, :3] % 251).to(torch.uint8))
+                got = f8.wait()
+                want = (_fake_render([step * n_frames + f for f in range(n_frames)])[:, :3] % 251).to(torch.uint8)
+                ok_stream = ok_stream and got.dtype == torch.uint8 and torch.equal(got, want)
         q.put((rank, ok_gather, ok_reduce and ok_stream))
     finally:
         dist.destroy_process_group()
@@ -82,3 +90,31 @@ def test_gather_and_reduce_world2(n_frames):
         assert p.exitcode == 0
     assert sorted(r[0] for r in res) == [0, 1]
     assert all(r[1] and r[2] for r in res), res
+
+
+def test_bench_rank_launch_contract(monkeypatch):
+    """bench.py --gpus N starts its own N ranks (torch.distributed.run as a child process, rendezvous
+    on 127.0.0.1) when no launcher set WORLD_SIZE, and refuses a launcher world that differs from N."""
+    import subprocess
+    import sys as _sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, WORLD_SIZE="1")
+    r = subprocess.run([_sys.executable, os.path.join(root, "bench.py"), "--gpus", "2"], env=env,
+                       capture_output=True, text=True, timeout=120)
+    assert r.returncode == 2 and "WORLD_SIZE=1" in r.stderr
+    _sys.path.insert(0, root)
+    import bench
+    seen = {}
+
+    class Done:
+        returncode = 0
+
+    def fake_run(cmd, *a, **k):
+        seen["cmd"] = cmd
+        return Done()
+    monkeypatch.setattr(bench.subprocess, "run", fake_run)
+    monkeypatch.setattr(_sys, "argv", ["bench.py", "--gpus", "4", "--steps", "7"])
+    assert bench._launch_ranks(4) == 0
+    cmd = seen["cmd"]
+    assert cmd[1:3] == ["-m", "torch.distributed.run"] and "--nproc-per-node=4" in cmd
+    assert "--master-addr=127.0.0.1" in cmd and cmd[-4:] == ["--gpus", "4", "--steps", "7"]

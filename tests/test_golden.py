@@ -51,9 +51,7 @@ def test_oracle_reproduces_golden(name):
 def test_gpu_matches_golden(name):
     import torch
     from helpers import gpu_forward, torch_inputs
-    from guava_renderer_amd import _lib
     from guava_renderer_amd.diff_gaussian_rasterization_32 import _C
-    _lib.set_exact_exp(True)
     d, g = _scene(name)
     W, H = d["image_width"], d["image_height"]
     col, radii, invd, st = gpu_forward(d)

@@ -159,3 +159,61 @@ def test_async_forward_equals_synchronous_forward(monkeypatch):
     assert isinstance(Rs, int) and int(Ra) == Rs and Ra == Rs and Rs > 0
     assert torch.equal(ca, cs) and torch.equal(ra, rs) and torch.equal(ia, is_)
     assert bba.numel() >= bbs.numel()
+
+
+def test_binning_buffer_sizes():
+    """The binning buffer autograd keeps for backward is sized to the exact instance count (as the
+    reference's read-back of num_rendered does); the no-sync inference forward's P x tiles buffer
+    is never saved (GaussianRasterizer_32 under no_grad keeps no context)."""
+    import diff_gaussian_rasterization_32 as m
+    from guava_renderer_amd import _lib, camera, scenes
+    from guava_renderer_amd.diff_gaussian_rasterization_32 import _C
+    d = scenes.avatar_cloud(20000, seed=5)
+    cam = camera.camera(200, 136)
+    t = lambda x: torch.tensor(np.ascontiguousarray(x), device="cuda")  # noqa: E731
+    empty = torch.Tensor([])
+    args = (t(np.zeros(32, np.float32)), t(d["means3D"]), t(d["colors"]), t(d["opacities"]), t(d["scales"]),
+            t(d["rotations"]), 1.0, empty, t(cam["viewmatrix"]), t(cam["projmatrix"]), cam["tanfovx"],
+            cam["tanfovy"], 136, 200, empty, 0, t(np.zeros(3, np.float32)), False, False, False)
+    R, _, _, _, bb, _, _ = _C.rasterize_gaussians(*args, exact_binning=True)
+    assert isinstance(R, int) and R > 0
+    assert bb.numel() == _lib.load().gsr_binning_bytes(R) <= 4 * R + 512
+    # the drop-in autograd path: the buffer saved in ctx is the exact one
+    means3D = t(d["means3D"]).requires_grad_(True)
+    s = m.GaussianRasterizationSettings(136, 200, cam["tanfovx"], cam["tanfovy"], t(np.zeros(32, np.float32)), 1.0,
+                                        t(cam["viewmatrix"]), t(cam["projmatrix"]), 0, t(np.zeros(3, np.float32)),
+                                        False, False, False)
+    color, radii, _ = m.rasterize_gaussians(means3D, torch.zeros_like(means3D), empty, t(d["colors"]),
+                                            t(d["opacities"]), t(d["scales"]), t(d["rotations"]), empty, s)
+    saved = color.grad_fn.saved_tensors
+    assert saved[9].numel() == bb.numel()  # binningBuffer
+    assert isinstance(color.grad_fn.num_rendered, int) and color.grad_fn.num_rendered == R
+    color.sum().backward()
+    assert torch.isfinite(means3D.grad).all()
+    # no graph: the no-sync path, whose count resolves to the same R
+    with torch.no_grad():
+        Ra, _, _, _, bba, _, _ = _C.rasterize_gaussians(*args)
+    assert isinstance(Ra, _C.PendingCount) and int(Ra) == R and bba.numel() >= bb.numel()
+
+
+def test_deferred_error_stays_with_its_count():
+    """A prefiltered forward with a culled point (the reference's __trap) raises from its own
+    num_rendered, not from a later, unrelated call that reuses its status slot."""
+    from guava_renderer_amd import camera, scenes
+    from guava_renderer_amd.diff_gaussian_rasterization_32 import _C
+    d = scenes.random_cloud(500, seed=2)
+    cam = camera.camera(64, 48)
+    d["means3D"][0] = 3.0 * cam["campos"]  # behind the camera (it looks at the origin): culled
+    t = lambda x: torch.tensor(np.ascontiguousarray(x), device="cuda")  # noqa: E731
+    empty = torch.Tensor([])
+
+    def args(prefiltered):
+        return (t(np.zeros(32, np.float32)), t(d["means3D"]), t(d["colors"]), t(d["opacities"]), t(d["scales"]),
+                t(d["rotations"]), 1.0, empty, t(cam["viewmatrix"]), t(cam["projmatrix"]), cam["tanfovx"],
+                cam["tanfovy"], 48, 64, empty, 0, t(np.zeros(3, np.float32)), prefiltered, False, False)
+    bad = _C.rasterize_gaussians(*args(True))[0]
+    ring = next(iter(_C._RINGS.values()))
+    for _ in range(ring.buf.shape[0] + 2):  # wrap the ring: every slot, the bad one included, is reused
+        int(_C.rasterize_gaussians(*args(False))[0])
+    with pytest.raises(RuntimeError, match="prefiltered"):
+        int(bad)

@@ -16,7 +16,7 @@ pytestmark = pytest.mark.gpu
 NAMES = ("means2D", "colors", "opacity", "means3D", "cov3D", "sh", "scales", "rotations")
 
 
-def _gpu_backward(d, dL, dLinv, antialiasing=False, use_cov=None):
+def _gpu_backward(d, dL, dLinv, antialiasing=False, use_cov=None, numerics=0):
     from guava_renderer_amd.diff_gaussian_rasterization_32 import _C
     t = torch_inputs(d)
     empty = torch.Tensor([])
@@ -26,13 +26,13 @@ def _gpu_backward(d, dL, dLinv, antialiasing=False, use_cov=None):
     R, color, radii, gb, bb, ib, invd = _C.rasterize_gaussians(
         t["bg"], t["means3D"], t["colors"], t["opacities"], scales, rots, 1.0, cov,
         t["viewmatrix"], t["projmatrix"], d["tanfovx"], d["tanfovy"], d["image_height"],
-        d["image_width"], empty, 0, t["campos"], False, antialiasing, False)
+        d["image_width"], empty, 0, t["campos"], False, antialiasing, False, numerics=numerics)
     dLt = torch.tensor(dL, device="cuda")
     dLi = torch.tensor(dLinv, device="cuda") if dLinv is not None else torch.zeros((0, 1), device="cuda")
     grads = _C.rasterize_gaussians_backward(
         t["bg"], t["means3D"], radii, t["colors"], t["opacities"], scales, rots, 1.0, cov,
         t["viewmatrix"], t["projmatrix"], d["tanfovx"], d["tanfovy"], dLt, dLi, empty, 0, t["campos"],
-        gb, R, bb, ib, antialiasing, False)
+        gb, R, bb, ib, antialiasing, False, numerics=numerics)
     torch.cuda.synchronize()
     return [g.cpu().numpy() for g in grads]
 
@@ -74,18 +74,14 @@ def test_backward_matches_oracle(kind, P, W, H, seed):
 
 @pytest.mark.parametrize("kind,P,W,H,seed", [("random", 2000, 96, 64, 1), ("avatar", 12000, 128, 128, 3)])
 def test_backward_split_bf16_matches_oracle(kind, P, W, H, seed):
-    """gsr_set_split_bf16(1): the backward's g = f . dL/dpixel contraction on split-bf16 MFMAs (the
+    """GSR_NUMERICS_SPLIT_BF16: the backward's g = f . dL/dpixel contraction on split-bf16 MFMAs (the
     single-frame feature table pre-split by k_split_features) -- same 1e-4 bar."""
     from guava_renderer_amd import _lib
     d = make_scene(kind, P, W, H, seed=seed)
     rng = np.random.default_rng(seed)
     dL = rng.normal(size=(32, H, W)).astype(np.float32)
     dLinv = rng.normal(size=(1, H, W)).astype(np.float32)
-    prev = _lib.set_split_bf16(True)
-    try:
-        g = _gpu_backward(d, dL, dLinv)
-    finally:
-        _lib.set_split_bf16(bool(prev))
+    g = _gpu_backward(d, dL, dLinv, numerics=_lib.numerics(split_bf16=True))
     _check(g, _oracle_backward(d, dL, dLinv))
 
 

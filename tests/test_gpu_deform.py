@@ -199,3 +199,51 @@ def test_lbs_with_betas_b17_matrix_core_tails():
                                m["J_regressor"], m["parents"], m["lbs_weights"])
     np.testing.assert_allclose(verts.cpu().numpy(), r_verts, atol=ATOL, rtol=0)
     np.testing.assert_allclose(jt.cpu().numpy(), r_jt, atol=ATOL, rtol=0)
+
+
+def test_config5_cross_reenactment_avatar_pipeline():
+    """BASELINE config 5 as the bench runs it (`--config c5 --pipeline avatar`): 300k Gaussians (3 per
+    UV texel), cross-reenactment inputs (target poses with the source identity, main/test.py:21-28,
+    96-139), 1024x1024.  EHM + Gaussian assembly vs the oracle composition at full size (B=2), then
+    frame 1 rendered through the batched entry, bit-exact with the CPU oracle on the same assets."""
+    import oracle
+    from guava_renderer_amd import avatar, scenes
+    from guava_renderer_amd.pipeline import AvatarPipeline
+    B, P, W = 2, 300000, 1024
+    body, flame, extra = avatar.ehm_assets(seed=0)
+    verts, faces, tex = avatar.template_mesh()
+    g = avatar.gaussians(verts, faces, tex * 3, P=P, seed=0)
+    tb, tf = avatar.ehm_params(B, seed=2000)
+    sb, sf = avatar.ehm_params(1, seed=77)
+    bp, fp = avatar.change_id_info(tb, tf, sb, sf)
+    assert np.array_equal(bp["shape"][1], sb["shape"][0]) and np.array_equal(bp["body_pose"], tb["body_pose"])
+    pipe = AvatarPipeline(body, flame, extra, g, B, W, W, R_capacity=30 * P * B, device=DEV)
+    assert pipe.P == P
+    cams = scenes.frame_cameras(B, W, W, seed=1000)
+    views = _t(np.stack([c["viewmatrix"].reshape(16) for c in cams]))
+    projs = _t(np.stack([c["projmatrix"].reshape(16) for c in cams]))
+    tanf = _t(np.array([[c["tanfovx"], c["tanfovy"]] for c in cams], np.float32))
+    col, inv, radii, d = pipe.render({k: _t(v) for k, v in bp.items()}, {k: _t(v) for k, v in fp.items()},
+                                     views, projs, tanf)
+    torch.cuda.synchronize()
+    assert not pipe.rast.status()[1]
+    e = lo.ehm_forward(body, flame, extra, bp, fp)
+    ref = lo.deform_gaussians(e["vertices"], e["ver_transform_mat"], extra["faces"], g["vtx_rotations"],
+                              g["vtx_scales"], g["binding_face"], g["face_bary"], g["local_xyz"],
+                              g["uv_rotations"], g["uv_scales"])
+    np.testing.assert_allclose(d["xyz"].cpu().numpy(), ref["xyz"], atol=ATOL, rtol=0)
+    np.testing.assert_allclose(d["scaling"].cpu().numpy(), ref["scaling"], atol=ATOL, rtol=0)
+    q, rq = d["rotation"].cpu().numpy(), ref["rotation"]
+    err = np.minimum(np.abs(q - rq).max(-1), np.abs(q + rq).max(-1))
+    firm = ref["margin"] >= 1e-4
+    assert firm.mean() > 0.99 and err[firm].max() < ATOL, err[firm].max()
+    # the render of frame 1 from the GPU-deformed assets, bit-exact with the oracle
+    oracle.set_threads(16)
+    f = 1
+    o_col, o_radii, o_inv, _ = oracle.forward(
+        d["xyz"][f].cpu().numpy(), g["colors"], g["opacities"], d["scaling"][f].cpu().numpy(),
+        d["rotation"][f].cpu().numpy(), None, cams[f]["viewmatrix"], cams[f]["projmatrix"], W, W,
+        cams[f]["tanfovx"], cams[f]["tanfovy"], np.zeros(32, np.float32))
+    np.testing.assert_array_equal(radii[f].cpu().numpy(), o_radii)
+    np.testing.assert_array_equal(col[f].cpu().numpy(), o_col)
+    np.testing.assert_array_equal(inv[f].cpu().numpy(), o_inv.reshape(W, W))

@@ -28,10 +28,7 @@ def _inputs(frames):
 
 
 def _render(frames):
-    from guava_renderer_amd import _lib
     from guava_renderer_amd.batch import BatchRasterizer
-    _lib.set_exact_exp(True)
-    _lib.set_split_bf16(False)
     args, views, projs, tanf, bg = _inputs(frames)
     r = BatchRasterizer(len(frames), P, W, W, R_capacity=16 * P * len(frames), device="cuda:0")
     col, _, _ = r.forward(*args, views, projs, tanf, bg)
@@ -48,8 +45,10 @@ def _worker(rank, world, port, q):
         lo, hi = parallel.shard_range(N_FRAMES, rank, world)
         local = _render(list(range(lo, hi)))
         full = parallel.gather_frames(local.cpu(), N_FRAMES)
+        # the 8-bit exchange bench.py runs at N>1: encoded on the GPU, gathered as uint8
+        full8 = parallel.gather_frames(parallel.frames_to8b(local).cpu(), N_FRAMES)
         if rank == 0:
-            q.put(full.numpy())
+            q.put((full.numpy(), full8.numpy()))
     finally:
         dist.destroy_process_group()
 
@@ -64,13 +63,31 @@ def test_two_ranks_real_rasterizer_gather():
     procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
     for p in procs:
         p.start()
-    gathered = q.get(timeout=240)
+    gathered, gathered8 = q.get(timeout=240)
     for p in procs:
         p.join(timeout=120)
         assert p.exitcode == 0
     ref = _render(list(range(N_FRAMES))).cpu().numpy()
     assert gathered.shape == ref.shape
     np.testing.assert_array_equal(gathered, ref)
+    np.testing.assert_array_equal(gathered8, _to8b(ref[:, :3]))
+
+
+def _to8b(img):
+    """GUAVA's to8b (utils/general_utils.py:316-317)."""
+    return (255 * np.clip(img, 0, 1)).astype(np.uint8)
+
+
+def test_frames_to8b_matches_to8b():
+    from guava_renderer_amd import parallel
+    rng = np.random.default_rng(3)
+    x = rng.uniform(-0.5, 1.5, (3, 32, 37, 53)).astype(np.float32)  # ragged plane: the scalar kernel
+    x[0, 0, 0, :5] = [0.0, 1.0, 1.0 / 255, 254.999 / 255, 0.5]
+    for shape in ((3, 32, 37, 53), (2, 32, 64, 64)):
+        xs = np.ascontiguousarray(x[:shape[0], :, :shape[2], :shape[3]]) if shape[2] <= 37 else \
+            rng.uniform(-0.5, 1.5, shape).astype(np.float32)
+        got = parallel.frames_to8b(torch.tensor(xs, device="cuda:0")).cpu().numpy()
+        np.testing.assert_array_equal(got, _to8b(xs[:, :3]))
 
 
 def _nccl_worker(port, q):
@@ -98,6 +115,11 @@ def _nccl_worker(port, q):
             prev = ((fg.k - 1) % len(fg.bufs), ref)
         last = fg.wait()
         ok = ok and torch.equal(last, refs[-1])
+        # uint8 staging: the 32-channel frames are encoded (to8b) into the buffer the collective sends
+        f8 = parallel.FrameGather(2, (3, W, W), torch.uint8, dev)
+        for b in batches:
+            f8.push(_render(b))
+        ok = ok and torch.equal(f8.wait(), parallel.frames_to8b(_render(batches[-1])))
         q.put(bool(ok))
     finally:
         dist.destroy_process_group()

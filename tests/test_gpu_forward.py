@@ -42,68 +42,53 @@ def _compare_exact(d, antialiasing=False):
 @pytest.mark.parametrize("kind,P,W,H", [("random", 3000, 128, 96), ("random", 10000, 256, 256),
                                         ("avatar", 20000, 200, 136)])
 def test_forward_bit_exact(kind, P, W, H):
-    _lib().set_exact_exp(True)
     d = make_scene(kind, P, W, H, seed=3)
     _compare_exact(d)
 
 
 def test_forward_antialiasing_bit_exact():
-    _lib().set_exact_exp(True)
     d = make_scene("random", 4000, 96, 80, seed=5)
     _compare_exact(d, antialiasing=True)
 
 
 def test_forward_yaw_pitch_and_ragged_image():
-    _lib().set_exact_exp(True)
     d = make_scene("avatar", 15000, 150, 101, seed=7, yaw=0.3, pitch=-0.2)
     _compare_exact(d)
 
 
 def test_forward_fast_exp_tolerance():
-    L = _lib()
-    L.set_exact_exp(False)
-    try:
-        d = make_scene("random", 10000, 256, 256, seed=11)
-        g_col, g_radii, _, gs = gpu_forward(d)
-        o_col, o_radii, _, os_ = oracle_forward(d, exact=False)
-        np.testing.assert_array_equal(g_radii, o_radii)
-        np.testing.assert_array_equal(gs["point_list"][:gs["R"]], os_["point_list"])
-        mism = (gs["n_contrib"] != os_["n_contrib"]).mean()
-        assert mism <= 1e-3, mism
-        same = (gs["n_contrib"] == os_["n_contrib"]).reshape(d["image_height"], d["image_width"])
-        err = np.abs(g_col - o_col)[:, same]
-        assert err.max() <= 1e-4, err.max()
-    finally:
-        L.set_exact_exp(True)
+    d = make_scene("random", 10000, 256, 256, seed=11)
+    g_col, g_radii, _, gs = gpu_forward(d, numerics=_lib().numerics(fast_exp=True))
+    o_col, o_radii, _, os_ = oracle_forward(d, exact=False)
+    np.testing.assert_array_equal(g_radii, o_radii)
+    np.testing.assert_array_equal(gs["point_list"][:gs["R"]], os_["point_list"])
+    mism = (gs["n_contrib"] != os_["n_contrib"]).mean()
+    assert mism <= 1e-3, mism
+    same = (gs["n_contrib"] == os_["n_contrib"]).reshape(d["image_height"], d["image_width"])
+    err = np.abs(g_col - o_col)[:, same]
+    assert err.max() <= 1e-4, err.max()
 
 
 @pytest.mark.parametrize("kind,P,W,H", [("random", 10000, 256, 256), ("avatar", 20000, 200, 136)])
 def test_forward_split_bf16_tolerance(kind, P, W, H):
-    """gsr_set_split_bf16(1): the colour accumulation runs as four exact bf16 products per
+    """GSR_NUMERICS_SPLIT_BF16: the colour accumulation runs as four exact bf16 products per
     feature x weight on v_mfma_f32_32x32x16_bf16.  Everything the blend decides on VALU stays
     bit-exact (radii, lists, n_contrib, final_T, inverse depth); the 32 channels are within the
     north_star's 1e-4 L_inf of the oracle (bound: 3e-5 relative per product, sum of weights <= 1)."""
-    L = _lib()
-    L.set_exact_exp(True)
-    prev = L.set_split_bf16(True)
-    try:
-        d = make_scene(kind, P, W, H, seed=12)
-        g_col, g_radii, g_inv, gs = gpu_forward(d)
-        o_col, o_radii, o_inv, os_ = oracle_forward(d, exact=True)
-        np.testing.assert_array_equal(g_radii, o_radii)
-        np.testing.assert_array_equal(gs["point_list"][:gs["R"]], os_["point_list"])
-        np.testing.assert_array_equal(gs["n_contrib"], os_["n_contrib"])
-        np.testing.assert_array_equal(gs["final_T"], os_["final_T"])
-        np.testing.assert_array_equal(g_inv, o_inv)
-        err = np.abs(g_col - o_col)
-        assert err.max() <= 1e-4, err.max()
-        assert err.max() > 0.0  # the mode really ran (f32 accumulation is bit-exact)
-    finally:
-        L.set_split_bf16(bool(prev))
+    d = make_scene(kind, P, W, H, seed=12)
+    g_col, g_radii, g_inv, gs = gpu_forward(d, numerics=_lib().numerics(split_bf16=True))
+    o_col, o_radii, o_inv, os_ = oracle_forward(d, exact=True)
+    np.testing.assert_array_equal(g_radii, o_radii)
+    np.testing.assert_array_equal(gs["point_list"][:gs["R"]], os_["point_list"])
+    np.testing.assert_array_equal(gs["n_contrib"], os_["n_contrib"])
+    np.testing.assert_array_equal(gs["final_T"], os_["final_T"])
+    np.testing.assert_array_equal(g_inv, o_inv)
+    err = np.abs(g_col - o_col)
+    assert err.max() <= 1e-4, err.max()
+    assert err.max() > 0.0  # the mode really ran (f32 accumulation is bit-exact)
 
 
 def test_forward_precomputed_cov3D():
-    _lib().set_exact_exp(True)
     import oracle
     d = make_scene("random", 2000, 96, 96, seed=13)
     st = oracle.preprocess(d["means3D"], d["scales"], d["rotations"], d["opacities"], None,
@@ -121,7 +106,6 @@ def test_render_counters_match_oracle(kind, P, W, H):
     the pairs the reference's per-pixel loop visits and blends."""
     import oracle
     from guava_renderer_amd.batch import render_counters
-    _lib().set_exact_exp(True)
     d = make_scene(kind, P, W, H, seed=3)
     res = {}
     cnt = render_counters(lambda: res.update(out=gpu_forward(d)))
@@ -142,7 +126,6 @@ def test_strip_work_list():
     bit over the tile's list, and the strip work list holds every strip of every non-empty tile
     exactly once, tile-major (GSR_STRIP_ORDER default): a tile's 4 strips consecutive, tiles in
     non-increasing order of their longest strip up to the 4-buckets-per-octave granularity."""
-    _lib().set_exact_exp(True)
     d = make_scene("avatar", 20000, 200, 136, seed=3)
     _, _, _, gs = gpu_forward(d)
     T = gs["ranges"].size // 2

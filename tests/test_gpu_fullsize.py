@@ -22,8 +22,6 @@ pytestmark = pytest.mark.gpu
 def _batch_render(sc, cams, colors=None, split_bf16=False):
     from guava_renderer_amd import _lib
     from guava_renderer_amd.batch import BatchRasterizer
-    _lib.set_exact_exp(True)
-    _lib.set_split_bf16(split_bf16)
     dev = torch.device("cuda")
     t = lambda x: torch.tensor(np.ascontiguousarray(x), device=dev)  # noqa: E731
     B = len(cams)
@@ -32,12 +30,12 @@ def _batch_render(sc, cams, colors=None, split_bf16=False):
     views = t(np.stack([c["viewmatrix"].reshape(16) for c in cams]))
     projs = t(np.stack([c["projmatrix"].reshape(16) for c in cams]))
     tanf = t(np.array([[c["tanfovx"], c["tanfovy"]] for c in cams], np.float32))
-    r = BatchRasterizer(B, P, W, H, R_capacity=24 * P * B, device=dev)
+    r = BatchRasterizer(B, P, W, H, R_capacity=24 * P * B, device=dev,
+                        numerics=_lib.numerics(split_bf16=split_bf16))
     col, inv, radii = r.forward(t(sc["means3D"]), t(sc["colors"] if colors is None else colors),
                                 t(sc["opacities"]), t(sc["scales"]), t(sc["rotations"]), views, projs, tanf,
                                 torch.zeros((B, 32), device=dev))
     torch.cuda.synchronize()
-    _lib.set_split_bf16(False)
     R, ovf = r.status()
     assert not ovf
     return r, col.cpu().numpy(), inv.cpu().numpy(), radii.cpu().numpy()

@@ -48,9 +48,7 @@ def _oracle_grads(sc, cam, dL, dLinv, W=512):
 
 def test_fullsize_backward_single_frame_drop_in():
     """Config 4 gradients of one frame through _C.rasterize_gaussians(_backward)."""
-    from guava_renderer_amd import _lib
     from guava_renderer_amd.diff_gaussian_rasterization_32 import _C
-    _lib.set_exact_exp(True)
     sc, cams = _scene_c2()
     cam = cams[1]
     d = dict(sc, **cam, bg=np.zeros(32, np.float32))
@@ -78,9 +76,8 @@ def test_fullsize_backward_single_frame_drop_in():
 def test_config5_backward_single_frame():
     """Config 5 (300k Gaussians, 3 per UV texel, 1024^2): one frame's gradients through the batched
     entry vs the oracle, 1e-4 of each gradient's scale."""
-    from guava_renderer_amd import _lib, scenes
+    from guava_renderer_amd import scenes
     from guava_renderer_amd.batch import BatchRasterizer
-    _lib.set_exact_exp(True)
     P, W = 300000, 1024
     sc = scenes.avatar_cloud(P, seed=0, gaussians_per_texel=3)
     cam = scenes.frame_cameras(2, W, W, seed=1000)[1]
@@ -114,8 +111,6 @@ def test_fullsize_backward_batch6(split, per_frame_colors):
     batch-shared pre-split feature table, or splits per-frame features ([B, P, 32]) in the kernel."""
     from guava_renderer_amd import _lib
     from guava_renderer_amd.batch import BatchRasterizer
-    _lib.set_exact_exp(True)
-    prev = _lib.set_split_bf16(split)
     sc, cams = _scene_c2(cams=6)
     cams = cams[:6]
     B = 6
@@ -127,16 +122,14 @@ def test_fullsize_backward_batch6(split, per_frame_colors):
     args = [t(sc[k]) for k in ("means3D", "colors", "opacities", "scales", "rotations")]
     if per_frame_colors:
         args[1] = args[1][None].repeat(B, 1, 1).contiguous()
-    r = BatchRasterizer(B, 100000, 512, 512, R_capacity=12 * 100000 * B, device=DEV)
-    try:
-        r.forward(*args, views, projs, tanf, bgs)
-        rng = np.random.default_rng(12)
-        dL = rng.normal(size=(B, 32, 512, 512)).astype(np.float32)
-        dLinv = rng.normal(size=(B, 512, 512)).astype(np.float32)
-        g = r.backward(*args, views, projs, tanf, bgs, t(dL), t(dLinv))
-        torch.cuda.synchronize()
-    finally:
-        _lib.set_split_bf16(bool(prev))
+    r = BatchRasterizer(B, 100000, 512, 512, R_capacity=12 * 100000 * B, device=DEV,
+                        numerics=_lib.numerics(split_bf16=split))
+    r.forward(*args, views, projs, tanf, bgs)
+    rng = np.random.default_rng(12)
+    dL = rng.normal(size=(B, 32, 512, 512)).astype(np.float32)
+    dLinv = rng.normal(size=(B, 512, 512)).astype(np.float32)
+    g = r.backward(*args, views, projs, tanf, bgs, t(dL), t(dLinv))
+    torch.cuda.synchronize()
     assert not r.status()[1]
     gpu = {k: v.cpu().numpy() for k, v in g.items() if v is not None}
     for f in (0, 5):
@@ -165,10 +158,8 @@ def _ssim64(img, tgt):
 
 
 def test_trainer_gradients_match_cpu_recomputation():
-    from guava_renderer_amd import _lib, scenes
+    from guava_renderer_amd import scenes
     from guava_renderer_amd.train import SplatTrainer
-    _lib.set_exact_exp(True)
-    _lib.set_split_bf16(False)
     B, W = 2, 512
     sc = scenes.avatar_cloud(100000, seed=0)
     cams = scenes.frame_cameras(B, W, W, seed=1000)

@@ -24,9 +24,8 @@ args = [t(sc[k]) for k in ("means3D", "colors", "opacities", "scales", "rotation
 bgs = torch.zeros((B, 32), device=dev)
 out = {}
 for fast in (False, True):
-    _lib.set_split_bf16(True)
-    _lib.set_exact_exp(not fast)
-    r = BatchRasterizer(B, P, W, W, R_capacity=24 * P * B, device=dev)
+    r = BatchRasterizer(B, P, W, W, R_capacity=24 * P * B, device=dev,
+                        numerics=_lib.numerics(fast_exp=fast, split_bf16=True))
     col, inv, _ = r.forward(*args, views, projs, tanf, bgs)
     torch.cuda.synchronize()
     out[fast] = (col.clone(), inv.clone(), r.n_contrib().clone() if hasattr(r, "n_contrib") else None)

@@ -83,7 +83,9 @@ def main():
         for k, cs in _all_counters(d).items():
             kernels.setdefault(k, {}).setdefault("sq", {}).update({c: round(v) for c, v in cs.items()})
     rf = kernels.get("k_render_fwd", {})
-    res = {"config": config, "batch": int(batch),
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    from guava_renderer_amd import build as _build  # the sources the measured library was built from
+    res = {"config": config, "batch": int(batch), "source_hash": _build.source_hash(),
            "correction": "FETCH_SIZE KiB x1024 x2 (gfx950 half-count), WRITE_SIZE KiB x1024",
            "hbm_bytes_per_launch": rf.get("hbm_bytes"), "kernels": kernels}
     if calib_dir:
