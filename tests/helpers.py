@@ -120,7 +120,12 @@ def gpu_forward(d, antialiasing=False, use_cov=None, debug=False, numerics=0):
     st = {}
     st.update(decode(gb.cpu().numpy(), geom_layout(P, W, H)))
     st.update(decode(ib.cpu().numpy(), image_layout(W, H)))
-    st.update(decode(bb.cpu().numpy(), bin_layout(R)))
+    # the binning buffer is carved for its capacity: R after the synchronous read-back, the P x tiles
+    # bound on the no-sync path
+    from guava_renderer_amd import _lib
+    L = _lib.load()
+    cap = int(R) if bb.numel() == L.gsr_binning_bytes(int(R)) else L.gsr_forward_async_bound(P, W, H)
+    st.update(decode(bb.cpu().numpy(), bin_layout(cap)))
     st["smask"] = st["point_list"] >> 28           # entries: index | strip mask << 28
     st["point_list"] = st["point_list"] & 0x0FFFFFFF
     st["R"] = R

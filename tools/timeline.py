@@ -11,7 +11,8 @@ sys.path.insert(0, ROOT)
 from guava_renderer_amd import _lib, scenes  # noqa: E402
 from guava_renderer_amd.batch import BatchRasterizer  # noqa: E402
 
-B, P, W, H = 32, 100000, 512, 512
+B = int(sys.argv[1]) if len(sys.argv) > 1 else 32
+P, W, H = 100000, 512, 512
 dev = torch.device("cuda")
 sc = scenes.avatar_cloud(P, seed=0)
 cams = scenes.frame_cameras(B, W, H, seed=1000)
@@ -32,4 +33,12 @@ torch.cuda.synchronize()
 L.gsr_render_timeline(None, 0)
 os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)
 np.savez_compressed(os.path.join(ROOT, "gpurun_out", "timeline.npz"), tl=tl.cpu().numpy(), cnt=cnt.cpu().numpy())
-print("ok", cnt.cpu().numpy())
+tl = tl.cpu().numpy().astype(np.int64)
+tl = tl[tl[:, 1] > 0]
+dur = tl[:, 1] - tl[:, 0]
+span = tl[:, 1].max() - tl[:, 0].min()
+print(f"items {len(tl)} span {span / 100:.1f} us, longest item {dur.max() / 100:.1f} us ({tl[dur.argmax(), 2]} k-steps), "
+      f"mean {dur.mean() / 100:.1f} us, p99 {np.percentile(dur, 99) / 100:.1f} us, "
+      f"items ending in the last 20% of the span: {int((tl[:, 1] > tl[:, 0].min() + 0.8 * span).sum())}")
+order = np.argsort(-dur)[:8]
+print("top items (start, dur us, ksteps):", [(round((tl[i, 0] - tl[:, 0].min()) / 100, 1), round(dur[i] / 100, 1), int(tl[i, 2])) for i in order])
