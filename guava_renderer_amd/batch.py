@@ -210,6 +210,12 @@ class BatchRasterizer:
                 raise ValueError("dL_dinvdepth: expected [B,H,W]")
             dLi = dL_dinvdepth.to(torch.float32).contiguous()
         if shared:
+            # the frame-reduced kernels read ONE attribute row set: per-frame inputs would come back
+            # as a single sum over distinct tensors, so they are refused here
+            strides = head[5::2]  # means3D, colors, opacities, scales, rotations frame strides
+            if any(st_ != 0 for st_ in strides):
+                raise ValueError("backward(shared=True) needs attributes shared by every frame "
+                                 "([P,k] tensors or frame stride 0); got per-frame inputs")
             g = dict(colors=torch.zeros((P, C), **o), opacity=torch.empty((P, 1), **o),
                      means3D=torch.empty((P, 3), **o), scales=torch.empty((P, 3), **o),
                      rotations=torch.empty((P, 4), **o))

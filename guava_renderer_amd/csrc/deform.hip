@@ -14,7 +14,7 @@
 // Kernels (all B frames per launch):
 //   k_pack_rows      segs x B WGs     the coefficient rows of EHM.forward from their pieces
 //   k_lbs_rodrigues  B*J threads      axis-angle -> R, pose feature R - I
-//   k_lbs_blend      3V/64 x B/16 WGs v_shaped = template + shapedirs.betas, v_posed = v_shaped +
+//   k_lbs_blend      3V/64 x B/16 WGs (B = 1: one frame, 16 waves per WG) v_shaped = template + shapedirs.betas, v_posed = v_shaped +
 //                                     posedirs.feature: the bases are streamed once per 16 frames
 //                                     (HBM-bound: 4*(NB + 9(J-1)) bytes per vertex coordinate)
 //   k_lbs_blend_mfma 3V/32 x B/32 WGs the same for B > 16 on the matrix cores (f32 MFMA), bases
@@ -42,6 +42,9 @@ namespace gsr {
 
 constexpr int kLbsFrames = 16;  // frames per k_lbs_blend workgroup (accumulators per thread)
 constexpr int kLbsSplit = 4;    // k_lbs_blend waves per workgroup, each an interleaved slice of k
+// single-frame batches (the per-frame drop-in path): one accumulator per thread and 16 waves per
+// workgroup, so the K-long stream of every coordinate has 16 slices of loads in flight
+constexpr int kLbsSplit1 = 16;
 
 struct Parents {
     int8_t p[GSR_LBS_MAX_JOINTS];
@@ -87,25 +90,31 @@ __global__ void k_lbs_rodrigues(int B, int J, const float* __restrict__ pose, in
 // kLbsBatch loads of the k-major base issued before their FMAs (enough bytes in flight to stream
 // from HBM with ~4 waves per SIMD).
 constexpr int kLbsBatch = 16;
+template <int NF, int SPLIT>
 __device__ __forceinline__ void lbs_stream(const float* __restrict__ base, int M, int m, int K, int w,
-                                           const float* coef, float (&acc)[kLbsFrames]) {
-    for (int k0 = w; k0 < K; k0 += kLbsSplit * kLbsBatch) {
+                                           const float* coef, float (&acc)[NF]) {
+    for (int k0 = w; k0 < K; k0 += SPLIT * kLbsBatch) {
         float v[kLbsBatch];
 #pragma unroll
         for (int u = 0; u < kLbsBatch; u++) {
-            const int k = k0 + u * kLbsSplit;
+            const int k = k0 + u * SPLIT;
             v[u] = k < K ? base[(int64_t)k * M + m] : 0.f;
         }
 #pragma unroll
         for (int u = 0; u < kLbsBatch; u++) {
-            const int k = k0 + u * kLbsSplit;
+            const int k = k0 + u * SPLIT;
             if (k >= K) break;
-            const float4* c = reinterpret_cast<const float4*>(&coef[k * kLbsFrames]);
+            if constexpr (NF % 4 == 0) {
+                const float4* c = reinterpret_cast<const float4*>(&coef[k * NF]);
 #pragma unroll
-            for (int q = 0; q < kLbsFrames / 4; q++) {
-                const float4 cq = c[q];
-                acc[4 * q] = fmaf(cq.x, v[u], acc[4 * q]); acc[4 * q + 1] = fmaf(cq.y, v[u], acc[4 * q + 1]);
-                acc[4 * q + 2] = fmaf(cq.z, v[u], acc[4 * q + 2]); acc[4 * q + 3] = fmaf(cq.w, v[u], acc[4 * q + 3]);
+                for (int q = 0; q < NF / 4; q++) {
+                    const float4 cq = c[q];
+                    acc[4 * q] = fmaf(cq.x, v[u], acc[4 * q]); acc[4 * q + 1] = fmaf(cq.y, v[u], acc[4 * q + 1]);
+                    acc[4 * q + 2] = fmaf(cq.z, v[u], acc[4 * q + 2]); acc[4 * q + 3] = fmaf(cq.w, v[u], acc[4 * q + 3]);
+                }
+            } else {
+#pragma unroll
+                for (int f = 0; f < NF; f++) acc[f] = fmaf(coef[k * NF + f], v[u], acc[f]);
             }
         }
     }
@@ -118,12 +127,13 @@ __device__ __forceinline__ void lbs_stream(const float* __restrict__ base, int M
 // loads in flight instead of one serial chain, and the slice sums are added in slice order through
 // LDS (deterministic).  The frame coefficients sit in LDS (broadcast reads); the k-major bases are
 // read coalesced, once per frame group.
-inline dim3 lbs_blend_grid(int M, int B) {
+inline dim3 lbs_blend_grid(int M, int B, int nf) {
     const int nx8 = ((M + 63) / 64 + 7) / 8 * 8;
-    return dim3(nx8 * ((B + kLbsFrames - 1) / kLbsFrames));
+    return dim3(nx8 * ((B + nf - 1) / nf));
 }
 
-__global__ __launch_bounds__(64 * kLbsSplit) void k_lbs_blend(int B, int M, int NB, int NP,
+template <int NF, int SPLIT>
+__global__ __launch_bounds__(64 * SPLIT) void k_lbs_blend(int B, int M, int NB, int NP,
                                                               const float* __restrict__ vt, int64_t vt_stride,
                                                               const float* __restrict__ betas,
                                                               const float* __restrict__ sd_t,
@@ -131,19 +141,19 @@ __global__ __launch_bounds__(64 * kLbsSplit) void k_lbs_blend(int B, int M, int 
                                                               const float* __restrict__ pd,
                                                               float* __restrict__ v_shaped,
                                                               float* __restrict__ v_posed) {
-    extern __shared__ float4 lds4[];  // coef [(NB + NP)][kLbsFrames], then the slice reduction
+    extern __shared__ float4 lds4[];  // coef [(NB + NP)][NF], then the slice reduction
     float* coef = reinterpret_cast<float*>(lds4);
     // XCD-aware order (1-D grid, lbs_blend_grid): the frame groups of one coordinate block are
     // dealt to the same XCD back to back, so all but the first read the basis slice from its L2
-    const int ng = (B + kLbsFrames - 1) / kLbsFrames;
+    const int ng = (B + NF - 1) / NF;
     const int jx = (int)(blockIdx.x >> 3);
     const int by = jx % ng;
     const int bx = (jx / ng) * 8 + (int)(blockIdx.x & 7);
     if (bx * 64 >= M) return;  // padding block (the whole workgroup, before any barrier)
-    const int b0 = by * kLbsFrames;
+    const int b0 = by * NF;
     const int nk = NB + NP;
-    for (int idx = threadIdx.x; idx < nk * kLbsFrames; idx += blockDim.x) {
-        const int k = idx / kLbsFrames, f = idx - k * kLbsFrames;
+    for (int idx = threadIdx.x; idx < nk * NF; idx += blockDim.x) {
+        const int k = idx / NF, f = idx - k * NF;
         const int b = b0 + f;
         float v = 0.f;
         if (b < B) v = k < NB ? betas[(int64_t)b * NB + k] : feat[(int64_t)b * NP + (k - NB)];
@@ -153,28 +163,28 @@ __global__ __launch_bounds__(64 * kLbsSplit) void k_lbs_blend(int B, int M, int 
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int m = bx * 64 + lane;
     const bool ok = m < M;
-    const int nf = min(kLbsFrames, B - b0);
-    float as[kLbsFrames], ap[kLbsFrames];
+    const int nf = min(NF, B - b0);
+    float as[NF], ap[NF];
 #pragma unroll
-    for (int f = 0; f < kLbsFrames; f++) { as[f] = 0.f; ap[f] = 0.f; }
+    for (int f = 0; f < NF; f++) { as[f] = 0.f; ap[f] = 0.f; }
     if (ok) {
-        lbs_stream(sd_t, M, m, NB, w, coef, as);
-        lbs_stream(pd, M, m, NP, w, coef + NB * kLbsFrames, ap);
+        lbs_stream<NF, SPLIT>(sd_t, M, m, NB, w, coef, as);
+        lbs_stream<NF, SPLIT>(pd, M, m, NP, w, coef + NB * NF, ap);
     }
     // slice reduction through LDS: red[w][f][lane]
     float* red = coef;
     __syncthreads();  // coefficients no longer needed
 #pragma unroll
-    for (int f = 0; f < kLbsFrames; f++) red[(w * kLbsFrames + f) * 64 + lane] = as[f];
+    for (int f = 0; f < NF; f++) red[(w * NF + f) * 64 + lane] = as[f];
     __syncthreads();
-    float vs[kLbsFrames];
+    float vs[NF];
 #pragma unroll
-    for (int f = 0; f < kLbsFrames; f++) vs[f] = 0.f;
+    for (int f = 0; f < NF; f++) vs[f] = 0.f;
     if (w == 0) {
 #pragma unroll
-        for (int f = 0; f < kLbsFrames; f++) {
+        for (int f = 0; f < NF; f++) {
             float acc = red[f * 64 + lane];
-            for (int u = 1; u < kLbsSplit; u++) acc += red[(u * kLbsFrames + f) * 64 + lane];
+            for (int u = 1; u < SPLIT; u++) acc += red[(u * NF + f) * 64 + lane];
             const int b = b0 + f;
             if (ok && f < nf) {
                 const float tv = vt[(int64_t)b * vt_stride + m];
@@ -186,13 +196,13 @@ __global__ __launch_bounds__(64 * kLbsSplit) void k_lbs_blend(int B, int M, int 
     if (!v_posed) return;  // blend_shapes + joints only (gsr_blend_joints); uniform
     __syncthreads();
 #pragma unroll
-    for (int f = 0; f < kLbsFrames; f++) red[(w * kLbsFrames + f) * 64 + lane] = ap[f];
+    for (int f = 0; f < NF; f++) red[(w * NF + f) * 64 + lane] = ap[f];
     __syncthreads();
     if (w == 0) {
 #pragma unroll
-        for (int f = 0; f < kLbsFrames; f++) {
+        for (int f = 0; f < NF; f++) {
             float acc = red[f * 64 + lane];
-            for (int u = 1; u < kLbsSplit; u++) acc += red[(u * kLbsFrames + f) * 64 + lane];
+            for (int u = 1; u < SPLIT; u++) acc += red[(u * NF + f) * 64 + lane];
             if (ok && f < nf) v_posed[(int64_t)(b0 + f) * M + m] = acc + vs[f];
         }
     }
@@ -273,9 +283,9 @@ static void launch_blend(int B, int M, int NB, int NP, const float* vt, int64_t 
                          const float* sd_t, const float* feat, const float* pd, float* vs, float* vp,
                          hipStream_t s);
 
-static size_t lbs_blend_lds(int NB, int NP) {
-    const size_t coef = sizeof(float) * (size_t)(NB + NP) * kLbsFrames;
-    const size_t red = sizeof(float) * (size_t)kLbsSplit * kLbsFrames * 64;
+static size_t lbs_blend_lds(int NB, int NP, int nf, int split) {
+    const size_t coef = sizeof(float) * (size_t)(NB + NP) * nf;
+    const size_t red = sizeof(float) * (size_t)split * nf * 64;
     return coef > red ? coef : red;
 }
 
@@ -283,7 +293,10 @@ static void lbs_blend_attr(size_t lds) {
     static size_t attr = 0;
     if (lds > 65536 && attr < lds) {
         attr = lds;
-        hipFuncSetAttribute((const void*)k_lbs_blend, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        hipFuncSetAttribute((const void*)k_lbs_blend<kLbsFrames, kLbsSplit>,
+                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        hipFuncSetAttribute((const void*)k_lbs_blend<1, kLbsSplit1>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            (int)lds);
     }
 }
 
@@ -299,10 +312,21 @@ static void launch_blend(int B, int M, int NB, int NP, const float* vt, int64_t 
                            vp ? NP : 0, vt, vt_stride, betas, sd_t, feat, pd, vs, vp);
         return;
     }
-    const size_t lds = lbs_blend_lds(NB, vp ? NP : 0);
+    static const bool single = [] {  // GSR_BLEND_SINGLE=0: B = 1 on the 16-frame kernel (A/B)
+        const char* e = getenv("GSR_BLEND_SINGLE");
+        return !(e && e[0] == '0');
+    }();
+    if (B == 1 && single) {
+        const size_t lds = lbs_blend_lds(NB, vp ? NP : 0, 1, kLbsSplit1);
+        lbs_blend_attr(lds);
+        hipLaunchKernelGGL((k_lbs_blend<1, kLbsSplit1>), lbs_blend_grid(M, B, 1), dim3(64 * kLbsSplit1), lds, s, B, M,
+                           NB, vp ? NP : 0, vt, vt_stride, betas, sd_t, feat, pd, vs, vp);
+        return;
+    }
+    const size_t lds = lbs_blend_lds(NB, vp ? NP : 0, kLbsFrames, kLbsSplit);
     lbs_blend_attr(lds);
-    hipLaunchKernelGGL(k_lbs_blend, lbs_blend_grid(M, B), dim3(64 * kLbsSplit), lds, s, B, M, NB, vp ? NP : 0,
-                       vt, vt_stride, betas, sd_t, feat, pd, vs, vp);
+    hipLaunchKernelGGL((k_lbs_blend<kLbsFrames, kLbsSplit>), lbs_blend_grid(M, B, kLbsFrames), dim3(64 * kLbsSplit),
+                       lds, s, B, M, NB, vp ? NP : 0, vt, vt_stride, betas, sd_t, feat, pd, vs, vp);
 }
 
 // vertices2joints (lbs.py:335-352): J[b,j,:] = sum_v J_regressor[j,v] v_shaped[b,v,:], plus
@@ -774,7 +798,7 @@ int gsr_lbs(int B, int V, int J, int NB, const float* v_template, int64_t v_temp
     hipLaunchKernelGGL(k_lbs_rodrigues, dim3((B * J + 255) / 256), dim3(256), 0, s, B, J, pose,
                        pose2rot, a.rot, a.feat);
     if (int rc = hip_check("lbs_rodrigues")) return rc;
-    if (lbs_blend_lds(NB, NP) > 160 * 1024) return api_fail(GSR_ERR_ARG, "gsr_lbs: NB + 9(J-1) too large for LDS");
+    if (lbs_blend_lds(NB, NP, kLbsFrames, kLbsSplit) > 160 * 1024) return api_fail(GSR_ERR_ARG, "gsr_lbs: NB + 9(J-1) too large for LDS");
     launch_blend(B, M, NB, NP, v_template, v_template_stride, betas, shapedirs_t, a.feat, posedirs, vs, a.vp, s);
     if (int rc = hip_check("lbs_blend")) return rc;
     hipLaunchKernelGGL(k_lbs_joints, dim3((J + kJointsPerWG - 1) / kJointsPerWG, B), dim3(256), 0, s, V, J, J_regressor, vs,
@@ -798,7 +822,7 @@ int gsr_blend_joints(int B, int V, int J, int NB, const float* v_template, int64
     if (betas && (NB <= 0 || !shapedirs_t))
         return api_fail(GSR_ERR_ARG, "gsr_blend_joints: betas need NB > 0 and shapedirs");
     if (!betas) NB = 0;
-    if (lbs_blend_lds(NB, 0) > 160 * 1024) return api_fail(GSR_ERR_ARG, "gsr_blend_joints: NB too large for LDS");
+    if (lbs_blend_lds(NB, 0, kLbsFrames, kLbsSplit) > 160 * 1024) return api_fail(GSR_ERR_ARG, "gsr_blend_joints: NB too large for LDS");
     hipStream_t s = (hipStream_t)stream;
     const int M = V * 3;
     launch_blend(B, M, NB, 0, v_template, v_template_stride, betas, shapedirs_t, nullptr, nullptr, v_shaped, nullptr, s);

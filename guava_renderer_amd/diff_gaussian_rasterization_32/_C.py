@@ -229,7 +229,8 @@ def rasterize_gaussians(background, means3D, colors, opacity, scales, rotations,
                 int(bool(antialiasing)), radii.data_ptr(), int(bool(debug)))
         bound = L.gsr_forward_async_bound(P, W, H)
         with torch.cuda.device(dev):
-            if not debug and not exact_binning and bound < 0x7FFFFFFF and 4 * bound <= ASYNC_BINNING_MB << 20:
+            if (not debug and not exact_binning and bound < 0x7FFFFFFF
+                    and L.gsr_binning_bytes(bound) <= ASYNC_BINNING_MB << 20):
                 ring = _RINGS.get(dev)
                 if ring is None:
                     ring = _RINGS[dev] = _StatusRing()

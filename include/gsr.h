@@ -179,7 +179,10 @@ int gsr_backward_batch(int B, int P, int width, int height, const float* means3D
  * over the frames, [P,k], with no per-frame [B,P,k] buffers (the reference's autograd sums the
  * per-frame gradients of the shared leaves).  dL_dcolor [P,32] is ACCUMULATED into (zero it);
  * dL_dopacity [P], dL_dmean3D [P,3], dL_dscale [P,3], dL_drot [P,4] are written.  Each Gaussian's
- * frames are summed in frame order (deterministic, except dL_dcolor's float atomics). */
+ * frames are summed in frame order.  Not bitwise reproducible run to run: dL_dcolor and each
+ * frame's screen-space gradient row (dL/dmean2D, conic, opacity, inverse depth, from which the
+ * mean3D / opacity / scale / rotation gradients follow) are accumulated with float atomics across
+ * strips and tiles, as the reference's backward accumulates them with atomicAdd. */
 int gsr_backward_batch_shared(int B, int P, int width, int height, const float* means3D,
                               int64_t means_stride, const float* colors, int64_t colors_stride,
                               const float* opacities, int64_t opac_stride, const float* scales,
