@@ -633,17 +633,22 @@ void launch_tile_scan(const Dims& d, const GeomArena& g, const ImageArena& im, h
 // of the conic's quadratic form Q = a dx^2 + 2b dx dy + c dy^2 (power = -Q/2 in the blend).  Q is
 // convex (a, c > 0, ac > b^2), so the minimum is 0 if the mean lies inside, else it lies on an edge:
 // each edge is a 1-D quadratic minimised by clamping its vertex.
+// Only the edges FACING the mean can hold that minimum: from a point of any other edge the segment
+// towards the mean enters the rectangle and Q falls along it (convexity).  So at most one vertical
+// edge (the column nearest the mean, when the mean is left or right of the rectangle) and one
+// horizontal edge are evaluated -- half of the four-edge form's work, the same minimum.
 __host__ __device__ __forceinline__ float rect_qmin(float a, float b, float c, float ia, float ic, float dxl, float dxh,
                                            float dyl, float dyh) {
-    if (dxl <= 0.f && dxh >= 0.f && dyl <= 0.f && dyh >= 0.f) return 0.f;
+    const bool xin = dxl <= 0.f && dxh >= 0.f, yin = dyl <= 0.f && dyh >= 0.f;
+    if (xin && yin) return 0.f;
     float q = 3.0e38f;
-    const float xs[2] = {dxl, dxh}, ys[2] = {dyl, dyh};
-#pragma unroll
-    for (int k = 0; k < 2; k++) {
-        const float X = xs[k];
+    if (!xin) {  // the facing column: dx = dxl (mean right of it) or dxh (mean left of it)
+        const float X = dxl > 0.f ? dxl : dxh;
         const float y = fminf(fmaxf(-b * X * ic, dyl), dyh);
-        q = fminf(q, a * X * X + 2.f * b * X * y + c * y * y);
-        const float Y = ys[k];
+        q = a * X * X + 2.f * b * X * y + c * y * y;
+    }
+    if (!yin) {  // the facing row
+        const float Y = dyl > 0.f ? dyl : dyh;
         const float x = fminf(fmaxf(-b * Y * ia, dxl), dxh);
         q = fminf(q, a * x * x + 2.f * b * x * Y + c * Y * Y);
     }

@@ -11,6 +11,7 @@
 namespace gsr {  // link stand-ins for the launch helpers binning.hip uses (host check only)
 int persistent_grid(int) { return 1; }
 int strip_order_tile_major() { return 1; }
+int xcd_queue_map() { return 2; }
 }  // namespace gsr
 
 int main() {
