@@ -20,7 +20,7 @@
 //   k_lbs_blend_mfma 3V/32 x B/32 WGs the same for B > 16 on the matrix cores (f32 MFMA), bases
 //                                     streamed once per 32 frames
 //   k_lbs_joints     J/4 x B WGs      J_regressor . v_shaped (+ joints_offset)
-//   k_lbs_chain      B waves          the kinematic chain (J sequential 4x4 products) in LDS
+//   k_lbs_chain      B WGs            the kinematic chain in LDS, one tree level per step
 //   k_lbs_skin       V x B            T_v = sum_j w_vj A_j, v = T_v [v_posed; 1]
 //   k_deform_gaussians (V+N) x B/8    vertex + UV Gaussians straight into the rasterizer's inputs
 //                                     (face frames once per face and frame, in LDS)
@@ -394,17 +394,24 @@ __global__ __launch_bounds__(256) void k_lbs_joints(int V, int J, const float* _
     }
 }
 
-// batch_rigid_transform (lbs.py:426-482) for one frame per 64-lane workgroup: local transforms
-// [R | J_i - J_parent], the chain product in parent order (16 lanes, one matrix element each),
-// posed joints = chain[:, :3, 3], A = chain - pad(chain . [J; 0]).
-__global__ __launch_bounds__(64) void k_lbs_chain(int J, Parents par, const float* __restrict__ rot,
-                                                  const float* __restrict__ joints,
-                                                  float* __restrict__ jtrans,
-                                                  float* __restrict__ A) {
+// batch_rigid_transform (lbs.py:426-482), one frame per workgroup: local transforms
+// [R | J_i - J_parent], the chain product chain_i = chain_parent . local_i, posed joints =
+// chain[:, :3, 3], A = chain - pad(chain . [J; 0]).  The chain runs level by level of the kinematic
+// tree (16 threads per joint, one matrix element each): every joint of a level in one step, so
+// SMPL-X's 54 sequential products become its tree depth (~10) barrier steps -- each product is
+// the same expression as the sequential chain's, so the results are identical.
+__global__ __launch_bounds__(16 * GSR_LBS_MAX_JOINTS) void k_lbs_chain(int J, Parents par,
+                                                                     const float* __restrict__ rot,
+                                                                     const float* __restrict__ joints,
+                                                                     float* __restrict__ jtrans,
+                                                                     float* __restrict__ A) {
     __shared__ float tm[GSR_LBS_MAX_JOINTS][16];
     __shared__ float ch[GSR_LBS_MAX_JOINTS][16];
+    __shared__ int depth[GSR_LBS_MAX_JOINTS];
+    __shared__ int maxd;
     const int b = blockIdx.x, t = threadIdx.x;
     const float* Jb = joints + (int64_t)b * J * 3;
+    if (t == 0) maxd = 0;
     if (t < J) {
         const float* R = rot + ((int64_t)b * J + t) * 9;
         float rel[3];
@@ -414,17 +421,21 @@ __global__ __launch_bounds__(64) void k_lbs_chain(int J, Parents par, const floa
             tm[t][4 * r + 3] = rel[r];
         }
         tm[t][12] = 0.f; tm[t][13] = 0.f; tm[t][14] = 0.f; tm[t][15] = 1.f;
+        int dd = 0;
+        for (int i = t; i > 0 && dd < GSR_LBS_MAX_JOINTS; i = par.p[i]) dd++;  // (parents precede children)
+        depth[t] = dd;
     }
     __syncthreads();
+    if (t < J) atomicMax(&maxd, depth[t]);
     if (t < 16) ch[0][t] = tm[0][t];
     __syncthreads();
-    const int r = t >> 2, c = t & 3;
-    for (int i = 1; i < J; i++) {
-        if (t < 16) {
-            const float* P = ch[par.p[i]];
-            const float* L = tm[i];
-            ch[i][t] = P[4 * r] * L[c] + P[4 * r + 1] * L[4 + c] + P[4 * r + 2] * L[8 + c] +
-                       P[4 * r + 3] * L[12 + c];
+    const int j = t >> 4, e = t & 15, r = e >> 2, c = e & 3;
+    const int dj = j < J ? depth[j] : -1;
+    for (int lvl = 1; lvl <= maxd; lvl++) {
+        if (dj == lvl) {
+            const float* P = ch[par.p[j]];
+            const float* L = tm[j];
+            ch[j][e] = P[4 * r] * L[c] + P[4 * r + 1] * L[4 + c] + P[4 * r + 2] * L[8 + c] + P[4 * r + 3] * L[12 + c];
         }
         __syncthreads();
     }
@@ -804,7 +815,7 @@ int gsr_lbs(int B, int V, int J, int NB, const float* v_template, int64_t v_temp
     hipLaunchKernelGGL(k_lbs_joints, dim3((J + kJointsPerWG - 1) / kJointsPerWG, B), dim3(256), 0, s, V, J, J_regressor, vs,
                        joints_offset, jr);
     if (int rc = hip_check("lbs_joints")) return rc;
-    hipLaunchKernelGGL(k_lbs_chain, dim3(B), dim3(64), 0, s, J, par, a.rot, jr, joints_transformed, A);
+    hipLaunchKernelGGL(k_lbs_chain, dim3(B), dim3(16 * GSR_LBS_MAX_JOINTS), 0, s, J, par, a.rot, jr, joints_transformed, A);
     if (int rc = hip_check("lbs_chain")) return rc;
     hipLaunchKernelGGL(k_lbs_skin, dim3((V + 255) / 256, B), dim3(256), 0, s, V, J, lbs_weights_t, A,
                        a.vp, verts, vert_transforms);

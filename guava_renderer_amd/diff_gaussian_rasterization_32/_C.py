@@ -24,6 +24,15 @@ NUM_CHANNELS = 32
 # buffer (exact_binning=False: inference -- GaussianRasterizer_32 under no_grad drops it with the
 # call); a forward whose buffers autograd saves for backward sizes it to the exact R.
 ASYNC_BINNING_MB = int(os.environ.get("GSR_ASYNC_BINNING_MB", "512"))
+# numerics of the reference-signature calls that pass none (GaussianRasterizer_32 as GUAVA calls it):
+# 0 = bit-identical to the oracle.  A deployment can opt into a tolerance mode for the unchanged
+# caller, e.g. GSR_NUMERICS=split_bf16 (or fast_exp), comma-separated.
+_NUMERICS_NAMES = {"fast_exp": 1, "split_bf16": 2}
+DEFAULT_NUMERICS = 0
+for _n in filter(None, (x.strip() for x in os.environ.get("GSR_NUMERICS", "").split(","))):
+    if _n not in _NUMERICS_NAMES:
+        raise ValueError(f"GSR_NUMERICS: unknown flag {_n!r} (known: {sorted(_NUMERICS_NAMES)})")
+    DEFAULT_NUMERICS |= _NUMERICS_NAMES[_n]
 
 
 class PendingCount:
@@ -179,7 +188,7 @@ class _Resizer:
 
 def rasterize_gaussians(background, means3D, colors, opacity, scales, rotations, scale_modifier,
                         cov3D_precomp, viewmatrix, projmatrix, tan_fovx, tan_fovy, image_height,
-                        image_width, sh, degree, campos, prefiltered, antialiasing, debug, *, numerics=0,
+                        image_width, sh, degree, campos, prefiltered, antialiasing, debug, *, numerics=None,
                         exact_binning=False):
     """RasterizeGaussiansCUDA (rasterize_points.cu:36-124).  Returns
     (num_rendered, color[32,H,W], radii[P] int32, geomBuffer, binningBuffer, imgBuffer, invdepth[1,H,W]).
@@ -191,6 +200,8 @@ def rasterize_gaussians(background, means3D, colors, opacity, scales, rotations,
     P x tiles bound (4 B per possible instance; R cannot exceed it) and num_rendered a PendingCount."""
     if means3D.ndimension() != 2 or means3D.size(1) != 3:
         raise RuntimeError("means3D must have dimensions (num_points, 3)")
+    if numerics is None:
+        numerics = DEFAULT_NUMERICS
     P = int(means3D.size(0))
     H = int(image_height)
     W = int(image_width)
@@ -248,10 +259,12 @@ def rasterize_gaussians(background, means3D, colors, opacity, scales, rotations,
 def rasterize_gaussians_backward(background, means3D, radii, colors, opacities, scales, rotations,
                                  scale_modifier, cov3D_precomp, viewmatrix, projmatrix, tan_fovx,
                                  tan_fovy, dL_dout_color, dL_dout_invdepth, sh, degree, campos,
-                                 geomBuffer, R, binningBuffer, imageBuffer, antialiasing, debug, *, numerics=0):
+                                 geomBuffer, R, binningBuffer, imageBuffer, antialiasing, debug, *, numerics=None):
     """RasterizeGaussiansBackwardCUDA (rasterize_points.cu:127-223).  Returns
     (dL_dmeans2D, dL_dcolors, dL_dopacity, dL_dmeans3D, dL_dcov3D, dL_dsh, dL_dscales, dL_drotations).
     numerics: as rasterize_gaussians."""
+    if numerics is None:
+        numerics = DEFAULT_NUMERICS
     P = int(means3D.size(0))
     H = int(dL_dout_color.size(1))
     W = int(dL_dout_color.size(2))

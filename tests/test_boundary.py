@@ -50,6 +50,25 @@ def test_numerics_flags():
             getattr(L, name)
 
 
+def test_unchanged_caller_numerics_from_env():
+    """The reference-signature _C calls take their numerics from GSR_NUMERICS (read at import; exact
+    by default), so an unchanged caller can opt into a tolerance mode; unknown names are refused."""
+    import subprocess
+    import sys
+    code = ("from guava_renderer_amd.diff_gaussian_rasterization_32 import _C; "
+            "print(_C.DEFAULT_NUMERICS)")
+    env = dict(os.environ)
+    env.pop("GSR_NUMERICS", None)
+    out = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, cwd=ROOT)
+    assert out.stdout.strip() == "0", out.stderr
+    env["GSR_NUMERICS"] = "split_bf16,fast_exp"
+    out = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, cwd=ROOT)
+    assert out.stdout.strip() == "3", out.stderr
+    env["GSR_NUMERICS"] = "bogus"
+    out = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, cwd=ROOT)
+    assert out.returncode != 0 and "unknown flag" in out.stderr
+
+
 def test_python_surface_matches_reference():
     import diff_gaussian_rasterization_32 as m
     from guava_renderer_amd.diff_gaussian_rasterization_32 import _C
