@@ -212,7 +212,7 @@ def rasterize_gaussians(background, means3D, colors, opacity, scales, rotations,
     alloc = torch.zeros if P == 0 else torch.empty
     out_color = alloc((NUM_CHANNELS, H, W), **fopts)
     out_invdepth = alloc((1, H, W), **fopts)
-    radii = torch.zeros((P,), dtype=torch.int32, device=dev)
+    radii = alloc((P,), dtype=torch.int32, device=dev)  # (preprocess writes every Gaussian's radius)
     geom, binning, img = _Resizer(dev), _Resizer(dev), _Resizer(dev)
     rendered = 0
     if P != 0:
