@@ -856,16 +856,27 @@ __global__ __launch_bounds__(256) void k_strip_count(Dims d, ImageArena im, BinA
     if (tile_g >= d.B * d.T) return;
     const uint2 r = im.ranges[tile_g];
     uint32_t c[kStrips] = {};
-    // 16 loads in flight per lane: the longest lists (several thousand entries) bound this kernel
-    // by their serial load round trips
-    for (uint32_t i = r.x + lane; i < r.y; i += 1024) {
-        uint32_t e[16];
+    // the 16-byte-aligned body as uint4 loads (8 per lane in flight: the longest lists, several
+    // thousand entries, bound this kernel by their load round trips), the unaligned ends by lanes
+    const uint32_t a4 = min((r.x + 3u) & ~3u, r.y), b4 = max(r.y & ~3u, a4);
+    if (r.x + (uint32_t)lane < a4) { const uint32_t e = bn.point_list[r.x + lane];
 #pragma unroll
-        for (int u = 0; u < 16; u++) e[u] = i + 64u * u < r.y ? bn.point_list[i + 64u * u] : 0u;
+        for (int s = 0; s < kStrips; s++) c[s] += (e >> (28 + s)) & 1u; }
+    if (b4 + (uint32_t)lane < r.y) { const uint32_t e = bn.point_list[b4 + lane];
 #pragma unroll
-        for (int u = 0; u < 16; u++)
+        for (int s = 0; s < kStrips; s++) c[s] += (e >> (28 + s)) & 1u; }
+    const uint4* __restrict__ q = reinterpret_cast<const uint4*>(bn.point_list + a4);
+    const uint32_t n4 = (b4 - a4) >> 2;
+    for (uint32_t i = lane; i < n4; i += 512) {
+        uint4 e[8];
 #pragma unroll
-            for (int s = 0; s < kStrips; s++) c[s] += (e[u] >> (28 + s)) & 1u;
+        for (int u = 0; u < 8; u++) e[u] = i + 64u * u < n4 ? q[i + 64u * u] : make_uint4(0u, 0u, 0u, 0u);
+#pragma unroll
+        for (int u = 0; u < 8; u++)
+#pragma unroll
+            for (int s = 0; s < kStrips; s++)
+                c[s] += ((e[u].x >> (28 + s)) & 1u) + ((e[u].y >> (28 + s)) & 1u) + ((e[u].z >> (28 + s)) & 1u) +
+                        ((e[u].w >> (28 + s)) & 1u);
     }
 #pragma unroll
     for (int s = 0; s < kStrips; s++) {
