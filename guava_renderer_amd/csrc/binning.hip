@@ -379,21 +379,33 @@ __global__ __launch_bounds__(kScanBlock) void k_bucket_scatter(Dims d, GeomArena
 }
 
 // Small buckets: each key's final position is its bucket start plus the number of smaller keys in
-// the bucket (keys are unique: the index is in the low word).
+// the bucket (keys are unique: the index is in the low word).  A small bucket holding one of the
+// workgroup's keys lies within kTinyBucket of the workgroup's range, so the keys it compares are
+// staged in LDS with that halo (one coalesced load each instead of a global load per comparison).
 __global__ __launch_bounds__(kScanBlock) void k_bucket_rank(Dims d, GeomArena g) {
+    __shared__ uint64_t win[kScanBlock + 2 * kTinyBucket];
     if (g.ctrl[kCtrlOverflow]) return;
     const int b = blockIdx.y;
-    const int j = blockIdx.x * kScanBlock + threadIdx.x;
-    if (j >= (int)g.fstat[kFsWords * b + kFsVisible]) return;
-    const uint32_t kmin = ~g.fstat[kFsWords * b + kFsNotKeyMax], kmax = g.fstat[kFsWords * b + kFsKeyMax];
+    const int V = (int)g.fstat[kFsWords * b + kFsVisible];
+    const int j0 = blockIdx.x * kScanBlock;
+    if (j0 >= V) return;  // (uniform)
     const uint64_t* sk = g.skey + (int64_t)b * d.P;
-    const uint64_t key = sk[j];
+    for (int t = threadIdx.x; t < kScanBlock + 2 * kTinyBucket; t += kScanBlock) {
+        const int m = j0 - kTinyBucket + t;
+        win[t] = (m >= 0 && m < V) ? sk[m] : 0ull;
+    }
+    __syncthreads();
+    const int j = j0 + threadIdx.x;
+    if (j >= V) return;
+    const uint32_t kmin = ~g.fstat[kFsWords * b + kFsNotKeyMax], kmax = g.fstat[kFsWords * b + kFsKeyMax];
+    const uint64_t key = win[threadIdx.x + kTinyBucket];
     const uint32_t bk = bucket_of((uint32_t)(key >> 32), kmin, bucket_scale(kmin, kmax, d.NB), d.NB);
     const uint32_t* bs = g.bstart + (int64_t)b * (d.NB + 1);
     const uint32_t s0 = bs[bk], e0 = bs[bk + 1];
     if (e0 - s0 > (uint32_t)kTinyBucket) return;
     uint32_t r = s0;
-    for (uint32_t m = s0; m < e0; m++) r += sk[m] < key ? 1u : 0u;
+    // (win[m - j0 + kTinyBucket] = sk[m] for m in [j0 - kTinyBucket, j0 + kScanBlock + kTinyBucket))
+    for (int m = (int)s0 - j0 + kTinyBucket; m < (int)e0 - j0 + kTinyBucket; m++) r += win[m] < key ? 1u : 0u;
     g.order[(int64_t)b * d.P + r] = (uint32_t)key;
 }
 
@@ -475,15 +487,45 @@ __global__ __launch_bounds__(kScanBlock) void k_chunk_count(Dims d, GeomArena g)
         }
     }
     __syncthreads();
-    for (int y = threadIdx.x; y < d.gy; y += kScanBlock) {  // prefix along x
-        int acc = 0;
-        for (int x = 0; x < d.gx; x++) { acc += diff[y * W1 + x]; diff[y * W1 + x] = acc; }
+    // 2-D inclusive prefix of the difference array, one wave per row (lanes along x), then one wave
+    // per column (lanes along y; the odd pitch W1 keeps the column reads conflict-free), 64
+    // elements per step with the carry in a register; then the table row is written coalesced
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    constexpr int kWaves = kScanBlock / 64;
+    for (int y = wv; y < d.gy; y += kWaves) {
+        int carry = 0;
+        for (int x0 = 0; x0 < d.gx; x0 += 64) {
+            const int x = x0 + lane;
+            int v = x < d.gx ? diff[y * W1 + x] : 0;
+#pragma unroll
+            for (int o = 1; o < 64; o <<= 1) {
+                const int t = __shfl_up(v, o);
+                if (lane >= o) v += t;
+            }
+            if (x < d.gx) diff[y * W1 + x] = v + carry;
+            carry += __shfl(v, 63);
+        }
+    }
+    __syncthreads();
+    for (int x = wv; x < d.gx; x += kWaves) {
+        int carry = 0;
+        for (int y0 = 0; y0 < d.gy; y0 += 64) {
+            const int y = y0 + lane;
+            int v = y < d.gy ? diff[y * W1 + x] : 0;
+#pragma unroll
+            for (int o = 1; o < 64; o <<= 1) {
+                const int t = __shfl_up(v, o);
+                if (lane >= o) v += t;
+            }
+            if (y < d.gy) diff[y * W1 + x] = v + carry;
+            carry += __shfl(v, 63);
+        }
     }
     __syncthreads();
     uint32_t* row = g.table + ((int64_t)b * d.nchunk + c) * d.T;
-    for (int x = threadIdx.x; x < d.gx; x += kScanBlock) {  // prefix along y, write the row
-        int acc = 0;
-        for (int y = 0; y < d.gy; y++) { acc += diff[y * W1 + x]; row[y * d.gx + x] = (uint32_t)acc; }
+    for (int t = threadIdx.x; t < d.T; t += kScanBlock) {
+        const int y = t / d.gx, x = t - y * d.gx;
+        row[t] = (uint32_t)diff[y * W1 + x];
     }
 }
 
