@@ -88,11 +88,7 @@ inline T* take(char* base, size_t& off, size_t count) {
 
 namespace gsr {
 
-// Scheduling knob read from the environment (no effect on results): GSR_PRIO_ITEMS = render_fwd
-// work items (longest first) run at raised issue priority (default 0).
 static void env_tuning(Inputs& in) {
-    static const uint32_t prio = [] { const char* e = getenv("GSR_PRIO_ITEMS"); return e ? (uint32_t)atoi(e) : 0u; }();
-    in.prio_items = prio;
     in.xcd_map = strip_order_tile_major() ? (uint32_t)xcd_queue_map() : 0u;
 }
 

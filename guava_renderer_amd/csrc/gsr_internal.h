@@ -175,7 +175,6 @@ struct Inputs {
     const float* bg; int64_t s_bg;
     float scale_mod;
     int prefiltered, antialiasing;
-    uint32_t prio_items;  // render_fwd: work items (longest first) that run at raised issue priority
     uint32_t xcd_map;     // render work-queue mapping (queue_item): 1 = tile-affine (strip order tile-major)
 };
 

@@ -46,6 +46,9 @@ namespace gsr {
 #ifndef GSR_SKIP_DEAD
 #define GSR_SKIP_DEAD 0  // 1: skip the blend + MFMAs of a k-step no live pixel takes (measured +2%: off)
 #endif
+#ifndef GSR_LDS_EARLY
+#define GSR_LDS_EARLY 1  // record LDS reads of the next slot issued before this slot's blend
+#endif
 #ifndef GSR_BATCH_NSLOT
 #define GSR_BATCH_NSLOT 3  // pipeline slots of the batched (throughput) kernels
 #endif
@@ -223,6 +226,27 @@ __device__ __forceinline__ void store_half(const Dims& d, const ImageArena& im, 
     }
 }
 
+// An empty tile inside the image (W a multiple of 4): background colour, T = 1, n_contrib = 0,
+// inverse depth 0, as 16-byte stores -- lane l owns pixels 4 (l % 4) .. +3 of tile row l / 4, so each
+// store instruction writes one channel of the whole tile (a quarter of store_strip's instruction
+// count for the same bytes).
+__device__ __forceinline__ void fill_tile(const Dims& d, const ImageArena& im, const Outputs& o, const float* bg,
+                                          int b, int tx, int ty, int lane) {
+    const int64_t HW = (int64_t)d.H * d.W;
+    const int off = (ty * GSR_BY + lane / 4) * d.W + tx * GSR_BX + 4 * (lane % 4);  // first pixel, in floats
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+        o.out_color + (int64_t)b * GSR_C * HW, 0, (int)((int64_t)GSR_C * HW * 4), 0x00020000);
+#pragma unroll 8
+    for (int c = 0; c < GSR_C; c++) {
+        const unsigned v = __float_as_uint(bg[c]);
+        __builtin_amdgcn_raw_buffer_store_b128((uint4x){v, v, v, v}, rs, off * 4, c * (int)HW * 4, 0);
+    }
+    const unsigned one = __float_as_uint(1.0f);
+    *reinterpret_cast<uint4x*>(im.final_T + b * HW + off) = (uint4x){one, one, one, one};
+    *reinterpret_cast<uint4x*>(im.n_contrib + b * HW + off) = (uint4x){0u, 0u, 0u, 0u};
+    if (o.out_invdepth) *reinterpret_cast<uint4x*>(o.out_invdepth + b * HW + off) = (uint4x){0u, 0u, 0u, 0u};
+}
+
 // gsr_refine_prepare: rows [f_0..f_{keep-1}, W.f (n_out values), 0...] of 32 floats.
 __global__ __launch_bounds__(256) void k_refine_prepare(int n, const float* __restrict__ in,
                                                         const float* __restrict__ w, int n_out,
@@ -320,21 +344,32 @@ __device__ __forceinline__ void render_fwd_body(const Dims& d, const Inputs& in,
         }
         if (!q_left) break;
         if (item >= nstrip) {  // empty tile: background everywhere, T = 1
+            const uint64_t te_start = TL ? __builtin_amdgcn_s_memrealtime() : 0;
             const int tile_g = (int)im.work_list[ne + (item - nstrip)];
             const int b = tile_g / d.T;
             const int t = tile_g - b * d.T;
             const floatx16 unused = {};
+            if (ABL == 8) {  /* timing ablation: no empty-tile stores */
+            } else if (!REFINE && (d.W & 3) == 0 && ((reinterpret_cast<uintptr_t>(o.out_color) |
+                                                      reinterpret_cast<uintptr_t>(o.out_invdepth)) & 15u) == 0 &&
+                       (t % d.gx + 1) * GSR_BX <= d.W && (t / d.gx + 1) * GSR_BY <= d.H) {
+                fill_tile(d, im, o, in.bg + in.s_bg * b, b, t % d.gx, t / d.gx, lane);
+            } else
             for (int sp = 0; sp < kStrips; sp++) {
                 int ex0, ey0;
                 strip_origin(t % d.gx, t / d.gx, sp, ex0, ey0);
                 store_strip<true, REFINE>(d, im, o, in.bg + in.s_bg * b, b, ex0, ey0, lane, unused, unused,
                                           1.0f, 0.f, 0u);
             }
+            if (TL && lane == 0 && item < o.timeline_cap) {  // empty tiles: k-steps 0xFFFFFFFF
+                uint32_t* rec = o.timeline + 4 * (size_t)item;
+                rec[0] = (uint32_t)te_start;
+                rec[1] = (uint32_t)__builtin_amdgcn_s_memrealtime();
+                rec[2] = 0xFFFFFFFFu;
+                rec[3] = __builtin_amdgcn_s_getreg((3 << 11) | 20) & 7u;
+            }
             continue;
         }
-        // the longest strips bound the kernel's latency: give them issue priority on their SIMD
-        if ((HALF ? item >> 1 : item) < in.prio_items) __builtin_amdgcn_s_setprio(3);
-        else __builtin_amdgcn_s_setprio(0);
         const uint64_t t_start = TL ? __builtin_amdgcn_s_memrealtime() : 0;
         const uint32_t code = im.strip_list[HALF ? item >> 1 : item];
         const int half = HALF ? (int)(item & 1u) : 0;
@@ -437,7 +472,7 @@ __device__ __forceinline__ void render_fwd_body(const Dims& d, const Inputs& in,
                 if (!S##hb) { gb_ = (uint32_t)d.P; pb_ = pa_; }                                     \
             }                                                                                       \
             S##pa = pa_; S##pb = pb_;                                                               \
-            if (GSR_REC_PATH == 3) {  /* lanes 0..7: dword `lane` of both records, SGPR offsets */  \
+            if (GSR_REC_PATH == 3) {  /* lanes 0..7: dword `lane` of both records, SGPR offsets */ \
                 S##r = __builtin_amdgcn_raw_buffer_load_b32(rrs, rec_voff, (int)(ga_ * 32), 0);     \
                 S##r2 = __builtin_amdgcn_raw_buffer_load_b32(rrs, rec_voff, (int)(gb_ * 32), 0);    \
             } else {                                                                                \
@@ -452,8 +487,9 @@ __device__ __forceinline__ void render_fwd_body(const Dims& d, const Inputs& in,
             S##fb = ABL == 2 ? 0u : __builtin_amdgcn_raw_buffer_load_b32(frs, feat_voff_b,          \
                                                                         (int)(gb_ * (GSR_C * 4)), 0); \
         }
-        // stage 2: the pixel-local alphas of slot S (a missing survivor has alpha 0)
-#define GSR_ALPHA(S)                                                                                \
+        // stage 2: the pixel-local alphas of slot S (a missing survivor has alpha 0): the records
+        // through the wave's LDS slot (GSR_ALPHA_LDS), then the alpha arithmetic (GSR_ALPHA_MATH)
+#define GSR_ALPHA_LDS(S)                                                                            \
         {                                                                                           \
             if (HALF) {  /* each lane its own Gaussian's record: a in lanes 0-31, b in 32-63 */     \
                 rec_lds[rec_widx] = S##r; rec_lds[rec_widx + 8] = S##r2;                            \
@@ -461,18 +497,22 @@ __device__ __forceinline__ void render_fwd_body(const Dims& d, const Inputs& in,
                 S##a0 = __builtin_bit_cast(float4, *(const uint4x*)&rec_lds[8 * hi]);               \
                 S##a1 = __builtin_bit_cast(float4, *(const uint4x*)&rec_lds[8 * hi + 4]);           \
                 __builtin_amdgcn_wave_barrier();                                                    \
+            } else if (GSR_REC_PATH == 3) {  /* uniform-address b128 reads (lanes 8..63: spare) */  \
+                rec_lds[rec_widx] = S##r; rec_lds[rec_widx + 8] = S##r2;                            \
+                __builtin_amdgcn_wave_barrier();                                                    \
+                S##a0 = __builtin_bit_cast(float4, *(const uint4x*)&rec_lds[0]);                    \
+                S##a1 = __builtin_bit_cast(float4, *(const uint4x*)&rec_lds[4]);                    \
+                S##b0 = __builtin_bit_cast(float4, *(const uint4x*)&rec_lds[8]);                    \
+                S##b1 = __builtin_bit_cast(float4, *(const uint4x*)&rec_lds[12]);                   \
+                __builtin_amdgcn_wave_barrier();                                                    \
+            }                                                                                       \
+        }
+#define GSR_ALPHA_MATH(S)                                                                           \
+        {                                                                                           \
+            if (HALF) {                                                                             \
                 S##al = alpha_of<EXACT>(S##a0, S##a1, pfx, pfy);                                    \
                 S##ai = S##a0.w;                                                                    \
             } else {                                                                                \
-                if (GSR_REC_PATH == 3) {  /* through this wave's LDS slot: uniform-address b128 reads */ \
-                    rec_lds[rec_widx] = S##r; rec_lds[rec_widx + 8] = S##r2;  /* lanes 8..63: spare */ \
-                    __builtin_amdgcn_wave_barrier();                                                \
-                    S##a0 = __builtin_bit_cast(float4, *(const uint4x*)&rec_lds[0]);                \
-                    S##a1 = __builtin_bit_cast(float4, *(const uint4x*)&rec_lds[4]);                \
-                    S##b0 = __builtin_bit_cast(float4, *(const uint4x*)&rec_lds[8]);                \
-                    S##b1 = __builtin_bit_cast(float4, *(const uint4x*)&rec_lds[12]);               \
-                    __builtin_amdgcn_wave_barrier();                                                \
-                }                                                                                   \
                 S##al = alpha_of<EXACT>(S##a0, S##a1, pfx, pfy);                                    \
                 S##bl = alpha_of<EXACT>(S##b0, S##b1, pfx, pfy);                                    \
                 S##ai = S##a0.w;                                                                    \
@@ -481,6 +521,14 @@ __device__ __forceinline__ void render_fwd_body(const Dims& d, const Inputs& in,
             S##f = __uint_as_float(S##fa | S##fb);                                                  \
             if (SPLIT) S##fp = SPLIT == 2 ? __float_as_uint(S##f) : split_hl(S##f);                 \
         }
+#define GSR_ALPHA(S) GSR_ALPHA_LDS(S) GSR_ALPHA_MATH(S)
+        // GSR_LDS_EARLY: slot S+1's record reads are issued before slot S's serial blend, so the LDS
+        // latency runs under the blend (the alpha arithmetic of S+1 still follows it)
+#if GSR_LDS_EARLY
+#define GSR_STEP(N, S) GSR_ALPHA_LDS(N) __builtin_amdgcn_sched_barrier(0); GSR_TAKE(S) GSR_ALPHA_MATH(N)
+#else
+#define GSR_STEP(N, S) GSR_ALPHA(N) GSR_TAKE(S)
+#endif
         // stage 3: the serial blend of slot S and its accumulation on the matrix cores
 #define GSR_TAKE(S)                                                                                 \
         if (HALF) {  /* both alphas to every lane (one swap each), the pixel's blend duplicated */ \
@@ -580,14 +628,11 @@ __device__ __forceinline__ void render_fwd_body(const Dims& d, const Inputs& in,
             GSR_FETCH(C)
             GSR_ALPHA(A)
             while (Av) {
-                GSR_ALPHA(B)
-                GSR_TAKE(A)
+                GSR_STEP(B, A)
                 GSR_FETCH(A)
-                GSR_ALPHA(C)
-                GSR_TAKE(B)
+                GSR_STEP(C, B)
                 GSR_FETCH(B)
-                GSR_ALPHA(A)
-                GSR_TAKE(C)
+                GSR_STEP(A, C)
                 GSR_FETCH(C)
                 if (!__any(!done)) break;  // every pixel of the strip finished
             }
@@ -603,20 +648,15 @@ __device__ __forceinline__ void render_fwd_body(const Dims& d, const Inputs& in,
             GSR_FETCH(E)
             GSR_ALPHA(A)
             while (Av) {
-                GSR_ALPHA(B)
-                GSR_TAKE(A)
+                GSR_STEP(B, A)
                 GSR_FETCH(A)
-                GSR_ALPHA(C)
-                GSR_TAKE(B)
+                GSR_STEP(C, B)
                 GSR_FETCH(B)
-                GSR_ALPHA(D)
-                GSR_TAKE(C)
+                GSR_STEP(D, C)
                 GSR_FETCH(C)
-                GSR_ALPHA(E)
-                GSR_TAKE(D)
+                GSR_STEP(E, D)
                 GSR_FETCH(D)
-                GSR_ALPHA(A)
-                GSR_TAKE(E)
+                GSR_STEP(A, E)
                 GSR_FETCH(E)
                 if (!__any(!done)) break;
             }
@@ -624,6 +664,9 @@ __device__ __forceinline__ void render_fwd_body(const Dims& d, const Inputs& in,
 #undef GSR_NEXT
 #undef GSR_FETCH
 #undef GSR_ALPHA
+#undef GSR_ALPHA_LDS
+#undef GSR_ALPHA_MATH
+#undef GSR_STEP
 #undef GSR_TAKE
 #undef GSR_SLOT
 
@@ -676,7 +719,7 @@ __attribute__((amdgpu_waves_per_eu((NSLOT == 5 && !HALF) ? 3 : GSR_RENDER_WPE)))
 
 // Timing ablations of the production kernel (GSR_RENDER_ABLATE=1: VALU stand-in for the MFMAs,
 // 4: bf16 32x32x16 MFMAs on dummy operands in place of the f32 ones,
-// 2: no feature loads).  Wrong images by construction; for attributing render_fwd time only.
+// 2: no feature loads, 8: no empty-tile stores).  Wrong images by construction; for attributing render_fwd time only.
 template <int ABL>
 __global__ __launch_bounds__(GSR_TILE_PIX) void k_render_fwd_ablate(Dims d, Inputs in, GeomArena g,
                                                                     ImageArena im, BinArena bn, Outputs o) {
@@ -723,6 +766,7 @@ void launch_render_fwd(const Dims& d, const Inputs& in_, const GeomArena& g, con
     else if (ablate == 1) hipLaunchKernelGGL((k_render_fwd_ablate<1>), gr, bl, 0, s, d, in, g, im, b, o);
     else if (ablate == 2) hipLaunchKernelGGL((k_render_fwd_ablate<2>), gr, bl, 0, s, d, in, g, im, b, o);
     else if (ablate == 4) hipLaunchKernelGGL((k_render_fwd_ablate<4>), gr, bl, 0, s, d, in, g, im, b, o);
+    else if (ablate == 8) hipLaunchKernelGGL((k_render_fwd_ablate<8>), gr, bl, 0, s, d, in, g, im, b, o);
     else if (d.B == 1 && latency_mode && half_mode) {
         // one frame, half-strip waves: a strip's two halves run in parallel, each lane one
         // (pixel, Gaussian) alpha per k-step -- the longest strip's time is what counts here

@@ -32,9 +32,10 @@ rast.forward(*args)
 torch.cuda.synchronize()
 L.gsr_render_timeline(None, 0)
 os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)
-np.savez_compressed(os.path.join(ROOT, "gpurun_out", "timeline.npz"), tl=tl.cpu().numpy(), cnt=cnt.cpu().numpy())
-tl = tl.cpu().numpy().astype(np.int64)
-tl = tl[tl[:, 1] > 0]
+np.savez_compressed(os.path.join(ROOT, "gpurun_out", os.environ.get("TL_OUT", "timeline.npz")), tl=tl.cpu().numpy(), cnt=cnt.cpu().numpy())
+tl = tl.cpu().numpy()
+tl = tl[tl[:, 1] != 0].astype(np.uint32).astype(np.int64)
+tl[:, 1] += (tl[:, 1] < tl[:, 0]) * (1 << 32)  # 32-bit tick wrap inside an item
 dur = tl[:, 1] - tl[:, 0]
 span = tl[:, 1].max() - tl[:, 0].min()
 print(f"items {len(tl)} span {span / 100:.1f} us, longest item {dur.max() / 100:.1f} us ({tl[dur.argmax(), 2]} k-steps), "
