@@ -49,6 +49,9 @@ namespace gsr {
 #ifndef GSR_LDS_EARLY
 #define GSR_LDS_EARLY 1  // record LDS reads of the next slot issued before this slot's blend
 #endif
+#ifndef GSR_STORE_AUX
+#define GSR_STORE_AUX 0  // cache-policy bits of the strip epilogue's colour stores (2 = nt)
+#endif
 #ifndef GSR_BATCH_NSLOT
 #define GSR_BATCH_NSLOT 3  // pipeline slots of the batched (throughput) kernels
 #endif
@@ -146,6 +149,10 @@ __device__ __forceinline__ void store_strip(const Dims& d, const ImageArena& im,
     }
     const float T0 = __shfl(T, lane & 31);
     const float T1 = __shfl(T, 32 + (lane & 31));
+    // the background: one load of bg[lane % 32], then each register's channel (which differs
+    // between the half-waves) by ds_bpermute -- a per-lane `hi ? bg[c + 4] : bg[c]` compiled to 16
+    // dependent global loads, each waited for before its stores
+    const float bgl = bg[lane & 31];
     // channel rows through a buffer resource: one VGPR byte offset per half-strip row, the channel
     // offset in an SGPR; pixels outside the image get an offset past the buffer and are dropped
     const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
@@ -165,13 +172,13 @@ __device__ __forceinline__ void store_strip(const Dims& d, const ImageArena& im,
 #pragma unroll
     for (int r = 0; r < 16; r++) {
         const int c = (r & 3) + 8 * (r >> 2);  // + 4 in the upper half-wave (in hoff)
-        const float bgc = hi ? bg[c + 4] : bg[c];
+        const float bgc = __shfl(bgl, c + 4 * hi);
         const int so = c * (int)HW * 4;
         float x0 = EMPTY ? bgc : fmaf(T0, bgc, acc0[r]);
         float x1 = EMPTY ? bgc : fmaf(T1, bgc, acc1[r]);
         if (!REFINE) {
-            __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(x0), rs, v0, so, 0);
-            __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(x1), rs, v1, so, 0);
+            __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(x0), rs, v0, so, GSR_STORE_AUX);
+            __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(x1), rs, v1, so, GSR_STORE_AUX);
         } else {
             // branch-free: every channel is offered to both outputs; the one it does not belong to
             // gets an offset past its buffer (dropped by the buffer range check)
@@ -218,10 +225,11 @@ __device__ __forceinline__ void store_half(const Dims& d, const ImageArena& im, 
         o.out_color + (int64_t)b * GSR_C * HW, 0, (int)((int64_t)GSR_C * HW * 4), 0x00020000);
     const int hi = lane >> 5;
     const int v = in_img ? (hi * 4 * (int)HW + qy * d.W + qx) * 4 : 0x7FFFFFF0;
+    const float bgl = bg[lane & 31];  // (as store_strip)
 #pragma unroll
     for (int r = 0; r < 16; r++) {
         const int c = (r & 3) + 8 * (r >> 2);  // + 4 in the upper half-wave (in v)
-        const float bgc = hi ? bg[c + 4] : bg[c];
+        const float bgc = __shfl(bgl, c + 4 * hi);
         __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(fmaf(T, bgc, acc[r])), rs, v, c * (int)HW * 4, 0);
     }
 }
@@ -698,6 +706,9 @@ __device__ __forceinline__ void render_fwd_body(const Dims& d, const Inputs& in,
         }
         if constexpr (HALF) store_half(d, im, o, in.bg + in.s_bg * b, b, sx0, sy0 + half * (32 / kStripW), lane,
                                        acc0, T, invd, last);
+        else if (ABL == 9) {  /* timing ablation: only final_T of the strip is stored */
+            if (px < d.W && py < d.H) im.final_T[b * (int64_t)d.H * d.W + (int64_t)py * d.W + px] = T + acc0[0] + acc1[0];
+        }
         else store_strip<false, REFINE>(d, im, o, in.bg + in.s_bg * b, b, sx0, sy0, lane, acc0, acc1, T,
                                         invd, last);
     }
@@ -719,7 +730,7 @@ __attribute__((amdgpu_waves_per_eu((NSLOT == 5 && !HALF) ? 3 : GSR_RENDER_WPE)))
 
 // Timing ablations of the production kernel (GSR_RENDER_ABLATE=1: VALU stand-in for the MFMAs,
 // 4: bf16 32x32x16 MFMAs on dummy operands in place of the f32 ones,
-// 2: no feature loads, 8: no empty-tile stores).  Wrong images by construction; for attributing render_fwd time only.
+// 2: no feature loads, 8: no empty-tile stores, 9: no strip colour stores).  Wrong images by construction; for attributing render_fwd time only.
 template <int ABL>
 __global__ __launch_bounds__(GSR_TILE_PIX) void k_render_fwd_ablate(Dims d, Inputs in, GeomArena g,
                                                                     ImageArena im, BinArena bn, Outputs o) {
@@ -767,6 +778,7 @@ void launch_render_fwd(const Dims& d, const Inputs& in_, const GeomArena& g, con
     else if (ablate == 2) hipLaunchKernelGGL((k_render_fwd_ablate<2>), gr, bl, 0, s, d, in, g, im, b, o);
     else if (ablate == 4) hipLaunchKernelGGL((k_render_fwd_ablate<4>), gr, bl, 0, s, d, in, g, im, b, o);
     else if (ablate == 8) hipLaunchKernelGGL((k_render_fwd_ablate<8>), gr, bl, 0, s, d, in, g, im, b, o);
+    else if (ablate == 9) hipLaunchKernelGGL((k_render_fwd_ablate<9>), gr, bl, 0, s, d, in, g, im, b, o);
     else if (d.B == 1 && latency_mode && half_mode) {
         // one frame, half-strip waves: a strip's two halves run in parallel, each lane one
         // (pixel, Gaussian) alpha per k-step -- the longest strip's time is what counts here
