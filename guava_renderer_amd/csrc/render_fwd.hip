@@ -398,6 +398,17 @@ __device__ __forceinline__ void render_fwd_body(const Dims& d, const Inputs& in,
         float T = 1.0f, invd = 0.f;
         uint32_t last = 0, stop = 0;
         const uint32_t smask_bit = 1u << (28 + strip);
+        if (!STATS && !TL && im.strip_cnt[(int64_t)tile_g * kStrips + strip] == 0u) {
+            // no list entry reaches the strip (k_strip_count): nothing is taken anywhere in it, so
+            // its outputs are the background, T = 1, n_contrib = 0, inverse depth 0 -- the values
+            // the list walk would give -- without walking the tile's list
+            const floatx16 zero = {};
+            if constexpr (HALF) store_half(d, im, o, in.bg + in.s_bg * b, b, sx0, sy0 + half * (32 / kStripW), lane,
+                                           zero, 1.0f, 0.f, 0u);
+            else store_strip<false, REFINE>(d, im, o, in.bg + in.s_bg * b, b, sx0, sy0, lane, zero, zero, 1.0f,
+                                            0.f, 0u);
+            continue;
+        }
         const uint2 range = im.ranges[tile_g];
         const int n = (int)(range.y - range.x);
         const uint32_t* __restrict__ plist = bn.point_list + range.x;
