@@ -17,7 +17,7 @@ fi
 DST=${2:-$DEF}
 OUT=gpurun_out/pmc_$PIPE
 mkdir -p $OUT
-B="python3 bench.py --pipeline $PIPE --batch $BATCH --no-cpu-baseline --no-extras --steps 3 --warmup 1"
+B="python3 bench.py --pipeline $PIPE --batch $BATCH --inflight 1 --no-cpu-baseline --no-extras --steps 3 --warmup 1"
 if [ ! -x tools/micro/fetch_calib ]; then
   /opt/rocm/bin/hipcc -O2 --offload-arch=gfx950 tools/micro/fetch_calib.hip -o tools/micro/fetch_calib || exit 1
 fi
