@@ -70,9 +70,9 @@ def _args():
                     help="train = BASELINE config 4: raster fwd + fused-SSIM/L1 loss + raster bwd + "
                          "gradient all-reduce + Adam; frame = GUAVA's unchanged caller: "
                          "one GaussianRasterizer_32 call per frame as gaussian_render.py:37-67 does")
-    ap.add_argument("--inflight", type=int, default=2,
-                    help="batches in flight on separate HIP streams (avatar/raster pipelines; default 2: "
-                         "one batch's deform + binning chain runs beside the other's compositing); "
+    ap.add_argument("--inflight", type=int, default=4,
+                    help="batches in flight on separate HIP streams (avatar/raster pipelines; default 4: "
+                         "the deform + binning chains of the next batches run beside one batch's compositing); "
                          "kernel times for the roofline then come from an isolated pass")
     ap.add_argument("--refine", action="store_true",
                     help="fuse the refiner's first 1x1 conv 32->16 + leaky ReLU into the render "
