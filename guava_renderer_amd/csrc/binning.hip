@@ -314,9 +314,23 @@ __global__ __launch_bounds__(kCountThreads) void k_bucket_count_lds(Dims d, Geom
     }
     __syncthreads();
     uint32_t* bs = g.bstart + (int64_t)b * (d.NB + 1);
-    for (int k = threadIdx.x; k < d.NB; k += kCountThreads) {
-        const uint32_t c = hist[k];
-        if (c) hist[k] = atomicAdd(&bs[k], c);
+    // the workgroup's claims, all of a thread's returning atomics in flight together (NB <= 16384
+    // = 16 per thread here; a loop that waits for each claim before the next costs a frame's
+    // latency-bound single launch ~16 memory round trips)
+    constexpr int kClaims = 16384 / kCountThreads;
+    uint32_t cl[kClaims];
+#pragma unroll
+    for (int j = 0; j < kClaims; j++) {
+        const int k = threadIdx.x + j * kCountThreads;
+        cl[j] = k < d.NB ? hist[k] : 0u;
+    }
+#pragma unroll
+    for (int j = 0; j < kClaims; j++)
+        if (cl[j]) cl[j] = atomicAdd(&bs[threadIdx.x + j * kCountThreads], cl[j]);
+#pragma unroll
+    for (int j = 0; j < kClaims; j++) {
+        const int k = threadIdx.x + j * kCountThreads;
+        if (k < d.NB && hist[k]) hist[k] = cl[j];
     }
     __syncthreads();
 #pragma unroll
