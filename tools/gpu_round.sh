@@ -14,7 +14,7 @@ if [ -z "${SKIP_TESTS:-}" ]; then
 fi
 timeout -k 10 300 python bench.py > $OUT/bench.json 2> $OUT/bench.err; rc=$?; echo "bench rc=$rc"; cat $OUT/bench.json
 [ $rc -eq 0 ] || { tail -20 $OUT/bench.err; exit $rc; }
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/kt -o run --output-format csv -- python3 bench.py --no-cpu-baseline --no-extras --steps 100 --warmup 10 > $OUT/kt.log 2>&1; rc=$?; echo "kt rc=$rc"
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/kt -o run --output-format csv -- python3 bench.py --inflight 1 --no-cpu-baseline --no-extras --steps 100 --warmup 10 > $OUT/kt.log 2>&1; rc=$?; echo "kt rc=$rc"
 [ $rc -eq 0 ] || exit $rc
 timeout -k 10 300 python bench.py --pipeline train --steps 200 --warmup 10 > $OUT/bench_train.json 2> $OUT/bench_train.err; rc=$?; echo "train rc=$rc"; tail -1 $OUT/bench_train.json
 exit $rc
