@@ -70,9 +70,10 @@ def _args():
                     help="train = BASELINE config 4: raster fwd + fused-SSIM/L1 loss + raster bwd + "
                          "gradient all-reduce + Adam; frame = GUAVA's unchanged caller: "
                          "one GaussianRasterizer_32 call per frame as gaussian_render.py:37-67 does")
-    ap.add_argument("--inflight", type=int, default=4,
-                    help="batches in flight on separate HIP streams (avatar/raster pipelines; default 4: "
-                         "the deform + binning chains of the next batches run beside one batch's compositing); "
+    ap.add_argument("--inflight", type=int, default=None,
+                    help="batches in flight on separate HIP streams (avatar/raster pipelines; default 4 at c2, "
+                         "2 at the render-bound c5: the deform + binning chains of the next batches run beside "
+                         "one batch's compositing; at N>1 at most GPU_MAX_HW_QUEUES - 1, parallel.stream_budget); "
                          "kernel times for the roofline then come from an isolated pass")
     ap.add_argument("--refine", action="store_true",
                     help="fuse the refiner's first 1x1 conv 32->16 + leaky ReLU into the render "
@@ -90,6 +91,8 @@ def _args():
     a = ap.parse_args()
     if a.batch is None:
         a.batch = 6 if a.pipeline == "train" else 32
+    if a.inflight is None:
+        a.inflight = 2 if a.config == "c5" else 4
     return a
 
 
@@ -423,6 +426,8 @@ def main():
     else:
         B, scaling, n_total = a.batch, "weak", a.batch * world
     lo = rank * B
+    # hardware-queue budget: at N>1 one of the GPU_MAX_HW_QUEUES queues stays free for RCCL
+    a.inflight = parallel.stream_budget(a.inflight, world)
     w = Workload(a, wl, B, lo, n_total, dev, numerics)
     P = w.P
     workload = wl["name"] + {"avatar": "-deform+raster" + ("-cross" if a.config == "c5" else ""),
@@ -442,11 +447,12 @@ def main():
         gdev = dev if backend == "nccl" else torch.device("cpu")
         return parallel.FrameGather(b, (3, H, W), torch.uint8 if a.gather == "u8" else torch.float32, gdev)
 
-    def make_step(wk, gatherer):
+    def make_step(wk, gatherer, inflight=None):
         cnt = [0]
+        nin = n_inflight if inflight is None else inflight
 
         def step():
-            i = cnt[0] % n_inflight
+            i = cnt[0] % nin
             cnt[0] += 1
             with torch.cuda.stream(streams[i]):
                 res = wk.step_on(i)
@@ -541,6 +547,13 @@ def main():
         other_line = {"value": round(B * n_o / el_o, 2), "ms_per_step": round(1e3 * el_o / n_o, 4), "steps": n_o,
                       "colour_accum": "split-bf16 mfma (<=1e-4 L_inf)" if other & _lib.NUMERICS_SPLIT_BF16
                       else "f32 mfma (bit-exact with the oracle)"}
+    # the same workload with one batch in flight (kernel-level gain vs overlap gain, same process)
+    one_line = None
+    if extras and dist is None and n_inflight > 1 and a.pipeline in ("avatar", "raster"):
+        n_1 = max(20, a.steps // 4)
+        el_1 = timed(make_step(w, None, inflight=1), None, n_1, 3)
+        one_line = {"value": round(B * n_1 / el_1, 2), "ms_per_step": round(1e3 * el_1 / n_1, 4), "steps": n_1,
+                    "batches_in_flight": 1}
     # work counters of one extra (instrumented, untimed) step: which wall the render kernel hits
     work = render_counters(step, device=dev)
     # config 3 at N>1: the 32-frame batch split over the ranks (strong scaling) beside the weak line
@@ -668,6 +681,8 @@ def main():
         out["split_bf16" if not split_head else "exact_accum"] = other_line
     if strong_line is not None:
         out["config3_strong"] = strong_line
+    if one_line is not None:
+        out["one_in_flight"] = one_line
     if a.stages:
         out["stage_ms_per_step"] = {k: round(v[0] / max(v[1], 1), 4) for k, v in prof.items()}
     if extras and world == 1 and a.pipeline == "avatar":

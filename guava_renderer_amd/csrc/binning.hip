@@ -289,6 +289,11 @@ __global__ __launch_bounds__(kScanBlock) void k_bucket_count(Dims d, GeomArena g
 // memory side (MI355X_MICROARCH.md, global atomics), so this cuts them by the Gaussians per
 // (workgroup, bucket).
 constexpr int kCountThreads = 1024, kCountPer = 8;
+// the LDS bucket table of k_bucket_count_lds: at most kLdsBuckets buckets (64 KB), each claimed by
+// the register array cl[kLdsBuckets / kCountThreads] below; launch_depth_sort takes the global-atomic
+// kernel above that size, and make_dims' nb_cap keeps NB there for every P it serves
+constexpr int kLdsBuckets = 16384;
+static_assert(kLdsBuckets % kCountThreads == 0, "bucket claims: whole rows of the workgroup");
 __global__ __launch_bounds__(kCountThreads) void k_bucket_count_lds(Dims d, GeomArena g) {
     extern __shared__ uint32_t hist[];  // NB
     if (g.ctrl[kCtrlOverflow]) return;
@@ -317,7 +322,7 @@ __global__ __launch_bounds__(kCountThreads) void k_bucket_count_lds(Dims d, Geom
     // the workgroup's claims, all of a thread's returning atomics in flight together (NB <= 16384
     // = 16 per thread here; a loop that waits for each claim before the next costs a frame's
     // latency-bound single launch ~16 memory round trips)
-    constexpr int kClaims = 16384 / kCountThreads;
+    constexpr int kClaims = kLdsBuckets / kCountThreads;
     uint32_t cl[kClaims];
 #pragma unroll
     for (int j = 0; j < kClaims; j++) {
@@ -454,7 +459,7 @@ __global__ __launch_bounds__(NT) void k_bucket_sort(Dims d, GeomArena g) {
 
 void launch_depth_sort(const Dims& d, const GeomArena& g, hipStream_t s) {
     if (d.P == 0 || d.B == 0) return;
-    if ((size_t)d.NB * 4 <= 65536) {
+    if (d.NB <= kLdsBuckets) {  // every bucket has a claim slot (kClaims per thread)
         const int per_wg = kCountThreads * kCountPer;
         hipLaunchKernelGGL(k_bucket_count_lds, dim3((d.P + per_wg - 1) / per_wg, d.B), dim3(kCountThreads),
                            (size_t)d.NB * 4, s, d, g);

@@ -11,6 +11,7 @@ shared avatar (the DP gradient all-reduce a trainer would do; one flat bucket, s
 rings are per-link bound and favour few large messages).
 """
 import ctypes
+import os
 
 import torch
 import torch.distributed as dist
@@ -69,59 +70,79 @@ def frames_to8b(frames, channels=3, out=None):
     return out
 
 
+def to8b_host(frames, channels):
+    """Host to8b of the first `channels` planes of [B, C, H, W] frames (utils/general_utils.py:316-317:
+    (255 * clip(x, 0, 1)).astype(uint8), truncation toward zero, NaN -> 0 as frames_to8b)."""
+    x = torch.nan_to_num(frames[:, :channels].float(), nan=0.0).clamp_(0.0, 1.0)
+    return (x * 255.0).to(torch.uint8)
+
+
+def stream_budget(inflight, world, hw_queues=None):
+    """Compute streams the bench may keep busy: GPU_MAX_HW_QUEUES hardware queues per process (4 on
+    the box, HIP's default); at N > 1 one of them is left to the collective (ProcessGroupNCCL runs
+    every RCCL call on its own internal stream), so the all-gather never queues behind a persistent
+    render kernel on a shared hardware queue."""
+    if hw_queues is None:
+        hw_queues = int(os.environ.get("GPU_MAX_HW_QUEUES", "4") or 4)
+    reserved = 1 if world > 1 else 0
+    return max(1, min(int(inflight), hw_queues - reserved))
+
+
 class FrameGather:
     """Overlapped all-gather of a stream of equal per-rank batches [n_local, *shape] into
     [world * n_local, *shape] on every rank (frame order = rank order, as shard_range's contiguous
-    slices).  `push(frames)` copies the rank's frames into a staging buffer on the current stream
-    and starts the collective on a side stream once they are written, so batch i's exchange runs
-    under batch i+1's rendering; `n_buffers` batches may be in flight (a push waits for the
-    exchange that last used its buffer).  `wait()` orders the current stream after every exchange
-    pushed so far and returns the latest gathered batch.  One collective per batch, no padding and
-    no concatenation (RCCL rings over xGMI are per-link bound: one large message per batch).
-    With dtype uint8 and float32 [n_local, C, H, W] frames pushed on a HIP device, push() encodes
-    the first shape[0] planes with frames_to8b straight into the staging buffer (the consumer's
-    8-bit frames, 4x fewer bytes on the links than f32)."""
+    slices).  `push(frames)` writes the rank's frames into a staging buffer on the current stream
+    and issues the collective asynchronously: RCCL runs it on ProcessGroupNCCL's internal stream once
+    the staging write is done (no side stream of our own: with GPU_MAX_HW_QUEUES = 4 the bench keeps
+    3 compute streams + that one, `stream_budget`), so batch i's exchange runs under batch i+1's
+    rendering; `n_buffers` batches may be in flight (a push orders its stream after the exchange
+    that last used its buffer).  `wait()` orders the current stream after every exchange pushed so
+    far and returns the latest gathered batch.  One collective per batch, no padding and no
+    concatenation (RCCL rings over xGMI are per-link bound: one large message per batch).
+    With dtype uint8 and float32 [n_local, C, H, W] frames, push() encodes the first shape[0]
+    planes as to8b: frames_to8b straight into the staging buffer when both are on the same HIP
+    device, the host form (to8b_host) otherwise (the consumer's 8-bit frames, 4x fewer bytes on the
+    links than f32)."""
 
     def __init__(self, n_local, shape, dtype, device, group=None, n_buffers=2):
         self.group = group
         self.world = dist.get_world_size(group)
-        self.stream = torch.cuda.Stream(device) if device.type == "cuda" else None
+        self.device = device
         self.bufs = [(torch.empty((n_local,) + tuple(shape), dtype=dtype, device=device),
                       torch.empty((self.world * n_local,) + tuple(shape), dtype=dtype, device=device))
                      for _ in range(n_buffers)]
-        self.done = [None] * n_buffers
+        self.work = [None] * n_buffers
         self.k = 0
         self.last = None
+
+    def _stage(self, src, frames):
+        if src.dtype == torch.uint8 and frames.dtype == torch.float32:
+            if frames.is_cuda and src.is_cuda and frames.device == src.device:
+                frames_to8b(frames, src.shape[1], out=src)
+            else:
+                src.copy_(to8b_host(frames, src.shape[1]))
+        else:
+            src.copy_(frames)
 
     def push(self, frames):
         j = self.k % len(self.bufs)
         self.k += 1
         src, dst = self.bufs[j]
-        if self.stream is None:  # CPU (gloo): synchronous
-            src.copy_(frames)
+        if self.device.type != "cuda":  # CPU (gloo): synchronous
+            self._stage(src, frames)
             dist.all_gather_into_tensor(dst, src, group=self.group)
             self.last = dst
             return
-        cur = torch.cuda.current_stream(src.device)
-        if self.done[j] is not None:
-            cur.wait_event(self.done[j])  # the exchange that last read src / wrote dst
-        if src.dtype == torch.uint8 and frames.dtype == torch.float32:
-            frames_to8b(frames, src.shape[1], out=src)
-        else:
-            src.copy_(frames)
-        ready = torch.cuda.Event()
-        ready.record(cur)
-        with torch.cuda.stream(self.stream):
-            self.stream.wait_event(ready)
-            dist.all_gather_into_tensor(dst, src, group=self.group)
-            ev = torch.cuda.Event()
-            ev.record(self.stream)
-        self.done[j] = ev
+        if self.work[j] is not None:
+            self.work[j].wait()  # the current stream waits for the exchange that last read src / wrote dst
+        self._stage(src, frames)
+        self.work[j] = dist.all_gather_into_tensor(dst, src, group=self.group, async_op=True)
         self.last = dst
 
     def wait(self):
-        if self.stream is not None:
-            torch.cuda.current_stream(self.bufs[0][0].device).wait_stream(self.stream)
+        for wk in self.work:
+            if wk is not None:
+                wk.wait()
         return self.last
 
 

@@ -462,6 +462,54 @@ void gsro_render_counts(int W, int H, const uint32_t* ranges, const uint32_t* po
     out[1] = contrib;
 }
 
+/* Decision flips between the two blend exps (test infrastructure): per pixel, walks the loop of
+ * forward.cu:349-381 twice in lockstep -- once with the restatement's exp (exact_exp = 1), once
+ * with libm expf (the nearest this container has to CUDA's expf) -- and sets flags[pix] = 1 when any
+ * pair's take decision (alpha >= 1/255) or stop decision (T (1 - alpha) < 1e-4) differs.  Those are
+ * the pixels where two exps a few ulp apart legitimately give different colours (SURVEY.md §7,
+ * "exp() ulp differences"); everywhere else the images agree to the alphas' rounding.
+ * Returns the number of flagged pixels. */
+uint64_t gsro_render_decision_flips(int W, int H, const uint32_t* ranges, const uint32_t* point_list,
+                                    const float* means2D, const float* conic_opacity, uint8_t* flags) {
+    const int gx = (W + BX - 1) / BX, gy = (H + BY - 1) / BY;
+    uint64_t nflip = 0;
+#pragma omp parallel for schedule(dynamic, 1) num_threads(gsro_get_threads()) reduction(+ : nflip)
+    for (int tile = 0; tile < gx * gy; tile++) {
+        const int tx = tile % gx, ty = tile / gx;
+        const uint32_t start = ranges[2 * tile], end = ranges[2 * tile + 1];
+        for (int ly = 0; ly < BY; ly++)
+            for (int lx = 0; lx < BX; lx++) {
+                const int x = tx * BX + lx, y = ty * BY + ly;
+                if (x >= W || y >= H) continue;
+                float T0 = 1.0f, T1 = 1.0f;
+                int done0 = 0, done1 = 0, flip = 0;
+                for (uint32_t j = start; j < end && !(done0 && done1) && !flip; j++) {
+                    const uint32_t g = point_list[j];
+                    const float* co = conic_opacity + 4 * (size_t)g;
+                    const float dx = means2D[2 * (size_t)g] - (float)x;
+                    const float dy = means2D[2 * (size_t)g + 1] - (float)y;
+                    const float A = -0.5f * co[0], Bb = -co[1], Cq = -0.5f * co[2];
+                    const float power = fmaf(dy, fmaf(Cq, dy, Bb * dx), (A * dx) * dx);
+                    if (power > 0.0f) continue;
+                    const float a0 = gsro_blend_alpha(co[3], power, 1);
+                    const float a1 = gsro_blend_alpha(co[3], power, 0);
+                    const int take0 = !(a0 < 1.0f / 255.0f), take1 = !(a1 < 1.0f / 255.0f);
+                    if (take0 != take1) { flip = 1; break; }
+                    if (!take0) continue;
+                    const float t0 = T0 * (1.0f - a0), t1 = T1 * (1.0f - a1);
+                    const int stop0 = t0 < 0.0001f, stop1 = t1 < 0.0001f;
+                    if (stop0 != stop1) { flip = 1; break; }
+                    if (stop0) { done0 = done1 = 1; break; }
+                    T0 = t0;
+                    T1 = t1;
+                }
+                flags[(size_t)W * y + x] = (uint8_t)flip;
+                nflip += (uint64_t)flip;
+            }
+    }
+    return nflip;
+}
+
 void gsro_render_backward(int W, int H, const uint32_t* ranges, const uint32_t* point_list,
                           const float* bg, const float* means2D, const float* conic_opacity,
                           const float* colors, const float* depths, const float* final_T,

@@ -83,6 +83,9 @@ void gsro_render(int W, int H, const uint32_t* ranges, const uint32_t* point_lis
 void gsro_render_counts(int W, int H, const uint32_t* ranges, const uint32_t* point_list,
                         const float* means2D, const float* conic_opacity, int exact_exp,
                         uint64_t* out);
+/* Pixels whose take/stop decisions differ between exact_exp = 1 and libm expf (test only). */
+uint64_t gsro_render_decision_flips(int W, int H, const uint32_t* ranges, const uint32_t* point_list,
+                                    const float* means2D, const float* conic_opacity, uint8_t* flags);
 void gsro_render_backward(int W, int H, const uint32_t* ranges, const uint32_t* point_list,
                           const float* bg, const float* means2D, const float* conic_opacity,
                           const float* colors, const float* depths, const float* final_T,

@@ -56,6 +56,8 @@ def lib():
                                   ctypes.c_int, _f, _f, _f, _u32]
         L.gsro_render_counts.argtypes = [ctypes.c_int, ctypes.c_int, _u32, _u32, _f, _f, ctypes.c_int,
                                          _u64]
+        L.gsro_render_decision_flips.restype = ctypes.c_uint64
+        L.gsro_render_decision_flips.argtypes = [ctypes.c_int, ctypes.c_int, _u32, _u32, _f, _f, _u8]
         L.gsro_render_backward.argtypes = [ctypes.c_int, ctypes.c_int, _u32, _u32, _f, _f, _f, _f,
                                            _f, _f, _u32, _f, _f, ctypes.c_int, _f, _f, _f, _f, _f]
         L.gsro_preprocess_backward.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, _f, _i, _f,
@@ -180,6 +182,16 @@ def render_counts(st, W, H, exact_exp=True):
                              _p(st["means2D"], _f), _p(st["conic_opacity"], _f), int(bool(exact_exp)),
                              _p(out, _u64))
     return int(out[0]), int(out[1])
+
+
+def decision_flips(st, W, H):
+    """Pixels whose blend takes or stops differently with the restatement's exp and with libm expf
+    (gsro_render_decision_flips): bool [H, W]."""
+    flags = np.zeros(W * H, np.uint8)
+    pl = st["point_list"] if st["R"] > 0 else np.zeros(1, np.uint32)
+    lib().gsro_render_decision_flips(int(W), int(H), _p(st["ranges"], _u32), _p(pl, _u32),
+                                     _p(st["means2D"], _f), _p(st["conic_opacity"], _f), _p(flags, _u8))
+    return flags.reshape(H, W).astype(bool)
 
 
 def forward(means3D, colors, opacities, scales, rotations, cov3D_precomp, view, proj, W, H, tanx,

@@ -73,6 +73,48 @@ def all_cases():
     return cases
 
 
+def _teeth_template(n_teeth=120, seed=31):
+    """SMPL-X template (10,475 vertices) + 120 teeth vertices, the V = 10,595 of EHM's body mesh
+    (SMPLX.py:470-481 appends the teeth): synthetic teeth near the mouth region (the template's
+    front-most head vertices, jittered by 2 mm)."""
+    verts, _, _ = avatar.template_mesh()
+    rng = np.random.default_rng(seed)
+    head = np.nonzero(verts[:, 1] > np.percentile(verts[:, 1], 92))[0]
+    front = head[np.argsort(-verts[head, 2])[: 4 * n_teeth]]
+    pick = rng.choice(front, n_teeth, replace=False)
+    teeth = verts[pick] + rng.normal(0.0, 0.002, (n_teeth, 3))
+    return np.concatenate([verts, teeth]).astype(np.float32)
+
+
+def full_cases():
+    """SURVEY.md §8(c)'s full-size cases: SMPL-X body lbs_wobeta at V = 10,595, J = 55 (B = 2,
+    axis-angle pose, joints_offset) and the FLAME head lbs at FLAME size (V = 5,023, J = 5, 400
+    shape + expression betas, B = 2).  The inputs (62 MB of posedirs) are regenerated from the seeds;
+    lbs_golden_full.npz keeps the reference's outputs and the inputs' SHA-256."""
+    cases = {}
+    rng = np.random.default_rng(41)
+    verts = _teeth_template()
+    m = avatar.lbs_model(verts, J=55, NB=0, seed=42, pose_scale=1e-3)
+    B, V = 2, verts.shape[0]
+    assert V == 10595
+    cases["smplx_full_wobeta"] = dict(
+        kind="lbs_wobeta", B=B, pose=rng.normal(0.0, 0.3, (B, 55, 3)).astype(np.float32),
+        v_shaped=(m["v_template"][None] + rng.normal(0.0, 0.005, (B, V, 3))).astype(np.float32),
+        posedirs=m["posedirs"], J_regressor=m["J_regressor"], parents=m["parents"],
+        lbs_weights=m["lbs_weights"], joints_offset=rng.normal(0.0, 0.01, (B, 55, 3)).astype(np.float32),
+        pose2rot=True)
+    rng = np.random.default_rng(43)
+    m = avatar.lbs_model(_subset(5023, 44), J=5, NB=400, parents=avatar.FLAME_PARENTS, seed=45,
+                         shape_scale=2e-4)
+    cases["flame_full_lbs"] = dict(kind="lbs", B=2, betas=rng.normal(0.0, 1.0, (2, 400)).astype(np.float32),
+                                   pose=rng.normal(0.0, 0.3, (2, 5 * 3)).astype(np.float32),
+                                   v_template=m["v_template"], shapedirs=m["shapedirs"],
+                                   posedirs=m["posedirs"], J_regressor=m["J_regressor"],
+                                   parents=m["parents"], lbs_weights=m["lbs_weights"],
+                                   joints_offset=None, pose2rot=True)
+    return cases
+
+
 def digest(case):
     h = hashlib.sha256()
     for k in sorted(case):

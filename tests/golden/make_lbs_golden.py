@@ -22,6 +22,7 @@ import lbs_cases  # noqa: E402
 
 REF = "/root/reference/models/modules/flame/lbs.py"
 OUT = os.path.join(HERE, "lbs_golden.npz")
+OUT_FULL = os.path.join(HERE, "lbs_golden_full.npz")  # SMPL-X / FLAME full-size cases
 
 
 def _ref_module():
@@ -31,11 +32,10 @@ def _ref_module():
     return m
 
 
-def main():
-    ref = _ref_module()
+def run_cases(ref, cases):
     t = lambda x: torch.from_numpy(np.ascontiguousarray(x))  # noqa: E731
     out = {}
-    for name, c in lbs_cases.all_cases().items():
+    for name, c in cases.items():
         out[f"{name}/sha"] = np.frombuffer(lbs_cases.digest(c).encode(), np.uint8)
         if c["kind"] == "rodrigues":
             out[f"{name}/rot"] = ref.batch_rodrigues(t(c["rot_vecs"])).numpy()
@@ -57,8 +57,15 @@ def main():
             out[f"{name}/J"] = J.numpy()
             out[f"{name}/T"] = T.numpy()
             out[f"{name}/A"] = A.numpy()
-    np.savez_compressed(OUT, **out)
-    print(OUT, {k: v.shape for k, v in out.items()})
+    return out
+
+
+def main():
+    ref = _ref_module()
+    for path, cases in ((OUT, lbs_cases.all_cases()), (OUT_FULL, lbs_cases.full_cases())):
+        out = run_cases(ref, cases)
+        np.savez_compressed(path, **out)
+        print(path, {k: v.shape for k, v in out.items()})
 
 
 if __name__ == "__main__":

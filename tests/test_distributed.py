@@ -6,6 +6,7 @@ tested is the sharding, ordering and the two consumer-side collectives bench.py 
 import os
 import socket
 
+import numpy as np
 import pytest
 import torch
 import torch.distributed as dist
@@ -71,6 +72,15 @@ def _worker(rank, world, port, n_frames, q):
                 got = f8.wait()
                 want = (_fake_render([step * n_frames + f for f in range(n_frames)])[:, :3] % 251).to(torch.uint8)
                 ok_stream = ok_stream and got.dtype == torch.uint8 and torch.equal(got, want)
+            # float32 frames into the uint8 exchange on the host: to8b (general_utils.py:316-317)
+            for step in range(2):
+                ids = [step * n_frames + f for f in frames]
+                fr = _fake_render(ids)[:, :5] / 700.0 - 0.2
+                f8.push(fr)
+                got = f8.wait()
+                full_fr = _fake_render([step * n_frames + f for f in range(n_frames)])[:, :3] / 700.0 - 0.2
+                want = torch.from_numpy((255 * np.clip(full_fr.numpy(), 0, 1)).astype(np.uint8))
+                ok_stream = ok_stream and torch.equal(got, want)
         q.put((rank, ok_gather, ok_reduce and ok_stream))
     finally:
         dist.destroy_process_group()
@@ -90,6 +100,25 @@ def test_gather_and_reduce_world2(n_frames):
         assert p.exitcode == 0
     assert sorted(r[0] for r in res) == [0, 1]
     assert all(r[1] and r[2] for r in res), res
+
+
+def test_stream_budget_leaves_a_queue_for_rccl(monkeypatch):
+    """At N > 1 the bench keeps at most GPU_MAX_HW_QUEUES - 1 compute streams (RCCL runs every
+    collective on ProcessGroupNCCL's internal stream, FrameGather adds none), so the exchange never
+    shares a hardware queue with a persistent render kernel; at N = 1 all queues compute."""
+    monkeypatch.setenv("GPU_MAX_HW_QUEUES", "4")
+    assert parallel.stream_budget(4, 1) == 4
+    assert parallel.stream_budget(4, 2) == 3
+    assert parallel.stream_budget(4, 8) == 3
+    assert parallel.stream_budget(2, 8) == 2
+    assert parallel.stream_budget(1, 8) == 1
+    assert parallel.stream_budget(4, 2, hw_queues=8) == 4
+    import inspect
+    src = inspect.getsource(parallel.FrameGather)
+    assert "torch.cuda.Stream(" not in src  # no side stream of its own
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    bench_src = open(os.path.join(root, "bench.py")).read()
+    assert "a.inflight = parallel.stream_budget(a.inflight, world)" in bench_src
 
 
 def test_bench_rank_launch_contract(monkeypatch):

@@ -61,6 +61,68 @@ def test_lbs_with_betas_golden_case():
     np.testing.assert_allclose(jt.cpu().numpy(), r_jt, atol=ATOL, rtol=0)
 
 
+@pytest.fixture(scope="module")
+def full_golden():
+    return np.load(os.path.join(HERE, "golden", "lbs_golden_full.npz")), lbs_cases.full_cases()
+
+
+@pytest.mark.parametrize("frames", [(0, 1), (1,)])
+def test_full_size_goldens_match_reference(full_golden, frames):
+    """The GPU LBS at SURVEY.md §8(c)'s sizes against the reference's own lbs.py outputs
+    (lbs_golden_full.npz): SMPL-X lbs_wobeta at V = 10,595, J = 55 and FLAME lbs at V = 5,023 with
+    400 betas; both frames as one batch, and frame 1 alone (B = 1: the single-frame blend kernel)."""
+    from guava_renderer_amd import deform
+    gold, cases = full_golden
+    sel = list(frames)
+    c = cases["smplx_full_wobeta"]
+    got = deform.lbs_wobeta(_t(c["pose"][sel]), _t(c["v_shaped"][sel]), _t(c["posedirs"]), _t(c["J_regressor"]),
+                            torch.from_numpy(c["parents"]), _t(c["lbs_weights"]),
+                            joints_offset=_t(c["joints_offset"][sel]), pose2rot=True)
+    for key, g in zip(("verts", "J_transformed", "J", "T", "A"), got):
+        np.testing.assert_allclose(g.cpu().numpy(), gold[f"smplx_full_wobeta/{key}"][sel], atol=ATOL, rtol=0,
+                                   err_msg=key)
+    c = cases["flame_full_lbs"]
+    verts, jt = deform.lbs(_t(c["betas"][sel]), _t(c["pose"][sel]), _t(c["v_template"]), _t(c["shapedirs"]),
+                           _t(c["posedirs"]), _t(c["J_regressor"]), torch.from_numpy(c["parents"]),
+                           _t(c["lbs_weights"]))
+    np.testing.assert_allclose(verts.cpu().numpy(), gold["flame_full_lbs/verts"][sel], atol=ATOL, rtol=0)
+    np.testing.assert_allclose(jt.cpu().numpy(), gold["flame_full_lbs/J_transformed"][sel], atol=ATOL, rtol=0)
+
+
+def test_single_frame_deform_matches_oracle():
+    """B = 1 everywhere (the per-frame drop-in path, main/test.py:70-76): lbs with betas and
+    posedirs at SMPL-X size, lbs_wobeta, and EHM.forward, each against the oracle -- the
+    single-frame blend kernel (k_lbs_blend<1,16>) and its scalar tail for NF % 4 != 0."""
+    from guava_renderer_amd import avatar, deform
+    m, g, faces, betas, pose = _full_avatar(B=1, P=20000)
+    verts, jt = deform.lbs(_t(betas), _t(pose), _t(m["v_template"]), _t(m["shapedirs"]), _t(m["posedirs"]),
+                           _t(m["J_regressor"]), torch.from_numpy(m["parents"]), _t(m["lbs_weights"]))
+    r_verts, r_jt, r_J, r_T, r_A, r_vs = lo.lbs(betas, pose, m["v_template"], m["shapedirs"], m["posedirs"],
+                                                m["J_regressor"], m["parents"], m["lbs_weights"])
+    np.testing.assert_allclose(verts.cpu().numpy(), r_verts, atol=ATOL, rtol=0)
+    np.testing.assert_allclose(jt.cpu().numpy(), r_jt, atol=ATOL, rtol=0)
+    _, _, _, T2, A2 = deform.lbs_wobeta(_t(pose), _t(r_vs.astype(np.float32)), _t(m["posedirs"]),
+                                        _t(m["J_regressor"]), torch.from_numpy(m["parents"]), _t(m["lbs_weights"]))
+    np.testing.assert_allclose(T2.cpu().numpy(), r_T, atol=ATOL, rtol=0)
+    np.testing.assert_allclose(A2.cpu().numpy(), r_A, atol=ATOL, rtol=0)
+    # a blend with a coefficient count that is not a multiple of 4 (the scalar tail): 350 - 3 betas
+    nb = 347
+    v3, _ = deform.lbs(_t(betas[:, :nb]), _t(pose), _t(m["v_template"]), _t(m["shapedirs"][..., :nb].copy()),
+                       _t(m["posedirs"]), _t(m["J_regressor"]), torch.from_numpy(m["parents"]),
+                       _t(m["lbs_weights"]))
+    r3, *_ = lo.lbs(betas[:, :nb], pose, m["v_template"], m["shapedirs"][..., :nb], m["posedirs"],
+                    m["J_regressor"], m["parents"], m["lbs_weights"])
+    np.testing.assert_allclose(v3.cpu().numpy(), r3, atol=ATOL, rtol=0)
+    body, flame, extra = avatar.ehm_assets(seed=0)
+    bp, fp = avatar.ehm_params(1, seed=4000)
+    ehm = deform.EHMDeformer(body, flame, extra["smplx2flame_ind"], extra["l_eyelid"], extra["r_eyelid"],
+                             device=DEV)
+    out = ehm({k: _t(v) for k, v in bp.items()}, {k: _t(v) for k, v in fp.items()})
+    ref = lo.ehm_forward(body, flame, extra, bp, fp)
+    for k in ("vertices", "joints", "joints_transform", "ver_transform_mat", "joint_transform_mat"):
+        np.testing.assert_allclose(out[k].cpu().numpy(), ref[k], atol=ATOL, rtol=0, err_msg=k)
+
+
 def _full_avatar(B=4, P=40000):
     from guava_renderer_amd import avatar
     verts, faces, tex = avatar.template_mesh()

@@ -91,8 +91,8 @@ def test_frames_to8b_matches_to8b():
 
 
 def _nccl_worker(port, q):
-    """World-1 RCCL group on the one GPU: FrameGather's device path (side stream, events, staging
-    buffers reused every other batch) on real renders, each gathered batch checked after the
+    """World-1 RCCL group on the one GPU: FrameGather's device path (async RCCL work on the PG's own
+    stream, staging buffers reused every other batch) on real renders, each gathered batch checked after the
     next batch was pushed (so the overlap is exercised)."""
     import torch.distributed as dist
     from guava_renderer_amd import parallel
@@ -110,7 +110,7 @@ def _nccl_worker(port, q):
             fg.push(_render(b)[:, :3])
             if prev is not None:  # the previous batch's buffer, read while this one is in flight
                 pb, pref = prev
-                torch.cuda.current_stream(dev).wait_stream(fg.stream)
+                fg.work[pb].wait()  # this stream after that batch's exchange
                 ok = ok and torch.equal(fg.bufs[pb][1], pref)
             prev = ((fg.k - 1) % len(fg.bufs), ref)
         last = fg.wait()

@@ -131,3 +131,28 @@ def test_deform_identity_pose_keeps_gaussians():
     np.testing.assert_allclose(np.minimum(np.abs(q - qv).max(-1), np.abs(q + qv).max(-1)), 0, atol=1e-12)
     centre = np.einsum("nk,bnkj->bnj", bary, verts[:, faces[bind]])
     np.testing.assert_allclose(out["xyz"][:, V:], centre, atol=1e-12)
+
+
+@pytest.fixture(scope="module")
+def full():
+    return np.load(os.path.join(HERE, "golden", "lbs_golden_full.npz")), lbs_cases.full_cases()
+
+
+def test_full_size_lbs_matches_reference(full):
+    """SURVEY.md §8(c) sizes: SMPL-X body lbs_wobeta at V = 10,595 (template + 120 teeth), J = 55, and
+    the FLAME head lbs at V = 5,023 with 400 betas -- the oracle against the reference's lbs.py."""
+    gold, cases = full
+    for name, c in cases.items():
+        assert bytes(gold[f"{name}/sha"]).decode() == lbs_cases.digest(c), \
+            f"{name}: input generator drifted; rerun tests/golden/make_lbs_golden.py"
+    c = cases["smplx_full_wobeta"]
+    assert c["v_shaped"].shape[1] == 10595 and c["J_regressor"].shape[0] == 55
+    out = lo.lbs_wobeta(c["pose"], c["v_shaped"], c["posedirs"], c["J_regressor"], c["parents"],
+                        c["lbs_weights"], c["joints_offset"], c["pose2rot"])
+    for key, got in zip(("verts", "J_transformed", "J", "T", "A"), out):
+        np.testing.assert_allclose(got, gold[f"smplx_full_wobeta/{key}"], atol=ATOL, rtol=0, err_msg=key)
+    c = cases["flame_full_lbs"]
+    verts, jt, *_ = lo.lbs(c["betas"], c["pose"], c["v_template"], c["shapedirs"], c["posedirs"],
+                           c["J_regressor"], c["parents"], c["lbs_weights"], c["joints_offset"])
+    np.testing.assert_allclose(verts, gold["flame_full_lbs/verts"], atol=ATOL, rtol=0)
+    np.testing.assert_allclose(jt, gold["flame_full_lbs/J_transformed"], atol=ATOL, rtol=0)
