@@ -331,14 +331,14 @@ def profile_read():
 
 
 COUNTERS = ("pairs_evaluated", "pairs_contributing", "strip_pairs_blended", "mfma_ksteps",
-            "gaussians_staged", "list_entries", "tiles_rendered", "dead_ksteps")
+            "gaussians_staged", "list_entries", "tiles_rendered", "dead_ksteps", "quad_survivors")
 
 
 def render_counters(fn, device="cuda"):
     """Run `fn()` (one or more forwards) with the instrumented render kernel and return the work
     counters of include/gsr.h:gsr_render_counters as a dict."""
     L = _lib.load()
-    buf = torch.zeros(8, dtype=torch.int64, device=device)
+    buf = torch.zeros(len(COUNTERS), dtype=torch.int64, device=device)
     L.gsr_render_counters(buf.data_ptr())
     try:
         fn()

@@ -262,24 +262,26 @@ __device__ __forceinline__ uint32_t queue_item(uint32_t q, uint32_t k, uint32_t 
     return e < nempty ? 4u * ne + e : 0xFFFFFFFFu;
 }
 
-// The same mapping with every strip split into two work items (half-strip render waves): 8 items
-// per non-empty tile, then the empty tiles.
-__device__ __forceinline__ uint32_t queue_item_half(uint32_t q, uint32_t k, uint32_t ne, uint32_t nempty,
-                                                    uint32_t map, const uint32_t* ctrl) {
+// The same mapping with every strip split into S work items (S = 2: half-strip render waves, 4: quad
+// waves): 4 S items per non-empty tile, then the empty tiles.
+template <uint32_t S>
+__device__ __forceinline__ uint32_t queue_item_n(uint32_t q, uint32_t k, uint32_t ne, uint32_t nempty,
+                                                 uint32_t map, const uint32_t* ctrl) {
+    constexpr uint32_t per = 4u * S;  // items per tile
     if (map == 0) {
         const uint32_t item = q + 8u * k;
-        return item < 8u * ne + nempty ? item : 0xFFFFFFFFu;
+        return item < per * ne + nempty ? item : 0xFFFFFFFFu;
     }
     if (map == 2) {
         const uint32_t nq = ctrl[kCtrlQStart + 8 + q];
-        if (k < 8u * nq) return 8u * (ctrl[kCtrlQStart + q] + (k >> 3)) + (k & 7u);
-        const uint32_t e = q + 8u * (k - 8u * nq);
-        return e < nempty ? 8u * ne + e : 0xFFFFFFFFu;
+        if (k < per * nq) return per * (ctrl[kCtrlQStart + q] + k / per) + k % per;
+        const uint32_t e = q + 8u * (k - per * nq);
+        return e < nempty ? per * ne + e : 0xFFFFFFFFu;
     }
     const uint32_t ntq = ne > q ? (ne - q + 7u) >> 3 : 0u;
-    if (k < 8u * ntq) return 8u * (q + 8u * (k >> 3)) + (k & 7u);
-    const uint32_t e = q + 8u * (k - 8u * ntq);
-    return e < nempty ? 8u * ne + e : 0xFFFFFFFFu;
+    if (k < per * ntq) return per * (q + 8u * (k / per)) + k % per;
+    const uint32_t e = q + 8u * (k - per * ntq);
+    return e < nempty ? per * ne + e : 0xFFFFFFFFu;
 }
 
 // ---- launchers (all asynchronous on `stream`) ----

@@ -61,6 +61,7 @@ typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef unsigned uint4x __attribute__((ext_vector_type(4)));
 typedef unsigned uint2x __attribute__((ext_vector_type(2)));
 typedef short shortx4 __attribute__((ext_vector_type(4)));
+typedef float floatx4 __attribute__((ext_vector_type(4)));
 
 // The blend step of forward.cu:349-381 split in two (both halves are branch-free):
 //  * alpha_of: the pixel-local alpha of one Gaussian, independent of the pixel's transmittance, with
@@ -133,15 +134,17 @@ __device__ __forceinline__ float4 rec_load(__amdgpu_buffer_rsrc_t rs, uint32_t o
 // channels [keep, keep + n_out) already hold the refiner head's 1x1 conv W.(C + T bg); they get the
 // bias and the leaky ReLU here and go to out_refine, channels [0, keep) to out_color, the rest
 // nowhere.  No extra registers: the blend loop is the same kernel.
+// skip: strip pixels (bit = pixel) whose outputs are NOT written here (the quad tail's live
+// pixels, written by quad_store later).
 template <bool EMPTY, bool REFINE>
 __device__ __forceinline__ void store_strip(const Dims& d, const ImageArena& im, const Outputs& o,
                                             const float* bg, int b, int sx0, int sy0, int lane,
                                             const floatx16& acc0, const floatx16& acc1, float T,
-                                            float invd, uint32_t last) {
+                                            float invd, uint32_t last, uint64_t skip = 0) {
     const int64_t HW = (int64_t)d.H * d.W;
     const int px = sx0 + lane % kStripW;
     const int py = sy0 + lane / kStripW;
-    if (px < d.W && py < d.H) {
+    if (px < d.W && py < d.H && !((skip >> lane) & 1u)) {
         const int64_t pix = b * HW + (int64_t)py * d.W + px;
         im.final_T[pix] = T;
         im.n_contrib[pix] = last;
@@ -163,8 +166,9 @@ __device__ __forceinline__ void store_strip(const Dims& d, const ImageArena& im,
     const int qy1 = qy0 + 32 / kStripW;  // the upper 32 pixels of the strip
     const int hi = lane >> 5;
     const int hoff = hi * 4 * (int)HW;  // channels +4 for the upper half-wave
-    const int v0 = (qx < d.W && qy0 < d.H) ? (hoff + qy0 * d.W + qx) * 4 : 0x7FFFFFF0;
-    const int v1 = (qx < d.W && qy1 < d.H) ? (hoff + qy1 * d.W + qx) * 4 : 0x7FFFFFF0;
+    const int v0 = (qx < d.W && qy0 < d.H && !((skip >> j) & 1u)) ? (hoff + qy0 * d.W + qx) * 4 : 0x7FFFFFF0;
+    const int v1 = (qx < d.W && qy1 < d.H && !((skip >> (j + 32)) & 1u)) ? (hoff + qy1 * d.W + qx) * 4
+                                                                          : 0x7FFFFFF0;
     __amdgpu_buffer_rsrc_t rr = rs;
     if (REFINE)
         rr = __builtin_amdgcn_make_buffer_rsrc(o.out_refine + (int64_t)b * o.n_out * HW, 0,
@@ -319,7 +323,7 @@ __device__ __forceinline__ void overflow_fill(const Dims& d, const Outputs& o) {
 // step s+1's alphas (the exp-heavy, transmittance-independent part) are computed and step s's
 // serial blend and MFMA accumulation run.
 template <bool EXACT, bool STATS, bool TL, bool REFINE, int ABL = 0, int SPLIT = 0, int NSLOT = 3,
-          bool HALF = false>
+          bool HALF = false, bool QUAD = false, bool QONLY = false>
 __device__ __forceinline__ void render_fwd_body(const Dims& d, const Inputs& in, const GeomArena& g,
                                                 const ImageArena& im, const BinArena& bn,
                                                 const Outputs& o) {
@@ -328,9 +332,12 @@ __device__ __forceinline__ void render_fwd_body(const Dims& d, const Inputs& in,
         return;
     }
     static_assert(!HALF || (!STATS && !TL && !REFINE && ABL == 0), "half-strip waves: production kernel only");
+    static_assert(!QUAD || (!HALF && !REFINE && SPLIT == 0 && NSLOT == 3), "quad tail: full-strip f32 kernel only");
+    static_assert(!QONLY || (QUAD && !STATS && !TL && ABL == 0), "quad-only waves: production kernel only");
     const uint32_t ne = g.ctrl[kCtrlNonEmpty];
     // HALF: every strip is two work items (one wave per 32-pixel half, the strip's rows 0-3 / 4-7)
-    const uint32_t nstrip = (HALF ? 2u : 1u) * (uint32_t)kStrips * ne;
+    // QONLY: every strip is four work items (one wave per 4x4 quad of the strip)
+    const uint32_t nstrip = (HALF ? 2u : QONLY ? 4u : 1u) * (uint32_t)kStrips * ne;
     const uint32_t nitems = nstrip + (uint32_t)(d.B * d.T) - ne;
     const int lane = threadIdx.x & 63;
     const int hi = lane >> 5;
@@ -344,8 +351,9 @@ __device__ __forceinline__ void render_fwd_body(const Dims& d, const Inputs& in,
             uint32_t k = 0;
             if (lane == 0) k = atomicAdd(&g.ctrl[kCtrlXcdQueue + kCtrlXcdStride * q], 1u);
             k = __builtin_amdgcn_readfirstlane(k);
-            item = HALF ? queue_item_half(q, k, ne, nitems - nstrip, in.xcd_map, g.ctrl)
-                        : queue_item(q, k, ne, nitems - nstrip, in.xcd_map, g.ctrl);
+            item = HALF    ? queue_item_n<2>(q, k, ne, nitems - nstrip, in.xcd_map, g.ctrl)
+                   : QONLY ? queue_item_n<4>(q, k, ne, nitems - nstrip, in.xcd_map, g.ctrl)
+                           : queue_item(q, k, ne, nitems - nstrip, in.xcd_map, g.ctrl);
             if (item != 0xFFFFFFFFu) break;
             q = (q + 1) & 7u;
             q_left--;
@@ -379,8 +387,9 @@ __device__ __forceinline__ void render_fwd_body(const Dims& d, const Inputs& in,
             continue;
         }
         const uint64_t t_start = TL ? __builtin_amdgcn_s_memrealtime() : 0;
-        const uint32_t code = im.strip_list[HALF ? item >> 1 : item];
+        const uint32_t code = im.strip_list[HALF ? item >> 1 : QONLY ? item >> 2 : item];
         const int half = HALF ? (int)(item & 1u) : 0;
+        const int quad = QONLY ? (int)(item & 3u) : 0;  // 4x4 quad of the strip (x = quad & 1, y = quad >> 1)
         const int tile_g = (int)(code >> 2);
         const int strip = (int)(code & 3u);
         const int b = tile_g / d.T;
@@ -398,7 +407,8 @@ __device__ __forceinline__ void render_fwd_body(const Dims& d, const Inputs& in,
         float T = 1.0f, invd = 0.f;
         uint32_t last = 0, stop = 0;
         const uint32_t smask_bit = 1u << (28 + strip);
-        if (!STATS && !TL && im.strip_cnt[(int64_t)tile_g * kStrips + strip] == 0u) {
+        const bool strip_empty = im.strip_cnt[(int64_t)tile_g * kStrips + strip] == 0u;
+        if (!QONLY && !STATS && !TL && strip_empty) {
             // no list entry reaches the strip (k_strip_count): nothing is taken anywhere in it, so
             // its outputs are the background, T = 1, n_contrib = 0, inverse depth 0 -- the values
             // the list walk would give -- without walking the tile's list
@@ -410,7 +420,8 @@ __device__ __forceinline__ void render_fwd_body(const Dims& d, const Inputs& in,
             continue;
         }
         const uint2 range = im.ranges[tile_g];
-        const int n = (int)(range.y - range.x);
+        // (QONLY: a strip no entry reaches walks an empty list -- the quad epilogue stores the background)
+        const int n = (QONLY && strip_empty) ? 0 : (int)(range.y - range.x);
         const uint32_t* __restrict__ plist = bn.point_list + range.x;
         // render records through a buffer resource: the byte offset of a (wave-uniform) record is
         // one SGPR, no 64-bit address arithmetic per survivor
@@ -437,7 +448,7 @@ __device__ __forceinline__ void render_fwd_body(const Dims& d, const Inputs& in,
         uint4x sa_ = {0u, 0u, 0u, 0u}, sb0_ = {0u, 0u, 0u, 0u}, sb1_ = {0u, 0u, 0u, 0u};  // SPLIT operands, k 4..7 stay 0
 #pragma unroll
         for (int r = 0; r < 16; r++) { acc0[r] = 0.f; acc1[r] = 0.f; }
-        uint64_t n_surv = 0, n_steps = 0, n_contrib_pairs = 0, n_staged = 0, n_dead = 0;
+        uint64_t n_surv = 0, n_steps = 0, n_contrib_pairs = 0, n_staged = 0, n_dead = 0, n_qsurv = 0;
 
         // Survivor stream: wave-uniform state walking the list 64 entries at a time; the next
         // chunk's entries (index | strip mask << 28) are always in flight.
@@ -641,7 +652,9 @@ __device__ __forceinline__ void render_fwd_body(const Dims& d, const Inputs& in,
         GSR_SLOT(C)
         // An invalid slot takes nothing (alpha 0, feature 0); the loop leaves only at its head and
         // its foot, which keeps the MFMA accumulators in one register chain.
-        if constexpr (NSLOT == 3) {
+        bool to_quad = false;
+        if constexpr (QONLY) {
+        } else if constexpr (NSLOT == 3) {
             GSR_FETCH(A)
             GSR_FETCH(B)
             GSR_FETCH(C)
@@ -653,7 +666,20 @@ __device__ __forceinline__ void render_fwd_body(const Dims& d, const Inputs& in,
                 GSR_FETCH(B)
                 GSR_STEP(A, C)
                 GSR_FETCH(C)
-                if (!__any(!done)) break;  // every pixel of the strip finished
+                if constexpr (QUAD) {
+                    // at most 16 pixels still blending: the rest of the list runs in the quad tail
+                    const uint64_t live_ = __ballot(!done);
+                    if (live_ == 0ull) break;  // every pixel of the strip finished
+                    if (__builtin_popcountll(live_) <= 16) { to_quad = true; break; }
+                } else {
+                    if (!__any(!done)) break;  // every pixel of the strip finished
+                }
+            }
+            if (QUAD && to_quad) {
+                // drain the pipeline in strip layout: slot A's alphas are computed, B and C fetched
+                GSR_STEP(B, A)
+                GSR_STEP(C, B)
+                GSR_TAKE(C)
             }
         } else {
             // latency mode (single-frame launches, where one wave's strip sets the kernel time): five
@@ -680,6 +706,193 @@ __device__ __forceinline__ void render_fwd_body(const Dims& d, const Inputs& in,
                 if (!__any(!done)) break;
             }
         }
+        // ---- quad tail ----
+        // The strip's <= 16 still-blending pixels, compacted into 16 slots; each step takes the next
+        // FOUR survivors, lane = slot + 16 q computing Gaussian q's alpha at its slot's pixel (one
+        // alpha per lane instead of two alphas per lane for 64 mostly finished pixels).  Every lane
+        // of a slot runs the slot's serial blend over the four alphas (broadcast by one permlane16
+        // and two permlane32 swaps) in list order, and keeps its own Gaussian's weight as the
+        // K = 4 operand of two v_mfma_f32_16x16x4_f32 (channels 0-15, 16-31): an exact k-ordered fma
+        // chain continuing each pixel's colour chain, so the image is bit-identical to the strip
+        // layout's (and the oracle's).  The strip's finished pixels are stored first; the slots' state
+        // (T, inverse depth, last contributor, colour accumulators) moves over by ds_bpermute.
+        uint64_t quad_live = 0;  // strip pixels handed to the quad tail (stored by it)
+        uint64_t ev_quad = 0;    // STATS: the quad slots' pairs visited
+        if (QUAD && (QONLY || to_quad)) {
+            const int j = lane & 15, q = lane >> 4;
+            int nlive, p;
+            bool slot_ok;
+            float Ts, invds;
+            uint32_t lasts, stops;
+            floatx4 qa0, qa1;
+            if constexpr (QONLY) {
+                // a fresh 4x4 quad: slot j = quad pixel (j % 4, j / 4)
+                p = (4 * (quad >> 1) + (j >> 2)) * kStripW + 4 * (quad & 1) + (j & 3);
+                slot_ok = sx0 + p % kStripW < d.W && sy0 + p / kStripW < d.H;
+                nlive = 16;
+                Ts = 1.0f; invds = 0.f; lasts = 0u; stops = 0u;
+#pragma unroll
+                for (int r = 0; r < 4; r++) { qa0[r] = 0.f; qa1[r] = 0.f; }
+            } else {
+            quad_live = __ballot(!done);
+            nlive = __builtin_popcountll(quad_live);
+            // the strip's finished pixels: final now
+            store_strip<false, false>(d, im, o, in.bg + in.s_bg * b, b, sx0, sy0, lane, acc0, acc1, T, invd, last,
+                                      quad_live);
+            // slot j <- the j-th live pixel (in lane order), through the wave's LDS words
+            const uint32_t my_slot = __builtin_amdgcn_mbcnt_hi((uint32_t)(quad_live >> 32),
+                                                               __builtin_amdgcn_mbcnt_lo((uint32_t)quad_live, 0u));
+            if ((quad_live >> lane) & 1u) rec_lds[my_slot] = (unsigned)lane;
+            __builtin_amdgcn_wave_barrier();
+            slot_ok = j < nlive;
+            p = slot_ok ? (int)rec_lds[j] : 0;
+            __builtin_amdgcn_wave_barrier();
+            // the slot's pixel state (duplicated over the four lane groups)
+            Ts = __shfl(T, p);
+            invds = __shfl(invd, p);
+            lasts = (uint32_t)__shfl((int)last, p);
+            stops = STATS ? (uint32_t)__shfl((int)stop, p) : 0u;
+            // colour accumulators into the 16x16x4 layout: qa0[r] = channel 4q + r, qa1[r] = 16 + 4q + r
+            // of slot j; in the strip layout channel c of pixel p sits in acc_{p >= 32}[(c & 3) + 4 (c >> 3)]
+            // at lane (p & 31) + 32 ((c >> 2) & 1)
+            {
+                const int src = (p & 31) + 32 * (q & 1);
+                const bool up = p >= 32, h2 = (q >> 1) != 0;
+#pragma unroll
+                for (int r = 0; r < 4; r++) {
+                    const float a0l = __shfl(acc0[r], src), a0h = __shfl(acc0[r + 4], src);
+                    const float a1l = __shfl(acc1[r], src), a1h = __shfl(acc1[r + 4], src);
+                    qa0[r] = up ? (h2 ? a1h : a1l) : (h2 ? a0h : a0l);
+                    const float b0l = __shfl(acc0[r + 8], src), b0h = __shfl(acc0[r + 12], src);
+                    const float b1l = __shfl(acc1[r + 8], src), b1h = __shfl(acc1[r + 12], src);
+                    qa1[r] = up ? (h2 ? b1h : b1l) : (h2 ? b0h : b0l);
+                }
+            }
+            }
+            bool dones = !slot_ok;
+            const float qfx = (float)(sx0 + p % kStripW), qfy = (float)(sy0 + p / kStripW);
+            // f32 features (the quad tail runs in the exact mode only)
+            const __amdgpu_buffer_rsrc_t qfs = __builtin_amdgcn_make_buffer_rsrc(
+                (void*)(in.colors + in.s_colors * b), 0, (int)min((int64_t)d.P * GSR_C * 4, (int64_t)0x7FFFFFFF),
+                0x00020000);
+            const int qrec_w = lane < 32 ? lane : 24 + lane;  // LDS word of this lane's record dword
+            const int rq = (lane >> 3) & 3;                   // record loads: lanes 8 rq .. 8 rq + 7
+            // next four survivors of the strip (index P past the list's end: zero record, zero feature)
+#define GSR_QFETCH(S)                                                                               \
+            {                                                                                       \
+                uint32_t g0_ = (uint32_t)d.P, g1_ = (uint32_t)d.P, g2_ = (uint32_t)d.P, g3_ = (uint32_t)d.P; \
+                int p0_ = 0, p1_ = 0, p2_ = 0, p3_ = 0;                                             \
+                if (__builtin_expect(__builtin_popcountll(mask) >= 4, 1)) {                         \
+                    /* common case: four survivors of the chunk in hand */                          \
+                    const int i0_ = (int)__builtin_ctzll(mask); mask &= mask - 1;                   \
+                    const int i1_ = (int)__builtin_ctzll(mask); mask &= mask - 1;                   \
+                    const int i2_ = (int)__builtin_ctzll(mask); mask &= mask - 1;                   \
+                    const int i3_ = (int)__builtin_ctzll(mask); mask &= mask - 1;                   \
+                    g0_ = __builtin_amdgcn_readlane(cidx, i0_) & kIndexMask; p0_ = base + i0_ + 1;  \
+                    g1_ = __builtin_amdgcn_readlane(cidx, i1_) & kIndexMask; p1_ = base + i1_ + 1;  \
+                    g2_ = __builtin_amdgcn_readlane(cidx, i2_) & kIndexMask; p2_ = base + i2_ + 1;  \
+                    g3_ = __builtin_amdgcn_readlane(cidx, i3_) & kIndexMask; p3_ = base + i3_ + 1;  \
+                    S##v = true;                                                                    \
+                } else {                                                                            \
+                    S##v = GSR_NEXT(g0_, p0_);                                                      \
+                    if (S##v && !GSR_NEXT(g1_, p1_)) g1_ = (uint32_t)d.P;                           \
+                    if (S##v && g1_ != (uint32_t)d.P && !GSR_NEXT(g2_, p2_)) g2_ = (uint32_t)d.P;   \
+                    if (S##v && g2_ != (uint32_t)d.P && !GSR_NEXT(g3_, p3_)) g3_ = (uint32_t)d.P;   \
+                    if (!S##v) g0_ = (uint32_t)d.P;                                                 \
+                }                                                                                   \
+                S##p0 = p0_; S##p1 = p1_; S##p2 = p2_; S##p3 = p3_;                                 \
+                const uint32_t gr_ = rq == 0 ? g0_ : rq == 1 ? g1_ : rq == 2 ? g2_ : g3_;           \
+                S##r = __builtin_amdgcn_raw_buffer_load_b32(                                        \
+                    rrs, lane < 32 ? (int)(gr_ * 32u + (uint32_t)(lane & 7) * 4u) : (int)kOOB, 0, 0); \
+                const uint32_t gf_ = q == 0 ? g0_ : q == 1 ? g1_ : q == 2 ? g2_ : g3_;              \
+                const int fo_ = (int)(gf_ * (uint32_t)(GSR_C * 4) + (uint32_t)j * 4u);              \
+                S##f0 = __builtin_amdgcn_raw_buffer_load_b32(qfs, fo_, 0, 0);                       \
+                S##f1 = __builtin_amdgcn_raw_buffer_load_b32(qfs, fo_ + 64, 0, 0);                  \
+            }
+#define GSR_QSTEP(S)                                                                                \
+            {                                                                                       \
+                rec_lds[qrec_w] = S##r;                                                             \
+                __builtin_amdgcn_wave_barrier();                                                    \
+                const float4 ra_ = __builtin_bit_cast(float4, *(const uint4x*)&rec_lds[8 * q]);     \
+                const float4 rc_ = __builtin_bit_cast(float4, *(const uint4x*)&rec_lds[8 * q + 4]); \
+                __builtin_amdgcn_wave_barrier();                                                    \
+                const float al_ = alpha_of<EXACT>(ra_, rc_, qfx, qfy);                              \
+                /* the four Gaussians' alphas and inverse depths at this slot, to every lane */     \
+                const auto a16_ = __builtin_amdgcn_permlane16_swap(__float_as_uint(al_), __float_as_uint(al_), \
+                                                                    false, false);                  \
+                const auto a02_ = __builtin_amdgcn_permlane32_swap(a16_[0], a16_[0], false, false); \
+                const auto a13_ = __builtin_amdgcn_permlane32_swap(a16_[1], a16_[1], false, false); \
+                const auto i16_ = __builtin_amdgcn_permlane16_swap(__float_as_uint(ra_.w),          \
+                                                                    __float_as_uint(ra_.w), false, false); \
+                const auto i02_ = __builtin_amdgcn_permlane32_swap(i16_[0], i16_[0], false, false); \
+                const auto i13_ = __builtin_amdgcn_permlane32_swap(i16_[1], i16_[1], false, false); \
+                const bool was_ = dones;                                                            \
+                const float w0_ = take_step(__uint_as_float(a02_[0]), __uint_as_float(i02_[0]),     \
+                                            (uint32_t)S##p0, Ts, invds, lasts, dones);              \
+                if (STATS && !was_ && dones) stops = (uint32_t)S##p0;                               \
+                const bool was1_ = dones;                                                           \
+                const float w1_ = take_step(__uint_as_float(a13_[0]), __uint_as_float(i13_[0]),     \
+                                            (uint32_t)S##p1, Ts, invds, lasts, dones);              \
+                if (STATS && !was1_ && dones) stops = (uint32_t)S##p1;                              \
+                const bool was2_ = dones;                                                           \
+                const float w2_ = take_step(__uint_as_float(a02_[1]), __uint_as_float(i02_[1]),     \
+                                            (uint32_t)S##p2, Ts, invds, lasts, dones);              \
+                if (STATS && !was2_ && dones) stops = (uint32_t)S##p2;                              \
+                const bool was3_ = dones;                                                           \
+                const float w3_ = take_step(__uint_as_float(a13_[1]), __uint_as_float(i13_[1]),     \
+                                            (uint32_t)S##p3, Ts, invds, lasts, dones);              \
+                if (STATS && !was3_ && dones) stops = (uint32_t)S##p3;                              \
+                const float wq_ = q == 0 ? w0_ : q == 1 ? w1_ : q == 2 ? w2_ : w3_;                 \
+                qa0 = __builtin_amdgcn_mfma_f32_16x16x4f32(__uint_as_float(S##f0), wq_, qa0, 0, 0, 0); \
+                qa1 = __builtin_amdgcn_mfma_f32_16x16x4f32(__uint_as_float(S##f1), wq_, qa1, 0, 0, 0); \
+                if (STATS) {                                                                        \
+                    n_contrib_pairs += __popcll(__ballot(wq_ > 0.f));                               \
+                    n_qsurv += 1 + (S##p1 > 0) + (S##p2 > 0) + (S##p3 > 0);                         \
+                }                                                                                   \
+                if (TL) n_steps += 1;  /* (STATS: quad steps in cn[8] as survivors, not k-steps) */ \
+            }
+            bool Xv = false, Yv = false;
+            int Xp0, Xp1, Xp2, Xp3, Yp0, Yp1, Yp2, Yp3;
+            unsigned Xr, Xf0, Xf1, Yr, Yf0, Yf1;
+            if (nlive > 0) {
+                GSR_QFETCH(X)
+                while (Xv) {
+                    GSR_QFETCH(Y)
+                    GSR_QSTEP(X)
+                    if (!Yv || !__any(!dones)) break;
+                    GSR_QFETCH(X)
+                    GSR_QSTEP(Y)
+                    if (!__any(!dones)) break;
+                }
+            }
+#undef GSR_QFETCH
+#undef GSR_QSTEP
+            // the slots' outputs: group 0 stores final_T / n_contrib / inverse depth, every lane its
+            // four channels of each half (pixels in the image by construction: they were live)
+            {
+                const int64_t HW = (int64_t)d.H * d.W;
+                const int64_t pix = b * HW + (int64_t)(sy0 + p / kStripW) * d.W + (sx0 + p % kStripW);
+                if (slot_ok && q == 0) {
+                    im.final_T[pix] = Ts;
+                    im.n_contrib[pix] = lasts;
+                    if (o.out_invdepth) o.out_invdepth[pix] = invds;
+                }
+                const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+                    o.out_color + (int64_t)b * GSR_C * HW, 0, (int)((int64_t)GSR_C * HW * 4), 0x00020000);
+                const float* bgp = in.bg + in.s_bg * b;
+                const int vo = slot_ok ? (int)((pix - b * HW) * 4) : 0x7FFFFFF0;
+#pragma unroll
+                for (int r = 0; r < 4; r++) {
+                    const int c0 = 4 * q + r, c1 = 16 + 4 * q + r;
+                    __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(fmaf(Ts, bgp[c0], qa0[r])), rs, vo,
+                                                          c0 * (int)HW * 4, 0);
+                    __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(fmaf(Ts, bgp[c1], qa1[r])), rs, vo,
+                                                          c1 * (int)HW * 4, 0);
+                }
+                if (STATS && slot_ok && q == 0) ev_quad = dones ? stops : (uint32_t)n;
+            }
+        }
+
 #undef GSR_NEXT
 #undef GSR_FETCH
 #undef GSR_ALPHA
@@ -692,7 +905,9 @@ __device__ __forceinline__ void render_fwd_body(const Dims& d, const Inputs& in,
         // ---- epilogue ----
         if (STATS) {
             unsigned long long* cn = (unsigned long long*)o.stats;
-            uint64_t ev = (px < d.W && py < d.H) ? (done ? stop : (uint32_t)n) : 0;
+            // pixels handed to the quad tail count there (ev_quad, one lane per slot)
+            uint64_t ev = (px < d.W && py < d.H && !((quad_live >> lane) & 1u)) ? (done ? stop : (uint32_t)n) : 0;
+            ev += ev_quad;
             for (int off = 32; off > 0; off >>= 1) ev += __shfl_xor(ev, off);
             if (lane == 0) {
                 atomicAdd(&cn[0], (unsigned long long)ev);
@@ -701,6 +916,7 @@ __device__ __forceinline__ void render_fwd_body(const Dims& d, const Inputs& in,
                 atomicAdd(&cn[3], (unsigned long long)n_steps);
                 atomicAdd(&cn[4], (unsigned long long)n_staged);
                 atomicAdd(&cn[7], (unsigned long long)n_dead);
+                atomicAdd(&cn[8], (unsigned long long)n_qsurv);
                 if (strip == 0) {
                     atomicAdd(&cn[5], (unsigned long long)n);
                     atomicAdd(&cn[6], 1ull);
@@ -717,7 +933,8 @@ __device__ __forceinline__ void render_fwd_body(const Dims& d, const Inputs& in,
         }
         if constexpr (HALF) store_half(d, im, o, in.bg + in.s_bg * b, b, sx0, sy0 + half * (32 / kStripW), lane,
                                        acc0, T, invd, last);
-        else if (ABL == 9) {  /* timing ablation: only final_T of the strip is stored */
+        else if (QUAD && (QONLY || to_quad)) {  /* stored by the quad tail */
+        } else if (ABL == 9) {  /* timing ablation: only final_T of the strip is stored */
             if (px < d.W && py < d.H) im.final_T[b * (int64_t)d.H * d.W + (int64_t)py * d.W + px] = T + acc0[0] + acc1[0];
         }
         else store_strip<false, REFINE>(d, im, o, in.bg + in.s_bg * b, b, sx0, sy0, lane, acc0, acc1, T,
@@ -732,11 +949,15 @@ __device__ __forceinline__ void render_fwd_body(const Dims& d, const Inputs& in,
 #ifndef GSR_RENDER_WPE
 #define GSR_RENDER_WPE 5
 #endif
-template <bool EXACT, bool STATS, bool TL, int SPLIT = 0, int NSLOT = GSR_BATCH_NSLOT, bool HALF = false>
+#ifndef GSR_QONLY_WPE
+#define GSR_QONLY_WPE 6  // quad-only waves (one frame): no 32-register strip accumulators
+#endif
+template <bool EXACT, bool STATS, bool TL, int SPLIT = 0, int NSLOT = GSR_BATCH_NSLOT, bool HALF = false,
+          bool QUAD = false, bool QONLY = false>
 __global__ __launch_bounds__(GSR_TILE_PIX)
-__attribute__((amdgpu_waves_per_eu((NSLOT == 5 && !HALF) ? 3 : GSR_RENDER_WPE))) void k_render_fwd(Dims d, Inputs in, GeomArena g,
-                                                             ImageArena im, BinArena bn, Outputs o) {
-    render_fwd_body<EXACT, STATS, TL, false, 0, SPLIT, NSLOT, HALF>(d, in, g, im, bn, o);
+__attribute__((amdgpu_waves_per_eu(QONLY ? GSR_QONLY_WPE : (NSLOT == 5 && !HALF) ? 3 : GSR_RENDER_WPE))) void k_render_fwd(
+    Dims d, Inputs in, GeomArena g, ImageArena im, BinArena bn, Outputs o) {
+    render_fwd_body<EXACT, STATS, TL, false, 0, SPLIT, NSLOT, HALF, QUAD, QONLY>(d, in, g, im, bn, o);
 }
 
 // Timing ablations of the production kernel (GSR_RENDER_ABLATE=1: VALU stand-in for the MFMAs,
@@ -775,11 +996,24 @@ void launch_render_fwd(const Dims& d, const Inputs& in_, const GeomArena& g, con
     // GSR_RENDER_HALF=0: single-frame launches use full-strip waves (A/B); GSR_RENDER_HALF_WG: WGs per CU
     static const bool half_mode = [] { const char* e = getenv("GSR_RENDER_HALF"); return !(e && e[0] == '0'); }();
     static const int half_wg = [] { const char* e = getenv("GSR_RENDER_HALF_WG"); return e ? atoi(e) : 3; }();
+    // GSR_RENDER_QONLY=0: single-frame launches use the half-strip waves (A/B); GSR_RENDER_QONLY_WG: WGs per CU
+    static const bool qonly_mode = [] { const char* e = getenv("GSR_RENDER_QONLY"); return !(e && e[0] == '0'); }();
+    static const int qonly_wg = [] { const char* e = getenv("GSR_RENDER_QONLY_WG"); return e ? atoi(e) : GSR_QONLY_WPE; }();
+    // GSR_QUAD_TAIL=0: no quad tail (A/B); the f32 (non-split) throughput kernel and its instrumented
+    // variants take it by default
+    static const bool quad = [] { const char* e = getenv("GSR_QUAD_TAIL"); return !(e && e[0] == '0'); }();
+    const bool qt = quad && !split;
     const int grid = min((nwaves + 3) / 4, persistent_grid(wg_per_cu));
     const dim3 gr(grid), bl(GSR_TILE_PIX);
-#define GSR_LAUNCH(E, S, L) hipLaunchKernelGGL((k_render_fwd<E, S, L>), gr, bl, 0, s, d, in, g, im, b, o)
-    if (o.stats) { if (exact) GSR_LAUNCH(true, true, false); else GSR_LAUNCH(false, true, false); }
-    else if (o.timeline) { if (exact) GSR_LAUNCH(true, false, true); else GSR_LAUNCH(false, false, true); }
+#define GSR_LAUNCH(E, S, L)                                                                                   \
+    {                                                                                                         \
+        if (qt) hipLaunchKernelGGL((k_render_fwd<E, S, L, 0, GSR_BATCH_NSLOT, false, true>), gr, bl, 0, s, d, in, g, im, b, o); \
+        else hipLaunchKernelGGL((k_render_fwd<E, S, L>), gr, bl, 0, s, d, in, g, im, b, o);                  \
+    }
+    if (o.stats) {
+        if (exact) GSR_LAUNCH(true, true, false) else GSR_LAUNCH(false, true, false)
+    }
+    else if (o.timeline) { if (exact) GSR_LAUNCH(true, false, true) else GSR_LAUNCH(false, false, true) }
     else if (o.out_refine) {  // (4-wave register budget: 4 workgroups per CU)
         const dim3 grf(min((nwaves + 3) / 4, persistent_grid(4)));
         if (exact) hipLaunchKernelGGL((k_render_fwd_refine<true>), grf, bl, 0, s, d, in, g, im, b, o);
@@ -790,6 +1024,14 @@ void launch_render_fwd(const Dims& d, const Inputs& in_, const GeomArena& g, con
     else if (ablate == 4) hipLaunchKernelGGL((k_render_fwd_ablate<4>), gr, bl, 0, s, d, in, g, im, b, o);
     else if (ablate == 8) hipLaunchKernelGGL((k_render_fwd_ablate<8>), gr, bl, 0, s, d, in, g, im, b, o);
     else if (ablate == 9) hipLaunchKernelGGL((k_render_fwd_ablate<9>), gr, bl, 0, s, d, in, g, im, b, o);
+    else if (d.B == 1 && latency_mode && qonly_mode && !split) {
+        // one frame, quad waves: every strip is four 4x4-pixel work items, each wave taking four
+        // survivors per step (lane = pixel + 16 Gaussian) -- a quarter of the longest strip's serial
+        // chain per work item
+        const dim3 gq(min((4 * nwaves + 3) / 4, persistent_grid(qonly_wg)));
+        if (exact) hipLaunchKernelGGL((k_render_fwd<true, false, false, 0, 3, false, true, true>), gq, bl, 0, s, d, in, g, im, b, o);
+        else hipLaunchKernelGGL((k_render_fwd<false, false, false, 0, 3, false, true, true>), gq, bl, 0, s, d, in, g, im, b, o);
+    }
     else if (d.B == 1 && latency_mode && half_mode) {
         // one frame, half-strip waves: a strip's two halves run in parallel, each lane one
         // (pixel, Gaussian) alpha per k-step -- the longest strip's time is what counts here
@@ -823,7 +1065,7 @@ void launch_render_fwd(const Dims& d, const Inputs& in_, const GeomArena& g, con
         if (exact) hipLaunchKernelGGL((k_render_fwd<true, false, false, 1>), gr, bl, 0, s, d, in, g, im, b, o);
         else hipLaunchKernelGGL((k_render_fwd<false, false, false, 1>), gr, bl, 0, s, d, in, g, im, b, o);
     }
-    else { if (exact) GSR_LAUNCH(true, false, false); else GSR_LAUNCH(false, false, false); }
+    else { if (exact) GSR_LAUNCH(true, false, false) else GSR_LAUNCH(false, false, false) }
 #undef GSR_LAUNCH
 }
 
