@@ -331,7 +331,8 @@ def profile_read():
 
 
 COUNTERS = ("pairs_evaluated", "pairs_contributing", "strip_pairs_blended", "mfma_ksteps",
-            "gaussians_staged", "list_entries", "tiles_rendered", "dead_ksteps", "quad_survivors")
+            "gaussians_staged", "list_entries", "tiles_rendered", "dead_ksteps", "quad_survivors",
+            "half_survivors")
 
 
 def render_counters(fn, device="cuda"):

@@ -323,7 +323,7 @@ __device__ __forceinline__ void overflow_fill(const Dims& d, const Outputs& o) {
 // step s+1's alphas (the exp-heavy, transmittance-independent part) are computed and step s's
 // serial blend and MFMA accumulation run.
 template <bool EXACT, bool STATS, bool TL, bool REFINE, int ABL = 0, int SPLIT = 0, int NSLOT = 3,
-          bool HALF = false, bool QUAD = false, bool QONLY = false>
+          bool HALF = false, bool QUAD = false, bool QONLY = false, bool HTAIL = false>
 __device__ __forceinline__ void render_fwd_body(const Dims& d, const Inputs& in, const GeomArena& g,
                                                 const ImageArena& im, const BinArena& bn,
                                                 const Outputs& o) {
@@ -334,6 +334,7 @@ __device__ __forceinline__ void render_fwd_body(const Dims& d, const Inputs& in,
     static_assert(!HALF || (!STATS && !TL && !REFINE && ABL == 0), "half-strip waves: production kernel only");
     static_assert(!QUAD || (!HALF && !REFINE && SPLIT == 0 && NSLOT == 3), "quad tail: full-strip f32 kernel only");
     static_assert(!QONLY || (QUAD && !STATS && !TL && ABL == 0), "quad-only waves: production kernel only");
+    static_assert(!HTAIL || (QUAD && !QONLY), "half tail: before the quad tail of the strip kernel");
     const uint32_t ne = g.ctrl[kCtrlNonEmpty];
     // HALF: every strip is two work items (one wave per 32-pixel half, the strip's rows 0-3 / 4-7)
     // QONLY: every strip is four work items (one wave per 4x4 quad of the strip)
@@ -448,7 +449,7 @@ __device__ __forceinline__ void render_fwd_body(const Dims& d, const Inputs& in,
         uint4x sa_ = {0u, 0u, 0u, 0u}, sb0_ = {0u, 0u, 0u, 0u}, sb1_ = {0u, 0u, 0u, 0u};  // SPLIT operands, k 4..7 stay 0
 #pragma unroll
         for (int r = 0; r < 16; r++) { acc0[r] = 0.f; acc1[r] = 0.f; }
-        uint64_t n_surv = 0, n_steps = 0, n_contrib_pairs = 0, n_staged = 0, n_dead = 0, n_qsurv = 0;
+        uint64_t n_surv = 0, n_steps = 0, n_contrib_pairs = 0, n_staged = 0, n_dead = 0, n_qsurv = 0, n_hsurv = 0;
 
         // Survivor stream: wave-uniform state walking the list 64 entries at a time; the next
         // chunk's entries (index | strip mask << 28) are always in flight.
@@ -652,7 +653,7 @@ __device__ __forceinline__ void render_fwd_body(const Dims& d, const Inputs& in,
         GSR_SLOT(C)
         // An invalid slot takes nothing (alpha 0, feature 0); the loop leaves only at its head and
         // its foot, which keeps the MFMA accumulators in one register chain.
-        bool to_quad = false;
+        bool to_quad = false, to_half = false;
         if constexpr (QONLY) {
         } else if constexpr (NSLOT == 3) {
             GSR_FETCH(A)
@@ -670,12 +671,14 @@ __device__ __forceinline__ void render_fwd_body(const Dims& d, const Inputs& in,
                     // at most 16 pixels still blending: the rest of the list runs in the quad tail
                     const uint64_t live_ = __ballot(!done);
                     if (live_ == 0ull) break;  // every pixel of the strip finished
-                    if (__builtin_popcountll(live_) <= 16) { to_quad = true; break; }
+                    const int nl_ = __builtin_popcountll(live_);
+                    if (nl_ <= 16) { to_quad = true; break; }
+                    if (HTAIL && nl_ <= 32) { to_half = true; break; }
                 } else {
                     if (!__any(!done)) break;  // every pixel of the strip finished
                 }
             }
-            if (QUAD && to_quad) {
+            if (QUAD && (to_quad || to_half)) {
                 // drain the pipeline in strip layout: slot A's alphas are computed, B and C fetched
                 GSR_STEP(B, A)
                 GSR_STEP(C, B)
@@ -706,6 +709,171 @@ __device__ __forceinline__ void render_fwd_body(const Dims& d, const Inputs& in,
                 if (!__any(!done)) break;
             }
         }
+        // ---- half tail ----
+        // 17..32 pixels still blending: compacted into 32 slots, two survivors per step with ONE
+        // alpha per lane (lane = slot + 32 q, Gaussian q), the pair's blend run in both lane halves
+        // (one permlane32 swap per value), one v_mfma_f32_32x32x2_f32 per step on the slots' 32x32
+        // colour tile (the strip layout's acc0 with slots for pixels) -- half the matrix work and 60%
+        // of the vector work of a strip k-step for the same two survivors.  Reaching <= 16 live slots
+        // it hands over to the quad tail.  Bit-exact as the quad tail (each pixel's fma chain goes on).
+        uint64_t half_live = 0;     // strip pixels handed to the half tail
+        uint64_t half_quad = 0;     // half slots handed on to the quad tail (bit = slot)
+        uint64_t ev_half = 0;       // STATS: pairs visited of the half slots stored by it
+        const int hj = lane & 31, hq = lane >> 5;
+        int hp = 0;                 // the half slot's strip pixel
+        bool hslot_ok = false;
+        float Th = 1.0f, invdh = 0.f;
+        uint32_t lasth = 0, stoph = 0;
+        bool doneh = true;
+        floatx16 ha;
+        const __amdgpu_buffer_rsrc_t qfs = __builtin_amdgcn_make_buffer_rsrc(
+            (void*)(in.colors + in.s_colors * b), 0, (int)min((int64_t)d.P * GSR_C * 4, (int64_t)0x7FFFFFFF),
+            0x00020000);  // f32 features of the half / quad tails (exact mode only)
+        if constexpr (HTAIL) if (to_half) {
+            half_live = __ballot(!done);
+            const int nlive = __builtin_popcountll(half_live);
+            store_strip<false, false>(d, im, o, in.bg + in.s_bg * b, b, sx0, sy0, lane, acc0, acc1, T, invd, last,
+                                      half_live);
+            const uint32_t my_slot = __builtin_amdgcn_mbcnt_hi((uint32_t)(half_live >> 32),
+                                                               __builtin_amdgcn_mbcnt_lo((uint32_t)half_live, 0u));
+            if ((half_live >> lane) & 1u) rec_lds[my_slot] = (unsigned)lane;
+            __builtin_amdgcn_wave_barrier();
+            hslot_ok = hj < nlive;
+            hp = hslot_ok ? (int)rec_lds[hj] : 0;
+            __builtin_amdgcn_wave_barrier();
+            Th = __shfl(T, hp);
+            invdh = __shfl(invd, hp);
+            lasth = (uint32_t)__shfl((int)last, hp);
+            stoph = STATS ? (uint32_t)__shfl((int)stop, hp) : 0u;
+            doneh = !hslot_ok;
+            // ha[r] at lane l: channel (r & 3) + 8 (r >> 2) + 4 hq of slot hj = the strip layout's register r
+            // of pixel hp, at lane (hp & 31) + 32 hq of acc_{hp >= 32}
+            {
+                const int src = (hp & 31) + 32 * hq;
+                const bool up = hp >= 32;
+#pragma unroll
+                for (int r = 0; r < 16; r++) {
+                    const float x0 = __shfl(acc0[r], src), x1 = __shfl(acc1[r], src);
+                    ha[r] = up ? x1 : x0;
+                }
+            }
+            const float hfx = (float)(sx0 + hp % kStripW), hfy = (float)(sy0 + hp / kStripW);
+            const int hrec_w = lane < 16 ? lane : 24 + lane;  // lanes 16..63 -> spare words 40..87
+#define GSR_HFETCH(S)                                                                               \
+            {                                                                                       \
+                uint32_t ga_ = (uint32_t)d.P, gb_ = (uint32_t)d.P;                                  \
+                int pa_ = 0, pb_ = 0;                                                               \
+                if (__builtin_expect(__builtin_popcountll(mask) >= 2, 1)) {                         \
+                    const int i0_ = (int)__builtin_ctzll(mask); mask &= mask - 1;                   \
+                    const int i1_ = (int)__builtin_ctzll(mask); mask &= mask - 1;                   \
+                    ga_ = __builtin_amdgcn_readlane(cidx, i0_) & kIndexMask; pa_ = base + i0_ + 1;  \
+                    gb_ = __builtin_amdgcn_readlane(cidx, i1_) & kIndexMask; pb_ = base + i1_ + 1;  \
+                    S##v = true;                                                                    \
+                } else {                                                                            \
+                    S##v = GSR_NEXT(ga_, pa_);                                                      \
+                    if (S##v && !GSR_NEXT(gb_, pb_)) gb_ = (uint32_t)d.P;                           \
+                    if (!S##v) ga_ = (uint32_t)d.P;                                                 \
+                }                                                                                   \
+                S##pa = pa_; S##pb = pb_;                                                           \
+                const uint32_t gr_ = (lane & 8) ? gb_ : ga_;                                        \
+                S##r = __builtin_amdgcn_raw_buffer_load_b32(                                        \
+                    rrs, lane < 16 ? (int)(gr_ * 32u + (uint32_t)(lane & 7) * 4u) : (int)kOOB, 0, 0); \
+                const uint32_t gf_ = hq ? gb_ : ga_;                                                \
+                S##f = __builtin_amdgcn_raw_buffer_load_b32(qfs, (int)(gf_ * (uint32_t)(GSR_C * 4) + (uint32_t)hj * 4u), 0, 0); \
+            }
+#define GSR_HSTEP(S)                                                                                \
+            {                                                                                       \
+                rec_lds[hrec_w] = S##r;                                                             \
+                __builtin_amdgcn_wave_barrier();                                                    \
+                const float4 ra_ = __builtin_bit_cast(float4, *(const uint4x*)&rec_lds[8 * hq]);    \
+                const float4 rc_ = __builtin_bit_cast(float4, *(const uint4x*)&rec_lds[8 * hq + 4]); \
+                __builtin_amdgcn_wave_barrier();                                                    \
+                const float al_ = alpha_of<EXACT>(ra_, rc_, hfx, hfy);                              \
+                const auto a_ = __builtin_amdgcn_permlane32_swap(__float_as_uint(al_), __float_as_uint(al_), \
+                                                                  false, false);                    \
+                const auto i_ = __builtin_amdgcn_permlane32_swap(__float_as_uint(ra_.w), __float_as_uint(ra_.w), \
+                                                                  false, false);                    \
+                const bool was_ = doneh;                                                            \
+                const float w0_ = take_step(__uint_as_float(a_[0]), __uint_as_float(i_[0]), (uint32_t)S##pa, \
+                                            Th, invdh, lasth, doneh);                               \
+                if (STATS && !was_ && doneh) stoph = (uint32_t)S##pa;                               \
+                const bool was1_ = doneh;                                                           \
+                const float w1_ = take_step(__uint_as_float(a_[1]), __uint_as_float(i_[1]), (uint32_t)S##pb, \
+                                            Th, invdh, lasth, doneh);                               \
+                if (STATS && !was1_ && doneh) stoph = (uint32_t)S##pb;                              \
+                const float wq_ = hq ? w1_ : w0_;                                                   \
+                ha = __builtin_amdgcn_mfma_f32_32x32x2f32(__uint_as_float(S##f), wq_, ha, 0, 0, 0); \
+                if (STATS) {                                                                        \
+                    n_contrib_pairs += __popcll(__ballot(wq_ > 0.f));                               \
+                    n_hsurv += 1 + (S##pb > 0);                                                     \
+                }                                                                                   \
+                if (TL) n_steps += 1;                                                               \
+            }
+            bool Xv = false, Yv = false, to_q = false;
+            int Xpa, Xpb, Ypa, Ypb;
+            unsigned Xr, Xf, Yr, Yf;
+            // live half slots (lanes 0..31 carry every slot; the upper half duplicates them)
+#define GSR_HLIVE() ((uint32_t)__ballot(!doneh))
+            if (nlive > 0) {
+                GSR_HFETCH(X)
+                while (Xv) {
+                    GSR_HFETCH(Y)
+                    GSR_HSTEP(X)
+                    if (!Yv) break;
+                    {
+                        const int nl_ = __builtin_popcount(GSR_HLIVE());
+                        if (nl_ == 0) break;
+                        if (nl_ <= 16) {  /* Y's survivors are fetched: take them here first */
+                            GSR_HSTEP(Y)
+                            to_q = true;
+                            break;
+                        }
+                    }
+                    GSR_HFETCH(X)
+                    GSR_HSTEP(Y)
+                    {
+                        const int nl_ = __builtin_popcount(GSR_HLIVE());
+                        if (nl_ == 0) break;
+                        if (nl_ <= 16) {  /* X is fetched: take it, then the quad tail */
+                            if (Xv) GSR_HSTEP(X)
+                            to_q = true;
+                            break;
+                        }
+                    }
+                }
+            }
+#undef GSR_HFETCH
+#undef GSR_HSTEP
+            // slots still live go on to the quad tail (if it takes over), the rest are final now
+            const uint32_t hl = to_q ? GSR_HLIVE() : 0u;
+#undef GSR_HLIVE
+            half_quad = hl;
+            to_quad = to_q && hl != 0u;
+            {
+                const int64_t HW = (int64_t)d.H * d.W;
+                const int64_t pix = b * HW + (int64_t)(sy0 + hp / kStripW) * d.W + (sx0 + hp % kStripW);
+                const bool st = hslot_ok && !((hl >> hj) & 1u);
+                if (st && hq == 0) {
+                    im.final_T[pix] = Th;
+                    im.n_contrib[pix] = lasth;
+                    if (o.out_invdepth) o.out_invdepth[pix] = invdh;
+                }
+                const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+                    o.out_color + (int64_t)b * GSR_C * HW, 0, (int)((int64_t)GSR_C * HW * 4), 0x00020000);
+                const float* bgp = in.bg + in.s_bg * b;
+                const float bgl = bgp[lane & 31];
+                const int vo = st ? (int)((pix - b * HW) * 4) : 0x7FFFFFF0;
+#pragma unroll
+                for (int r = 0; r < 16; r++) {
+                    const int c = (r & 3) + 8 * (r >> 2) + 4 * hq;
+                    const float bgc = __shfl(bgl, c);
+                    __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(fmaf(Th, bgc, ha[r])), rs, vo,
+                                                          c * (int)HW * 4, 0);
+                }
+                if (STATS && st && hq == 0) ev_half = doneh ? stoph : (uint32_t)n;
+            }
+        }
+
         // ---- quad tail ----
         // The strip's <= 16 still-blending pixels, compacted into 16 slots; each step takes the next
         // FOUR survivors, lane = slot + 16 q computing Gaussian q's alpha at its slot's pixel (one
@@ -733,6 +901,30 @@ __device__ __forceinline__ void render_fwd_body(const Dims& d, const Inputs& in,
                 Ts = 1.0f; invds = 0.f; lasts = 0u; stops = 0u;
 #pragma unroll
                 for (int r = 0; r < 4; r++) { qa0[r] = 0.f; qa1[r] = 0.f; }
+            } else if (HTAIL && to_half) {
+                // from the half tail: quad slot j <- the j-th live half slot
+                nlive = __builtin_popcount((uint32_t)half_quad);
+                const uint32_t my_slot = __builtin_amdgcn_mbcnt_lo((uint32_t)half_quad, 0u);
+                if (lane < 32 && ((half_quad >> lane) & 1u)) rec_lds[my_slot] = (unsigned)lane;
+                __builtin_amdgcn_wave_barrier();
+                slot_ok = j < nlive;
+                const int hs = slot_ok ? (int)rec_lds[j] : 0;
+                __builtin_amdgcn_wave_barrier();
+                p = __shfl(hp, hs);
+                Ts = __shfl(Th, hs);
+                invds = __shfl(invdh, hs);
+                lasts = (uint32_t)__shfl((int)lasth, hs);
+                stops = STATS ? (uint32_t)__shfl((int)stoph, hs) : 0u;
+                // channel c of half slot hs sits in ha[(c & 3) + 4 (c >> 3)] at lane hs + 32 ((c >> 2) & 1)
+                const int src = hs + 32 * (q & 1);
+                const bool h2 = (q >> 1) != 0;
+#pragma unroll
+                for (int r = 0; r < 4; r++) {
+                    const float a0 = __shfl(ha[r], src), a1 = __shfl(ha[r + 4], src);
+                    qa0[r] = h2 ? a1 : a0;
+                    const float b0 = __shfl(ha[r + 8], src), b1 = __shfl(ha[r + 12], src);
+                    qa1[r] = h2 ? b1 : b0;
+                }
             } else {
             quad_live = __ballot(!done);
             nlive = __builtin_popcountll(quad_live);
@@ -771,10 +963,6 @@ __device__ __forceinline__ void render_fwd_body(const Dims& d, const Inputs& in,
             }
             bool dones = !slot_ok;
             const float qfx = (float)(sx0 + p % kStripW), qfy = (float)(sy0 + p / kStripW);
-            // f32 features (the quad tail runs in the exact mode only)
-            const __amdgpu_buffer_rsrc_t qfs = __builtin_amdgcn_make_buffer_rsrc(
-                (void*)(in.colors + in.s_colors * b), 0, (int)min((int64_t)d.P * GSR_C * 4, (int64_t)0x7FFFFFFF),
-                0x00020000);
             const int qrec_w = lane < 32 ? lane : 24 + lane;  // LDS word of this lane's record dword
             const int rq = (lane >> 3) & 3;                   // record loads: lanes 8 rq .. 8 rq + 7
             // next four survivors of the strip (index P past the list's end: zero record, zero feature)
@@ -906,8 +1094,9 @@ __device__ __forceinline__ void render_fwd_body(const Dims& d, const Inputs& in,
         if (STATS) {
             unsigned long long* cn = (unsigned long long*)o.stats;
             // pixels handed to the quad tail count there (ev_quad, one lane per slot)
-            uint64_t ev = (px < d.W && py < d.H && !((quad_live >> lane) & 1u)) ? (done ? stop : (uint32_t)n) : 0;
-            ev += ev_quad;
+            uint64_t ev = (px < d.W && py < d.H && !(((quad_live | half_live) >> lane) & 1u))
+                              ? (done ? stop : (uint32_t)n) : 0;
+            ev += ev_quad + ev_half;
             for (int off = 32; off > 0; off >>= 1) ev += __shfl_xor(ev, off);
             if (lane == 0) {
                 atomicAdd(&cn[0], (unsigned long long)ev);
@@ -917,6 +1106,7 @@ __device__ __forceinline__ void render_fwd_body(const Dims& d, const Inputs& in,
                 atomicAdd(&cn[4], (unsigned long long)n_staged);
                 atomicAdd(&cn[7], (unsigned long long)n_dead);
                 atomicAdd(&cn[8], (unsigned long long)n_qsurv);
+                atomicAdd(&cn[9], (unsigned long long)n_hsurv);
                 if (strip == 0) {
                     atomicAdd(&cn[5], (unsigned long long)n);
                     atomicAdd(&cn[6], 1ull);
@@ -933,7 +1123,7 @@ __device__ __forceinline__ void render_fwd_body(const Dims& d, const Inputs& in,
         }
         if constexpr (HALF) store_half(d, im, o, in.bg + in.s_bg * b, b, sx0, sy0 + half * (32 / kStripW), lane,
                                        acc0, T, invd, last);
-        else if (QUAD && (QONLY || to_quad)) {  /* stored by the quad tail */
+        else if (QUAD && (QONLY || to_quad || to_half)) {  /* stored by the half / quad tails */
         } else if (ABL == 9) {  /* timing ablation: only final_T of the strip is stored */
             if (px < d.W && py < d.H) im.final_T[b * (int64_t)d.H * d.W + (int64_t)py * d.W + px] = T + acc0[0] + acc1[0];
         }
@@ -953,11 +1143,11 @@ __device__ __forceinline__ void render_fwd_body(const Dims& d, const Inputs& in,
 #define GSR_QONLY_WPE 6  // quad-only waves (one frame): no 32-register strip accumulators
 #endif
 template <bool EXACT, bool STATS, bool TL, int SPLIT = 0, int NSLOT = GSR_BATCH_NSLOT, bool HALF = false,
-          bool QUAD = false, bool QONLY = false>
+          bool QUAD = false, bool QONLY = false, bool HTAIL = false>
 __global__ __launch_bounds__(GSR_TILE_PIX)
 __attribute__((amdgpu_waves_per_eu(QONLY ? GSR_QONLY_WPE : (NSLOT == 5 && !HALF) ? 3 : GSR_RENDER_WPE))) void k_render_fwd(
     Dims d, Inputs in, GeomArena g, ImageArena im, BinArena bn, Outputs o) {
-    render_fwd_body<EXACT, STATS, TL, false, 0, SPLIT, NSLOT, HALF, QUAD, QONLY>(d, in, g, im, bn, o);
+    render_fwd_body<EXACT, STATS, TL, false, 0, SPLIT, NSLOT, HALF, QUAD, QONLY, HTAIL>(d, in, g, im, bn, o);
 }
 
 // Timing ablations of the production kernel (GSR_RENDER_ABLATE=1: VALU stand-in for the MFMAs,
@@ -1002,12 +1192,16 @@ void launch_render_fwd(const Dims& d, const Inputs& in_, const GeomArena& g, con
     // GSR_QUAD_TAIL=0: no quad tail (A/B); the f32 (non-split) throughput kernel and its instrumented
     // variants take it by default
     static const bool quad = [] { const char* e = getenv("GSR_QUAD_TAIL"); return !(e && e[0] == '0'); }();
+    // GSR_HALF_TAIL=0: no half tail before the quad tail (A/B)
+    static const bool htail = [] { const char* e = getenv("GSR_HALF_TAIL"); return !(e && e[0] == '0'); }();
     const bool qt = quad && !split;
+    const bool ht = qt && htail;
     const int grid = min((nwaves + 3) / 4, persistent_grid(wg_per_cu));
     const dim3 gr(grid), bl(GSR_TILE_PIX);
 #define GSR_LAUNCH(E, S, L)                                                                                   \
     {                                                                                                         \
-        if (qt) hipLaunchKernelGGL((k_render_fwd<E, S, L, 0, GSR_BATCH_NSLOT, false, true>), gr, bl, 0, s, d, in, g, im, b, o); \
+        if (ht) hipLaunchKernelGGL((k_render_fwd<E, S, L, 0, GSR_BATCH_NSLOT, false, true, false, true>), gr, bl, 0, s, d, in, g, im, b, o); \
+        else if (qt) hipLaunchKernelGGL((k_render_fwd<E, S, L, 0, GSR_BATCH_NSLOT, false, true>), gr, bl, 0, s, d, in, g, im, b, o); \
         else hipLaunchKernelGGL((k_render_fwd<E, S, L>), gr, bl, 0, s, d, in, g, im, b, o);                  \
     }
     if (o.stats) {

@@ -244,7 +244,8 @@ int gsr_profile_read(double* ms, int* counts, int n);
  * wave, [4] Gaussians staged (list entries loaded into LDS), [5] list entries of all tiles,
  * [6] tiles rendered, [7] k-steps in which no pixel of the wave took either Gaussian, [8] survivors
  * blended in the quad tail (16 pixel slots, 4 Gaussians per step; [2] counts the 64-pixel strip
- * layout's).  NULL restores the production kernel. */
+ * layout's), [9] survivors blended in the half tail (32 slots, 2 Gaussians per step).  NULL
+ * restores the production kernel. */
 int gsr_render_counters(uint64_t* device_counters);
 /* Work-item timeline of the render kernel (a lightly instrumented variant runs while set):
  * record i (4 uint32: start, end in 100 MHz ticks, MFMA k-steps, XCD) for the first `capacity`

@@ -119,7 +119,7 @@ def test_render_counters_match_oracle(kind, P, W, H):
     if kind == "avatar":  # opaque avatar strips finish unevenly: the quad tail ran (and was bit-exact)
         assert cnt["quad_survivors"] > 0
     # lane-pairs blended: 64 per survivor in the strip layout, 16 in the quad tail (<= 16 live pixels)
-    assert contrib <= cnt["strip_pairs_blended"] * 64 + cnt["quad_survivors"] * 16
+    assert contrib <= cnt["strip_pairs_blended"] * 64 + cnt["half_survivors"] * 32 + cnt["quad_survivors"] * 16
     # survivors are taken two per k-step, an odd round tail pads with the null Gaussian
     assert cnt["strip_pairs_blended"] <= 2 * cnt["mfma_ksteps"] <= cnt["strip_pairs_blended"] + cnt["gaussians_staged"]
 
@@ -228,7 +228,7 @@ def _batch_vs_oracle(kind, P, W, H, seed, antialiasing=False, yaw=(0.0, 0.25), c
             contrib += k
     if counters:
         assert cnt["pairs_evaluated"] == visited and cnt["pairs_contributing"] == contrib
-        assert contrib <= cnt["strip_pairs_blended"] * 64 + cnt["quad_survivors"] * 16
+        assert contrib <= cnt["strip_pairs_blended"] * 64 + cnt["half_survivors"] * 32 + cnt["quad_survivors"] * 16
 
 
 @pytest.mark.parametrize("kind,P,W,H", [("random", 10000, 256, 256), ("avatar", 20000, 200, 136),

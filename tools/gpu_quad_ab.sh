@@ -7,8 +7,9 @@ OUT=gpurun_out/quad_${1:-x}
 mkdir -p $OUT
 timeout -k 10 400 python -u -m pytest tests/test_gpu_forward.py tests/test_gpu_fullsize.py tests/test_gpu_api_edges.py -x -q --timeout 120 --timeout-method thread > $OUT/pytest.log 2>&1; rc=$?; echo "pytest rc=$rc"; tail -3 $OUT/pytest.log
 [ $rc -eq 0 ] || exit $rc
-for v in 1 0 1; do
-  GSR_QUAD_TAIL=$v timeout -k 10 200 python bench.py --no-cpu-baseline --no-extras --inflight ${INFL:-1} --steps 100 --warmup 10 > $OUT/bench_q$v.json 2> $OUT/bench_q$v.err; rc=$?
+for v in 1 0 1 h; do
+  H=1; Q=$v; [ $v = h ] && { H=0; Q=1; }
+  GSR_HALF_TAIL=$H GSR_QUAD_TAIL=$Q timeout -k 10 200 python bench.py --no-cpu-baseline --no-extras --inflight ${INFL:-1} --steps 100 --warmup 10 > $OUT/bench_q$v.json 2> $OUT/bench_q$v.err; rc=$?
   echo "quad=$v rc=$rc"; [ $rc -eq 0 ] || { tail -5 $OUT/bench_q$v.err; exit $rc; }
   python -c "
 import json; d=json.load(open('$OUT/bench_q$v.json'))
