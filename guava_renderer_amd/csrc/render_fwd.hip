@@ -1039,17 +1039,23 @@ __device__ __forceinline__ void render_fwd_body(const Dims& d, const Inputs& in,
                 }                                                                                   \
                 if (TL) n_steps += 1;  /* (STATS: quad steps in cn[8] as survivors, not k-steps) */ \
             }
-            bool Xv = false, Yv = false;
-            int Xp0, Xp1, Xp2, Xp3, Yp0, Yp1, Yp2, Yp3;
-            unsigned Xr, Xf0, Xf1, Yr, Yf0, Yf1;
+            // three slots in rotation: a step's survivors are requested two steps before their blend
+            bool Xv = false, Yv = false, Zv = false;
+            int Xp0, Xp1, Xp2, Xp3, Yp0, Yp1, Yp2, Yp3, Zp0, Zp1, Zp2, Zp3;
+            unsigned Xr, Xf0, Xf1, Yr, Yf0, Yf1, Zr, Zf0, Zf1;
             if (nlive > 0) {
                 GSR_QFETCH(X)
-                while (Xv) {
-                    GSR_QFETCH(Y)
+                GSR_QFETCH(Y)
+                for (;;) {
+                    if (!Xv) break;
+                    GSR_QFETCH(Z)
                     GSR_QSTEP(X)
                     if (!Yv || !__any(!dones)) break;
                     GSR_QFETCH(X)
                     GSR_QSTEP(Y)
+                    if (!Zv || !__any(!dones)) break;
+                    GSR_QFETCH(Y)
+                    GSR_QSTEP(Z)
                     if (!__any(!dones)) break;
                 }
             }

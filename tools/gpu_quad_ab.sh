@@ -13,7 +13,7 @@ for v in 1 0 1 h; do
   echo "quad=$v rc=$rc"; [ $rc -eq 0 ] || { tail -5 $OUT/bench_q$v.err; exit $rc; }
   python -c "
 import json; d=json.load(open('$OUT/bench_q$v.json'))
-print('quad=$v', d['value'], d['ms_per_step'], d['roofline']['avg_launch_ms'], d['render_mfma']['useful_frac'], {k: d['render_work_per_frame'][k] for k in ('mfma_ksteps','strip_pairs_blended','quad_survivors') if k in d['render_work_per_frame']})"
+print('quad=$v', d['value'], d['ms_per_step'], d['roofline']['avg_launch_ms'], d['render_mfma']['useful_frac'], {k: d['render_work_per_frame'][k] for k in ('mfma_ksteps','strip_pairs_blended','half_survivors','quad_survivors') if k in d['render_work_per_frame']})"
 done
 for v in 1 0; do
   GSR_RENDER_QONLY=$v timeout -k 10 200 python bench.py --pipeline frame --no-cpu-baseline --no-extras --steps 8 --warmup 2 > $OUT/frame_q$v.json 2> $OUT/frame_q$v.err; rc=$?
