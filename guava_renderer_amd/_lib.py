@@ -17,7 +17,8 @@ EXPORTS = ("gsr_version", "gsr_last_error", "gsr_geometry_bytes",
            "gsr_render_counters", "gsr_render_timeline", "gsr_forward_batch_refine",
            "gsr_refine_prepare", "gsr_batch_status_offset", "gsr_frames_to8b",
            # include/gsr_deform.h
-           "gsr_lbs_workspace_bytes", "gsr_lbs", "gsr_blend_joints", "gsr_splice_head",
+           "gsr_lbs_workspace_bytes", "gsr_lbs", "gsr_lbs_sp", "gsr_blend_joints", "gsr_blend_joints_sp",
+           "gsr_splice_head",
            "gsr_pack_rows", "gsr_deform_gaussians",
            # include/gsr_ssim.h
            "gsr_fused_ssim", "gsr_fused_ssim_backward", "gsr_image_loss_partials", "gsr_image_loss")
@@ -55,6 +56,12 @@ class RowSegment(ctypes.Structure):
     """GsrRowSegment (include/gsr_deform.h)."""
     _fields_ = [("src", _vp), ("dst", _vp), ("src_stride", _i64), ("dst_stride", _i64), ("width", _i),
                 ("pad_", _i)]
+
+
+class LbsSparse(ctypes.Structure):
+    """GsrLbsSparse (include/gsr_deform.h)."""
+    _fields_ = [("jreg_row", _vp), ("jreg_col", _vp), ("jreg_val", _vp), ("skin_k", ctypes.c_int32),
+                ("pad_", ctypes.c_int32), ("skin_joint", _vp), ("skin_weight", _vp)]
 
 
 class GsrError(RuntimeError):
@@ -153,8 +160,14 @@ def load(path=None):
     L.gsr_lbs.argtypes = [_i, _i, _i, _i, _vp, _i64, _vp, _vp, _vp, _i, _vp, _vp, _vp, _vp, _vp, _vp,
                           _vp, _vp, _vp, _vp, _vp, _vp, _vp]
     L.gsr_lbs.restype = _i
+    L.gsr_lbs_sp.argtypes = [_i, _i, _i, _i, _vp, _i64, _vp, _vp, _vp, _i, _vp, _vp, _vp, _vp, _vp, _vp,
+                             _vp, _vp, _vp, _vp, _vp, _vp, ctypes.POINTER(LbsSparse), _vp]
+    L.gsr_lbs_sp.restype = _i
     L.gsr_blend_joints.argtypes = [_i, _i, _i, _i, _vp, _i64, _vp, _vp, _vp, _vp, _vp, _vp, _vp]
     L.gsr_blend_joints.restype = _i
+    L.gsr_blend_joints_sp.argtypes = [_i, _i, _i, _i, _vp, _i64, _vp, _vp, _vp, _vp, _vp, _vp,
+                                      ctypes.POINTER(LbsSparse), _vp]
+    L.gsr_blend_joints_sp.restype = _i
     L.gsr_splice_head.argtypes = [_i, _i, _i, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i, _i, _i, _vp, _i,
                                   _i, _i, _vp, _vp, _vp]
     L.gsr_splice_head.restype = _i

@@ -394,6 +394,42 @@ __global__ __launch_bounds__(256) void k_lbs_joints(int V, int J, const float* _
     }
 }
 
+// vertices2joints over the J_regressor's nonzeros (CSR rows, vertex order; gsr_lbs_sp): one wave
+// per (joint, frame), lanes take the row's nonzeros 64 at a time (each lane its own fmaf chain in
+// index order), then a fixed xor-tree across the lanes -- deterministic run to run.  SMPL-X / FLAME
+// joint regressors are sparse (a joint averages a few dozen vertices), so a frame's joints cost one
+// load round instead of the dense kernel's pass over J x V weights.
+__global__ __launch_bounds__(256) void k_lbs_joints_csr(int B, int V, int J, const int32_t* __restrict__ row,
+                                                        const int32_t* __restrict__ col,
+                                                        const float* __restrict__ val,
+                                                        const float* __restrict__ v_shaped,
+                                                        const float* __restrict__ joff,
+                                                        float* __restrict__ joints) {
+    const int w = (int)((blockIdx.x * 256u + threadIdx.x) >> 6), lane = threadIdx.x & 63;
+    if (w >= B * J) return;
+    const int b = w / J, j = w - b * J;
+    const float* vs = v_shaped + (int64_t)b * V * 3;
+    float x = 0.f, y = 0.f, z = 0.f;
+    for (int k = row[j] + lane; k < row[j + 1]; k += 64) {
+        const int v = col[k];
+        const float wv = val[k];
+        x = fmaf(wv, vs[3 * v], x);
+        y = fmaf(wv, vs[3 * v + 1], y);
+        z = fmaf(wv, vs[3 * v + 2], z);
+    }
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+        x += __shfl_xor(x, off);
+        y += __shfl_xor(y, off);
+        z += __shfl_xor(z, off);
+    }
+    if (lane < 3) {
+        float v = lane == 0 ? x : lane == 1 ? y : z;
+        if (joff) v = v + joff[((int64_t)b * J + j) * 3 + lane];
+        joints[((int64_t)b * J + j) * 3 + lane] = v;
+    }
+}
+
 // batch_rigid_transform (lbs.py:426-482), one frame per workgroup: local transforms
 // [R | J_i - J_parent], the chain product chain_i = chain_parent . local_i, posed joints =
 // chain[:, :3, 3], A = chain - pad(chain . [J; 0]).  The chain runs level by level of the kinematic
@@ -452,6 +488,52 @@ __global__ __launch_bounds__(16 * GSR_LBS_MAX_JOINTS) void k_lbs_chain(int J, Pa
         }
         if (jtrans)
             for (int rr = 0; rr < 3; rr++) jtrans[((int64_t)b * J + t) * 3 + rr] = T[4 * rr + 3];
+    }
+}
+
+// Skinning over each vertex's nonzero weights (ELL: K (joint, weight) pairs per vertex, joints
+// increasing, padding weight 0; gsr_lbs_sp): the same fmaf chains in joint order as k_lbs_skin,
+// minus its terms with a zero weight (fma(0, a, t) == t), so the results are bit-identical to the
+// dense kernel's with K loads per vertex instead of J.
+template <int KMAX>
+__global__ __launch_bounds__(256) void k_lbs_skin_ell(int V, int J, int K, const int32_t* __restrict__ sj,
+                                                      const float* __restrict__ sw,
+                                                      const float* __restrict__ A,
+                                                      const float* __restrict__ v_posed,
+                                                      float* __restrict__ verts,
+                                                      float* __restrict__ vtrans) {
+    __shared__ float As[GSR_LBS_MAX_JOINTS * 16];
+    const int b = blockIdx.y;
+    for (int i = threadIdx.x; i < J * 16; i += blockDim.x) As[i] = A[(int64_t)b * J * 16 + i];
+    __syncthreads();
+    const int v = blockIdx.x * blockDim.x + threadIdx.x;
+    if (v >= V) return;
+    int jj[KMAX];
+    float ww[KMAX];
+#pragma unroll
+    for (int u = 0; u < KMAX; u++) {
+        jj[u] = u < K ? sj[(int64_t)u * V + v] : 0;
+        ww[u] = u < K ? sw[(int64_t)u * V + v] : 0.f;
+    }
+    float T[16];
+#pragma unroll
+    for (int e = 0; e < 16; e++) T[e] = 0.f;
+#pragma unroll
+    for (int u = 0; u < KMAX; u++) {
+        if (u >= K) break;
+        const float* Aj = As + 16 * jj[u];
+#pragma unroll
+        for (int e = 0; e < 16; e++) T[e] = fmaf(ww[u], Aj[e], T[e]);
+    }
+    const float* vp = v_posed + ((int64_t)b * V + v) * 3;
+    const float px = vp[0], py = vp[1], pz = vp[2];
+    float* out = verts + ((int64_t)b * V + v) * 3;
+#pragma unroll
+    for (int r = 0; r < 3; r++) out[r] = T[4 * r] * px + T[4 * r + 1] * py + T[4 * r + 2] * pz + T[4 * r + 3] * 1.0f;
+    if (vtrans) {
+        float* o = vtrans + ((int64_t)b * V + v) * 16;
+#pragma unroll
+        for (int e = 0; e < 16; e++) o[e] = T[e];
     }
 }
 
@@ -771,13 +853,53 @@ size_t gsr_lbs_workspace_bytes(int B, int V, int J, int NB) {
     return carve_lbs(nullptr, B, V, J, nullptr);
 }
 
+}  // extern "C"
+
+namespace {
+// the joint regression of gsr_lbs / gsr_blend_joints: CSR rows when given, else the dense kernel
+void launch_joints(int B, int V, int J, const float* J_regressor, const GsrLbsSparse* sp, const float* vs,
+                   const float* joints_offset, float* joints, hipStream_t s) {
+    if (sp && sp->jreg_row) {
+        hipLaunchKernelGGL(k_lbs_joints_csr, dim3((B * J + 3) / 4), dim3(256), 0, s, B, V, J, sp->jreg_row,
+                           sp->jreg_col, sp->jreg_val, vs, joints_offset, joints);
+    } else {
+        hipLaunchKernelGGL(k_lbs_joints, dim3((J + kJointsPerWG - 1) / kJointsPerWG, B), dim3(256), 0, s, V, J,
+                           J_regressor, vs, joints_offset, joints);
+    }
+}
+int check_sparse(const GsrLbsSparse* sp, int J, const char* who) {
+    if (!sp) return 0;
+    if (sp->jreg_row && (!sp->jreg_col || !sp->jreg_val))
+        return api_fail(GSR_ERR_ARG, (std::string(who) + ": jreg_row without jreg_col / jreg_val").c_str());
+    if (sp->skin_k && (sp->skin_k < 0 || sp->skin_k > GSR_LBS_SKIN_MAX_K || !sp->skin_joint || !sp->skin_weight))
+        return api_fail(GSR_ERR_ARG, (std::string(who) + ": skin_k must be in [1, 16] with its arrays").c_str());
+    (void)J;
+    return 0;
+}
+}  // namespace
+
+extern "C" {
+
 int gsr_lbs(int B, int V, int J, int NB, const float* v_template, int64_t v_template_stride,
             const float* betas, const float* shapedirs_t, const float* pose, int pose2rot,
             const float* posedirs, const float* J_regressor, const int32_t* parents_host,
             const float* lbs_weights_t, const float* joints_offset, float* verts,
             float* joints_transformed, float* joints, float* vert_transforms,
             float* joint_transforms, float* v_shaped, char* workspace, void* stream) {
+    return gsr_lbs_sp(B, V, J, NB, v_template, v_template_stride, betas, shapedirs_t, pose, pose2rot, posedirs,
+                      J_regressor, parents_host, lbs_weights_t, joints_offset, verts, joints_transformed, joints,
+                      vert_transforms, joint_transforms, v_shaped, workspace, nullptr, stream);
+}
+
+int gsr_lbs_sp(int B, int V, int J, int NB, const float* v_template, int64_t v_template_stride,
+               const float* betas, const float* shapedirs_t, const float* pose, int pose2rot,
+               const float* posedirs, const float* J_regressor, const int32_t* parents_host,
+               const float* lbs_weights_t, const float* joints_offset, float* verts,
+               float* joints_transformed, float* joints, float* vert_transforms,
+               float* joint_transforms, float* v_shaped, char* workspace, const GsrLbsSparse* sp,
+               void* stream) {
     if (B <= 0 || V <= 0) return api_fail(GSR_ERR_ARG, "gsr_lbs: B and V must be positive");
+    if (int rc = check_sparse(sp, J, "gsr_lbs")) return rc;
     if (J < 1 || J > GSR_LBS_MAX_JOINTS) return api_fail(GSR_ERR_ARG, "gsr_lbs: J must be in [1, 64]");
     if (!v_template || !pose || !J_regressor || !parents_host || !lbs_weights_t || !verts || !workspace)
         return api_fail(GSR_ERR_ARG, "gsr_lbs: null required pointer");
@@ -812,20 +934,41 @@ int gsr_lbs(int B, int V, int J, int NB, const float* v_template, int64_t v_temp
     if (lbs_blend_lds(NB, NP, kLbsFrames, kLbsSplit) > 160 * 1024) return api_fail(GSR_ERR_ARG, "gsr_lbs: NB + 9(J-1) too large for LDS");
     launch_blend(B, M, NB, NP, v_template, v_template_stride, betas, shapedirs_t, a.feat, posedirs, vs, a.vp, s);
     if (int rc = hip_check("lbs_blend")) return rc;
-    hipLaunchKernelGGL(k_lbs_joints, dim3((J + kJointsPerWG - 1) / kJointsPerWG, B), dim3(256), 0, s, V, J, J_regressor, vs,
-                       joints_offset, jr);
+    launch_joints(B, V, J, J_regressor, sp, vs, joints_offset, jr, s);
     if (int rc = hip_check("lbs_joints")) return rc;
     hipLaunchKernelGGL(k_lbs_chain, dim3(B), dim3(16 * GSR_LBS_MAX_JOINTS), 0, s, J, par, a.rot, jr, joints_transformed, A);
     if (int rc = hip_check("lbs_chain")) return rc;
-    hipLaunchKernelGGL(k_lbs_skin, dim3((V + 255) / 256, B), dim3(256), 0, s, V, J, lbs_weights_t, A,
-                       a.vp, verts, vert_transforms);
+    if (sp && sp->skin_k > 0) {
+        const dim3 g((V + 255) / 256, B);
+        if (sp->skin_k <= 4)
+            hipLaunchKernelGGL(k_lbs_skin_ell<4>, g, dim3(256), 0, s, V, J, sp->skin_k, sp->skin_joint,
+                               sp->skin_weight, A, a.vp, verts, vert_transforms);
+        else if (sp->skin_k <= 8)
+            hipLaunchKernelGGL(k_lbs_skin_ell<8>, g, dim3(256), 0, s, V, J, sp->skin_k, sp->skin_joint,
+                               sp->skin_weight, A, a.vp, verts, vert_transforms);
+        else
+            hipLaunchKernelGGL(k_lbs_skin_ell<16>, g, dim3(256), 0, s, V, J, sp->skin_k, sp->skin_joint,
+                               sp->skin_weight, A, a.vp, verts, vert_transforms);
+    } else {
+        hipLaunchKernelGGL(k_lbs_skin, dim3((V + 255) / 256, B), dim3(256), 0, s, V, J, lbs_weights_t, A,
+                           a.vp, verts, vert_transforms);
+    }
     return hip_check("lbs_skin");
 }
 
 int gsr_blend_joints(int B, int V, int J, int NB, const float* v_template, int64_t v_template_stride,
                      const float* betas, const float* shapedirs_t, const float* J_regressor,
                      const float* joints_offset, float* v_shaped, float* joints, void* stream) {
+    return gsr_blend_joints_sp(B, V, J, NB, v_template, v_template_stride, betas, shapedirs_t, J_regressor,
+                               joints_offset, v_shaped, joints, nullptr, stream);
+}
+
+int gsr_blend_joints_sp(int B, int V, int J, int NB, const float* v_template, int64_t v_template_stride,
+                        const float* betas, const float* shapedirs_t, const float* J_regressor,
+                        const float* joints_offset, float* v_shaped, float* joints, const GsrLbsSparse* sp,
+                        void* stream) {
     if (B <= 0 || V <= 0 || J < 1) return api_fail(GSR_ERR_ARG, "gsr_blend_joints: bad sizes");
+    if (int rc = check_sparse(sp, J, "gsr_blend_joints")) return rc;
     if (!v_template || !J_regressor || !v_shaped || !joints)
         return api_fail(GSR_ERR_ARG, "gsr_blend_joints: null required pointer");
     if (v_template_stride != 0 && v_template_stride != (int64_t)V * 3)
@@ -838,8 +981,7 @@ int gsr_blend_joints(int B, int V, int J, int NB, const float* v_template, int64
     const int M = V * 3;
     launch_blend(B, M, NB, 0, v_template, v_template_stride, betas, shapedirs_t, nullptr, nullptr, v_shaped, nullptr, s);
     if (int rc = hip_check("blend_shapes")) return rc;
-    hipLaunchKernelGGL(k_lbs_joints, dim3((J + kJointsPerWG - 1) / kJointsPerWG, B), dim3(256), 0, s, V, J, J_regressor, v_shaped,
-                       joints_offset, joints);
+    launch_joints(B, V, J, J_regressor, sp, v_shaped, joints_offset, joints, s);
     return hip_check("vertices2joints");
 }
 

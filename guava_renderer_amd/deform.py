@@ -20,6 +20,7 @@ CPU path (CPU tensors raise).  The k-major operand layouts the kernels want (sha
 transposed) are made once per asset tensor and cached.
 """
 import ctypes
+import os
 
 import numpy as np
 import torch
@@ -244,6 +245,38 @@ class GaussianDeformer:
         return bool(self.bad.item())
 
 
+def _host(x):
+    return x.detach().cpu().numpy() if torch.is_tensor(x) else np.asarray(x)
+
+
+def sparse_lbs_assets(J_regressor, lbs_weights, device):
+    """GsrLbsSparse (include/gsr_deform.h) of one model's dense assets, built once on the host: the
+    J_regressor's nonzeros as CSR rows (vertex order) and, when every vertex has at most 16 nonzero
+    skinning weights, the weights as [K, V] (joint, weight) pairs in joint order (weight-0 padding).
+    Returns (struct, tensors kept alive by the caller)."""
+    jr = np.ascontiguousarray(_host(J_regressor), dtype=np.float32)
+    w = np.ascontiguousarray(_host(lbs_weights), dtype=np.float32)
+    J, V = jr.shape
+    nz = jr != 0
+    row = np.concatenate([[0], np.cumsum(nz.sum(1))]).astype(np.int32)
+    col = np.nonzero(nz)[1].astype(np.int32)  # row-major: vertex order inside each row
+    val = jr[nz].astype(np.float32)
+    t = lambda a: torch.as_tensor(np.ascontiguousarray(a), device=device)  # noqa: E731
+    keep = [t(row), t(col if col.size else np.zeros(1, np.int32)), t(val if val.size else np.zeros(1, np.float32))]
+    sp = _lib.LbsSparse(keep[0].data_ptr(), keep[1].data_ptr(), keep[2].data_ptr(), 0, 0, None, None)
+    wnz = w != 0
+    K = int(wnz.sum(1).max()) if V else 0
+    if 1 <= K <= 16:
+        order = np.argsort(~wnz, axis=1, kind="stable")[:, :K]  # each vertex's nonzero joints, in order
+        sj = np.where(np.take_along_axis(wnz, order, 1), order, 0).astype(np.int32)
+        sw = np.where(np.take_along_axis(wnz, order, 1), np.take_along_axis(w, sj, 1), 0.0)
+        keep += [t(sj.T), t(sw.T.astype(np.float32))]
+        sp.skin_k = K
+        sp.skin_joint = keep[3].data_ptr()
+        sp.skin_weight = keep[4].data_ptr()
+    return sp, keep
+
+
 class EHMDeformer:
     """EHM.forward (models/modules/ehm/EHM.py:36-156) for B frames on the GPU: FLAME head lbs ->
     eyelids and head scale -> body blend shapes and joints -> head splice -> body lbs_wobeta, with
@@ -267,6 +300,11 @@ class EHMDeformer:
         for a in (self.body, self.flame):
             a["shapedirs_t"] = _shapedirs_t(a["shapedirs"])
             a["lbs_weights_t"] = _weights_t(a["lbs_weights"])
+        # the sparse J_regressor / skinning weights (GSR_LBS_SPARSE=0: the dense kernels, A/B)
+        self.sparse = {}
+        if os.environ.get("GSR_LBS_SPARSE", "1") != "0":
+            for name, a in (("body", body), ("flame", flame)):
+                self.sparse[name] = sparse_lbs_assets(a["J_regressor"], a["lbs_weights"], dev)
         self.head_index = t(np.asarray(smplx2flame_ind, np.int32))
         self.l_eyelid, self.r_eyelid = t(np.asarray(l_eyelid, np.float32)), t(np.asarray(r_eyelid, np.float32))
         self.bad = torch.zeros(1, dtype=torch.int32, device=dev)
@@ -322,19 +360,21 @@ class EHMDeformer:
         # FLAME head (EHM.py:41-75)
         hv = torch.empty((B, Vh, 3), **o)
         hj = torch.empty((B, Jh, 3), **o)
-        rc = L.gsr_lbs(B, Vh, Jh, NBh, _ptr(fa["v_template"]), 0, _ptr(betas_h),
-                       _ptr(fa["shapedirs_t"]), _ptr(pose_h), 1, _ptr(fa["posedirs"]),
-                       _ptr(fa["J_regressor"]), fa["parents"].ctypes.data_as(ctypes.c_void_p),
-                       _ptr(fa["lbs_weights_t"]), None, _ptr(hv), _ptr(hj), None, None, None, None,
-                       _ptr(self._workspace(B, Vh, Jh, NBh)), st)
+        sph = ctypes.byref(self.sparse["flame"][0]) if "flame" in self.sparse else None
+        spb = ctypes.byref(self.sparse["body"][0]) if "body" in self.sparse else None
+        rc = L.gsr_lbs_sp(B, Vh, Jh, NBh, _ptr(fa["v_template"]), 0, _ptr(betas_h),
+                          _ptr(fa["shapedirs_t"]), _ptr(pose_h), 1, _ptr(fa["posedirs"]),
+                          _ptr(fa["J_regressor"]), fa["parents"].ctypes.data_as(ctypes.c_void_p),
+                          _ptr(fa["lbs_weights_t"]), None, _ptr(hv), _ptr(hj), None, None, None, None,
+                          _ptr(self._workspace(B, Vh, Jh, NBh)), sph, st)
         _lib.check(rc, "gsr_lbs (FLAME head)")
         # body template (EHM.py:101-118): blend shapes of shape ++ exp, regressed joints + offset
         joff = _f32(bp["joints_offset"]) if bp.get("joints_offset") is not None else None
         vt = torch.empty((B, Vb, 3), **o)
         tj = torch.empty((B, Jb, 3), **o)
-        _lib.check(L.gsr_blend_joints(B, Vb, Jb, NBb, _ptr(ba["v_template"]), 0, _ptr(sc),
-                                      _ptr(ba["shapedirs_t"]), _ptr(ba["J_regressor"]), _ptr(joff),
-                                      _ptr(vt), _ptr(tj), st), "gsr_blend_joints")
+        _lib.check(L.gsr_blend_joints_sp(B, Vb, Jb, NBb, _ptr(ba["v_template"]), 0, _ptr(sc),
+                                         _ptr(ba["shapedirs_t"]), _ptr(ba["J_regressor"]), _ptr(joff),
+                                         _ptr(vt), _ptr(tj), spb, st), "gsr_blend_joints")
         # head splice (EHM.py:72-75, 121-124)
         eyelid = _f32(fp["eyelid_params"]) if fp.get("eyelid_params") is not None else None
         _lib.check(L.gsr_splice_head(B, Vb, Vh, _ptr(self.head_index), _ptr(hv), _ptr(self.r_eyelid),
@@ -346,10 +386,10 @@ class EHMDeformer:
         J = torch.empty((B, Jb, 3), **o)
         T = torch.empty((B, Vb, 4, 4), **o)
         A = torch.empty((B, Jb, 4, 4), **o)
-        rc = L.gsr_lbs(B, Vb, Jb, 0, _ptr(vt), Vb * 3, None, None, _ptr(pose), 1, _ptr(ba["posedirs"]),
-                       _ptr(ba["J_regressor"]), ba["parents"].ctypes.data_as(ctypes.c_void_p),
-                       _ptr(ba["lbs_weights_t"]), _ptr(joff), _ptr(verts), _ptr(jt2), _ptr(J), _ptr(T),
-                       _ptr(A), None, _ptr(self._workspace(B, Vb, Jb, 0)), st)
+        rc = L.gsr_lbs_sp(B, Vb, Jb, 0, _ptr(vt), Vb * 3, None, None, _ptr(pose), 1, _ptr(ba["posedirs"]),
+                          _ptr(ba["J_regressor"]), ba["parents"].ctypes.data_as(ctypes.c_void_p),
+                          _ptr(ba["lbs_weights_t"]), _ptr(joff), _ptr(verts), _ptr(jt2), _ptr(J), _ptr(T),
+                          _ptr(A), None, _ptr(self._workspace(B, Vb, Jb, 0)), spb, st)
         _lib.check(rc, "gsr_lbs (SMPL-X body)")
         return {"vertices": verts, "joints": J, "joints_transform": jt2, "ver_transform_mat": T,
                 "joint_transform_mat": A}

@@ -63,12 +63,47 @@ int gsr_lbs(int B, int V, int J, int NB, const float* v_template, int64_t v_temp
             float* joints_transformed, float* joints, float* vert_transforms,
             float* joint_transforms, float* v_shaped, char* workspace, void* stream);
 
+/* Sparse forms of two dense LBS assets, built once per avatar by the caller (EHMDeformer does it at
+ * load).  Real SMPL-X / FLAME assets are sparse: a joint regresses a few dozen vertices and a vertex
+ * is skinned by a few joints.  With them, gsr_lbs_sp / gsr_blend_joints_sp take one load round per
+ * frame for the joints instead of a pass over J x V weights, and K (not J) weights per vertex.
+ *   jreg_row [J+1], jreg_col [nnz] (vertex, increasing in a row), jreg_val [nnz]: J_regressor's
+ *   nonzeros as CSR rows (NULL jreg_row: the dense J_regressor).  The joint sums are
+ *   re-associated (per-lane chains + a fixed tree), deterministic run to run.
+ *   skin_k in [1, 16] (0: the dense lbs_weights_t), skin_joint / skin_weight [skin_k, V]: per vertex
+ *   its nonzero (joint, weight) pairs in increasing joint order, padded with weight 0 -- the dense
+ *   skinning's fmaf chains minus their zero terms, so the vertices and transforms are identical. */
+typedef struct {
+    const int32_t* jreg_row;
+    const int32_t* jreg_col;
+    const float* jreg_val;
+    int32_t skin_k;
+    int32_t pad_;
+    const int32_t* skin_joint;
+    const float* skin_weight;
+} GsrLbsSparse;
+#define GSR_LBS_SKIN_MAX_K 16
+
+/* gsr_lbs with the sparse assets (sp may be NULL: gsr_lbs). */
+int gsr_lbs_sp(int B, int V, int J, int NB, const float* v_template, int64_t v_template_stride,
+               const float* betas, const float* shapedirs_t, const float* pose, int pose2rot,
+               const float* posedirs, const float* J_regressor, const int32_t* parents_host,
+               const float* lbs_weights_t, const float* joints_offset, float* verts,
+               float* joints_transformed, float* joints, float* vert_transforms,
+               float* joint_transforms, float* v_shaped, char* workspace, const GsrLbsSparse* sp,
+               void* stream);
+
 /* blend_shapes + vertices2joints (lbs.py:355-376, :335-352; EHM.py:115-118): v_shaped [B,V,3] =
  * v_template + shapedirs . betas (betas == NULL: a copy of v_template), joints [B,J,3] =
  * J_regressor . v_shaped (+ joints_offset [B,J,3] or NULL). */
 int gsr_blend_joints(int B, int V, int J, int NB, const float* v_template, int64_t v_template_stride,
                      const float* betas, const float* shapedirs_t, const float* J_regressor,
                      const float* joints_offset, float* v_shaped, float* joints, void* stream);
+/* gsr_blend_joints with the sparse J_regressor (sp may be NULL). */
+int gsr_blend_joints_sp(int B, int V, int J, int NB, const float* v_template, int64_t v_template_stride,
+                        const float* betas, const float* shapedirs_t, const float* J_regressor,
+                        const float* joints_offset, float* v_shaped, float* joints, const GsrLbsSparse* sp,
+                        void* stream);
 
 /* EHM.forward's head splice (EHM.py:72-75, :121-124) into the body template, in place:
  *   h = (head_verts + r_eyelid * eyelid[:,1] + l_eyelid * eyelid[:,0]) * head_scale

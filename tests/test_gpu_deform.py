@@ -214,6 +214,31 @@ def test_ehm_forward_then_gaussians_match_oracle():
     assert int(ehm.bad.item()) == 0
 
 
+def test_ehm_sparse_assets_match_dense(monkeypatch):
+    """EHMDeformer's sparse J_regressor (CSR) and skinning weights (K pairs per vertex) against the
+    dense kernels (GSR_LBS_SPARSE=0) at B = 1 and B = 5: the joints re-associate their sums
+    (1e-6), everything else follows within 2e-6; and both match the oracle."""
+    from guava_renderer_amd import avatar, deform
+    body, flame, extra = avatar.ehm_assets(seed=0)
+    for B in (1, 5):
+        bp, fp = avatar.ehm_params(B, seed=5000 + B)
+        outs = {}
+        for mode in ("1", "0"):
+            monkeypatch.setenv("GSR_LBS_SPARSE", mode)
+            ehm = deform.EHMDeformer(body, flame, extra["smplx2flame_ind"], extra["l_eyelid"], extra["r_eyelid"],
+                                     device=DEV)
+            assert bool(ehm.sparse) == (mode == "1")
+            if mode == "1":
+                assert ehm.sparse["body"][0].skin_k > 0  # the synthetic weights are sparse (<= 4 per vertex)
+            outs[mode] = {k: v.cpu().numpy() for k, v in
+                          ehm({k: _t(v) for k, v in bp.items()}, {k: _t(v) for k, v in fp.items()}).items()}
+        for k in ("vertices", "joints", "joints_transform", "ver_transform_mat", "joint_transform_mat"):
+            np.testing.assert_allclose(outs["1"][k], outs["0"][k], atol=2e-6, rtol=0, err_msg=k)
+        ref = lo.ehm_forward(body, flame, extra, bp, fp)
+        for k in ("vertices", "ver_transform_mat"):
+            np.testing.assert_allclose(outs["1"][k], ref[k], atol=ATOL, rtol=0, err_msg=k)
+
+
 def test_ehm_forward_large_batch_matrix_core_blend():
     """B=40 frames: the blend shapes run on the matrix-core kernel (k_lbs_blend_mfma, more than 16
     frames), one full 32-frame tile and one partial tile; V*3 = 31,425 is not a multiple of the
