@@ -5,7 +5,7 @@ set -u
 cd "$GRAFT_REPO_ROOT"
 OUT=gpurun_out/quad_${1:-x}
 mkdir -p $OUT
-timeout -k 10 400 python -u -m pytest tests/test_gpu_forward.py tests/test_gpu_fullsize.py tests/test_gpu_api_edges.py -x -q --timeout 120 --timeout-method thread > $OUT/pytest.log 2>&1; rc=$?; echo "pytest rc=$rc"; tail -3 $OUT/pytest.log
+timeout -k 10 400 python -u -m pytest tests/test_gpu_forward.py tests/test_gpu_fullsize.py tests/test_gpu_api_edges.py tests/test_gpu_deform.py -x -q --timeout 120 --timeout-method thread > $OUT/pytest.log 2>&1; rc=$?; echo "pytest rc=$rc"; tail -3 $OUT/pytest.log
 [ $rc -eq 0 ] || exit $rc
 for v in 1 0 1 h; do
   H=1; Q=$v; [ $v = h ] && { H=0; Q=1; }
