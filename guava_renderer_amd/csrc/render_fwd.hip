@@ -55,6 +55,9 @@ namespace gsr {
 #ifndef GSR_BATCH_NSLOT
 #define GSR_BATCH_NSLOT 3  // pipeline slots of the batched (throughput) kernels
 #endif
+#ifndef GSR_FILL16
+#define GSR_FILL16 1  // empty tiles as 16-byte stores (0: per-strip dword stores, the round-2 form; PMC A/B)
+#endif
 
 typedef float floatx16 __attribute__((ext_vector_type(16)));
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
@@ -367,7 +370,7 @@ __device__ __forceinline__ void render_fwd_body(const Dims& d, const Inputs& in,
             const int t = tile_g - b * d.T;
             const floatx16 unused = {};
             if (ABL == 8) {  /* timing ablation: no empty-tile stores */
-            } else if (!REFINE && (d.W & 3) == 0 && ((reinterpret_cast<uintptr_t>(o.out_color) |
+            } else if (GSR_FILL16 && !REFINE && (d.W & 3) == 0 &&((reinterpret_cast<uintptr_t>(o.out_color) |
                                                       reinterpret_cast<uintptr_t>(o.out_invdepth)) & 15u) == 0 &&
                        (t % d.gx + 1) * GSR_BX <= d.W && (t / d.gx + 1) * GSR_BY <= d.H) {
                 fill_tile(d, im, o, in.bg + in.s_bg * b, b, t % d.gx, t / d.gx, lane);
