@@ -993,9 +993,18 @@ __global__ __launch_bounds__(1024) void k_strip_qscan(Dims d, ImageArena im, uin
     constexpr int kN = 8 * kStripBuckets;  // (queue, bucket) runs, queue-major
     __shared__ uint32_t tot[kN + 1];
     __shared__ uint32_t sh[1024 / 64 + 1];
+    // (frames 8 at a time: eight independent loads in flight per thread instead of a chain of B)
     for (int i = threadIdx.x; i < kN; i += 1024) {
         uint32_t a = 0;
-        for (int f = 0; f < d.B; f++) a += im.strip_hist[(int64_t)f * kN + i];
+        int f = 0;
+        for (; f + 8 <= d.B; f += 8) {
+            uint32_t v[8];
+#pragma unroll
+            for (int u = 0; u < 8; u++) v[u] = im.strip_hist[(int64_t)(f + u) * kN + i];
+#pragma unroll
+            for (int u = 0; u < 8; u++) a += v[u];
+        }
+        for (; f < d.B; f++) a += im.strip_hist[(int64_t)f * kN + i];
         tot[i] = a;
     }
     if (threadIdx.x == 0) tot[kN] = 0;
@@ -1011,7 +1020,18 @@ __global__ __launch_bounds__(1024) void k_strip_qscan(Dims d, ImageArena im, uin
     __syncthreads();
     for (int i = threadIdx.x; i < kN; i += 1024) {
         uint32_t run = tot[i];
-        for (int f = 0; f < d.B; f++) {
+        int f = 0;
+        for (; f + 8 <= d.B; f += 8) {
+            uint32_t v[8];
+#pragma unroll
+            for (int u = 0; u < 8; u++) v[u] = im.strip_hist[(int64_t)(f + u) * kN + i];
+#pragma unroll
+            for (int u = 0; u < 8; u++) {
+                im.strip_hist[(int64_t)(f + u) * kN + i] = run;
+                run += v[u];
+            }
+        }
+        for (; f < d.B; f++) {
             uint32_t* h = im.strip_hist + (int64_t)f * kN + i;
             const uint32_t c = *h;
             *h = run;
