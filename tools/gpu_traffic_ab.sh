@@ -5,7 +5,7 @@
 #   fill4 -- empty tiles as per-strip dword stores (guava_renderer_amd/lib/ab/libgsr_fill4.so,
 #            built here by `python tools/build_ab.py fill4 -DGSR_FILL16=0`), the form before 4beb62b;
 #   abl8  -- no empty-tile stores at all (GSR_RENDER_ABLATE=8, timing-only, wrong images);
-#   qt0   -- no quad / half tail (GSR_QUAD_TAIL=0);
+#   qt1   -- the opt-in quad + half tails (GSR_QUAD_TAIL=1);
 #   train -- the config-4 training line twice (render_bwd's counters, unchanged kernel).
 # Summaries: gpurun_out/traffic/<variant>.json (tools/pmc_summary.py).
 set -u
@@ -28,7 +28,7 @@ variant() {  # name pipeline-cmd (env already exported by the caller's subshell)
   python3 - $O/$v.json <<'PY'
 import json, sys
 d = json.load(open(sys.argv[1]))
-for k in ("k_render_fwd", "k_render_bwd", "k_ordered_scatter"):
+for k in ("k_render_fwd", "k_render_fwd_ablate", "k_render_bwd", "k_ordered_scatter"):
     r = d["kernels"].get(k)
     if r:
         print(f"  {d['config']:7s} {k:18s} fetch {r['fetch_bytes']/1e6:8.1f} MB  write {r['write_bytes']/1e6:8.1f} MB  launches {r['launches']}")
@@ -37,7 +37,7 @@ PY
 ( variant base $A ) || exit 1
 ( export GSR_LIB=guava_renderer_amd/lib/ab/libgsr_fill4.so; variant fill4 $A ) || exit 1
 ( export GSR_RENDER_ABLATE=8; variant abl8 $A ) || exit 1
-( export GSR_QUAD_TAIL=0; variant qt0 $A ) || exit 1
+( export GSR_QUAD_TAIL=1; variant qt1 $A ) || exit 1
 ( variant base2 $A ) || exit 1
 ( variant train $T ) || exit 1
 ( variant train2 $T ) || exit 1
