@@ -1154,7 +1154,7 @@ __device__ __forceinline__ void render_fwd_body(const Dims& d, const Inputs& in,
 template <bool EXACT, bool STATS, bool TL, int SPLIT = 0, int NSLOT = GSR_BATCH_NSLOT, bool HALF = false,
           bool QUAD = false, bool QONLY = false, bool HTAIL = false>
 __global__ __launch_bounds__(GSR_TILE_PIX)
-__attribute__((amdgpu_waves_per_eu(QONLY ? GSR_QONLY_WPE : (NSLOT == 5 && !HALF) ? 3 : GSR_RENDER_WPE))) void k_render_fwd(
+__attribute__((amdgpu_waves_per_eu(QONLY ? GSR_QONLY_WPE : (NSLOT == 5 && !HALF && GSR_BATCH_NSLOT != 5) ? 3 : GSR_RENDER_WPE))) void k_render_fwd(
     Dims d, Inputs in, GeomArena g, ImageArena im, BinArena bn, Outputs o) {
     render_fwd_body<EXACT, STATS, TL, false, 0, SPLIT, NSLOT, HALF, QUAD, QONLY, HTAIL>(d, in, g, im, bn, o);
 }
@@ -1210,12 +1210,16 @@ void launch_render_fwd(const Dims& d, const Inputs& in_, const GeomArena& g, con
     const bool ht = qt && htail;
     const int grid = min((nwaves + 3) / 4, persistent_grid(wg_per_cu));
     const dim3 gr(grid), bl(GSR_TILE_PIX);
+#if GSR_BATCH_NSLOT == 3  /* (the tails follow the three-slot pipeline) */
 #define GSR_LAUNCH(E, S, L)                                                                                   \
     {                                                                                                         \
-        if (ht) hipLaunchKernelGGL((k_render_fwd<E, S, L, 0, GSR_BATCH_NSLOT, false, true, false, true>), gr, bl, 0, s, d, in, g, im, b, o); \
-        else if (qt) hipLaunchKernelGGL((k_render_fwd<E, S, L, 0, GSR_BATCH_NSLOT, false, true>), gr, bl, 0, s, d, in, g, im, b, o); \
+        if (ht) hipLaunchKernelGGL((k_render_fwd<E, S, L, 0, 3, false, true, false, true>), gr, bl, 0, s, d, in, g, im, b, o); \
+        else if (qt) hipLaunchKernelGGL((k_render_fwd<E, S, L, 0, 3, false, true>), gr, bl, 0, s, d, in, g, im, b, o); \
         else hipLaunchKernelGGL((k_render_fwd<E, S, L>), gr, bl, 0, s, d, in, g, im, b, o);                  \
     }
+#else
+#define GSR_LAUNCH(E, S, L) { (void)ht; (void)qt; hipLaunchKernelGGL((k_render_fwd<E, S, L>), gr, bl, 0, s, d, in, g, im, b, o); }
+#endif
     if (o.stats) {
         if (exact) GSR_LAUNCH(true, true, false) else GSR_LAUNCH(false, true, false)
     }
