@@ -286,7 +286,8 @@ class Workload:
             self.rasts = [BatchRasterizer(B, P, W, H, R_capacity=int(R_probe * 1.25) + 1024, device=dev,
                                           numerics=numerics) for _ in range(max(1, a.inflight))]
             rasts = self.rasts
-            self.step_on = lambda i: rasts[i].forward(means, colors, opac, scales, rots, views, projs, tanf, bgs)
+            self.step_on = lambda i: rasts[i].forward(means, colors, opac, scales, rots, views, projs, tanf, bgs,
+                                                      forward_only=True)
         self.rast = self.rasts[0] if self.rasts else None
 
     def _frame_pipeline(self, dpipe, numerics):

@@ -18,6 +18,7 @@ EXPORTS = ("gsr_version", "gsr_last_error", "gsr_geometry_bytes",
            "gsr_refine_prepare", "gsr_batch_status_offset", "gsr_frames_to8b",
            # include/gsr_deform.h
            "gsr_lbs_workspace_bytes", "gsr_lbs", "gsr_lbs_sp", "gsr_blend_joints", "gsr_blend_joints_sp",
+           "gsr_lbs_tiled_floats", "gsr_lbs_tile_bases",
            "gsr_splice_head",
            "gsr_pack_rows", "gsr_deform_gaussians",
            # include/gsr_ssim.h
@@ -27,6 +28,8 @@ EXPORTS = ("gsr_version", "gsr_last_error", "gsr_geometry_bytes",
 NUMERICS_EXACT = 0
 NUMERICS_FAST_EXP = 1
 NUMERICS_SPLIT_BF16 = 2
+# same flag word, batched forward only: no backward will read the workspace (include/gsr.h)
+FORWARD_ONLY = 0x100
 
 
 def numerics(fast_exp=False, split_bf16=False):
@@ -61,7 +64,8 @@ class RowSegment(ctypes.Structure):
 class LbsSparse(ctypes.Structure):
     """GsrLbsSparse (include/gsr_deform.h)."""
     _fields_ = [("jreg_row", _vp), ("jreg_col", _vp), ("jreg_val", _vp), ("skin_k", ctypes.c_int32),
-                ("pad_", ctypes.c_int32), ("skin_joint", _vp), ("skin_weight", _vp)]
+                ("pad_", ctypes.c_int32), ("skin_joint", _vp), ("skin_weight", _vp),
+                ("shapedirs_tiled", _vp), ("posedirs_tiled", _vp)]
 
 
 class GsrError(RuntimeError):
@@ -157,6 +161,10 @@ def load(path=None):
     L.gsr_frames_to8b.restype = _i
     L.gsr_lbs_workspace_bytes.argtypes = [_i, _i, _i, _i]
     L.gsr_lbs_workspace_bytes.restype = _sz
+    L.gsr_lbs_tiled_floats.argtypes = [_i, _i]
+    L.gsr_lbs_tiled_floats.restype = _sz
+    L.gsr_lbs_tile_bases.argtypes = [_i, _i, _vp, _vp, _vp]
+    L.gsr_lbs_tile_bases.restype = _i
     L.gsr_lbs.argtypes = [_i, _i, _i, _i, _vp, _i64, _vp, _vp, _vp, _i, _vp, _vp, _vp, _vp, _vp, _vp,
                           _vp, _vp, _vp, _vp, _vp, _vp, _vp]
     L.gsr_lbs.restype = _i

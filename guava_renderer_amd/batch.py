@@ -159,12 +159,18 @@ class BatchRasterizer:
         return self._overflow
 
     def forward(self, means3D, colors, opacities, scales, rotations, viewmatrices, projmatrices,
-                tanfov, backgrounds, scale_modifier=1.0, antialiasing=False, refine=None, numerics=None):
+                tanfov, backgrounds, scale_modifier=1.0, antialiasing=False, refine=None, numerics=None,
+                forward_only=False):
         """Render B frames.  refine: optional RefineHead -- the refiner's first 1x1 conv + leaky ReLU
         fused into the render epilogue (include/gsr.h gsr_refine_epilogue); its output is
-        refine.out [B,n_out,H,W] and only out_color[:, :refine.keep_channels] is written."""
+        refine.out [B,n_out,H,W] and only out_color[:, :refine.keep_channels] is written.
+        forward_only: no backward() will follow (inference; include/gsr.h GSR_FORWARD_ONLY): the
+        workspace skips the rows only the backward reads; the images are the same."""
         self.poll()
         nm = self.numerics if numerics is None else int(numerics)
+        if forward_only:
+            nm |= _lib.FORWARD_ONLY
+        self._fwd_only = bool(forward_only)
         keep, head, (v, pm, tf, bg, bs) = self._inputs(means3D, colors, opacities, scales, rotations,
                                                        viewmatrices, projmatrices, tanfov, backgrounds)
         args = head + (float(scale_modifier), v, pm, tf, bg, bs, self.workspace.data_ptr(), self.R_capacity,
@@ -197,6 +203,8 @@ class BatchRasterizer:
         attribute gradients summed over the frames instead, dict of [P,k] tensors (means3D, colors,
         opacity, scales, rotations) -- gsr_backward_batch_shared, no [B,P,k] buffers."""
         B, P = self.B, self.P
+        if getattr(self, "_fwd_only", False):
+            raise _lib.GsrError("backward after forward(forward_only=True): the workspace holds no backward rows")
         nm = self.numerics if numerics is None else int(numerics)
         o = dict(dtype=torch.float32, device=self.device)
         keep, head, (v, pm, tf, bg, bs) = self._inputs(means3D, colors, opacities, scales, rotations,

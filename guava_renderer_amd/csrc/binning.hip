@@ -817,10 +817,13 @@ __global__ __launch_bounds__(kSlots) __attribute__((amdgpu_waves_per_eu(6))) voi
             const int64_t gid = (int64_t)b * d.P + gi;
             r = g.rect[gid];
             nt = ((r.y & 0xFFFF) - (r.x & 0xFFFF)) * ((r.y >> 16) - (r.x >> 16));
-            const float4 co = g.conic[gid];
+            // conic, opacity and mean from the render record (exact: its conic words are the conic
+            // times -1/2 and -1, powers of two), so a GSR_FORWARD_ONLY preprocess need not write them
+            const float4 r0 = g.rrec[2 * gid], r1 = g.rrec[2 * gid + 1];
+            const float4 co = make_float4(-2.0f * r1.x, -r1.y, -2.0f * r1.z, r0.z);
             s_co[tid] = co;
             s_pre[tid] = strip_pre(co);
-            s_m[tid] = g.means2D[gid];
+            s_m[tid] = make_float2(r0.x, r0.y);
         }
         uint32_t total;
         s_pref[tid] = block_excl_scan<uint32_t, kSlots>(nt, &total, s_sh) + nt;  // (barriers inside)

@@ -72,6 +72,7 @@ struct StageTimer {
 inline bool exact_exp(uint32_t numerics) { return (numerics & GSR_NUMERICS_FAST_EXP) == 0; }
 inline bool split_bf16(uint32_t numerics) { return (numerics & GSR_NUMERICS_SPLIT_BF16) != 0; }
 constexpr uint32_t kNumericsKnown = GSR_NUMERICS_FAST_EXP | GSR_NUMERICS_SPLIT_BF16;
+constexpr uint32_t kForwardBatchKnown = kNumericsKnown | GSR_FORWARD_ONLY;
 
 inline size_t align_up(size_t x) { return (x + 255) & ~(size_t)255; }
 inline size_t ctrl_words(const Dims& d) { return (size_t)kCtrlWords + (size_t)kFsWords * d.B; }
@@ -488,7 +489,7 @@ int gsr_forward_batch_refine(int B, int P, int width, int height, const float* m
                              int* radii, int antialiasing, const gsr_refine_epilogue* refine,
                              uint32_t numerics, void* stream) {
     hipStream_t s = (hipStream_t)stream;
-    if (numerics & ~kNumericsKnown) return fail(GSR_ERR_ARG, "unknown numerics flags");
+    if (numerics & ~kForwardBatchKnown) return fail(GSR_ERR_ARG, "unknown numerics flags");
     if (refine) {
         if (!refine->out_refine || refine->n_out < 1 || refine->keep_channels < 0 ||
             refine->keep_channels + refine->n_out > GSR_C)
@@ -520,6 +521,7 @@ int gsr_forward_batch_refine(int B, int P, int width, int height, const float* m
     in.bg = backgrounds; in.s_bg = bg_stride;
     in.scale_mod = scale_modifier;
     in.prefiltered = 0; in.antialiasing = antialiasing;
+    in.fwd_only = (numerics & GSR_FORWARD_ONLY) != 0;
     Outputs o{out_color, out_invdepth, radii, g_render_counters, g_timeline, g_timeline_cap};
     if (refine) {
         o.rb = refine->bias;

@@ -278,10 +278,150 @@ __global__ __launch_bounds__(256) void k_lbs_blend_mfma(int B, int M, int NB, in
     }
 }
 
+// ---- tiled bases (GsrLbsSparse.shapedirs_tiled / posedirs_tiled, include/gsr_deform.h)
+// A base [K][M] re-laid once per avatar as 1-KB tiles of 32 coordinates x 8 k: tile (t, g) holds, as
+// float4 (t * nkg + g) * 64 + 32 h + c, component j, the value base[8g + 4h + j][32t + c] (K padded to
+// a multiple of 8, M to 32, with zeros).  Every load is then one fully coalesced 16-byte-per-lane
+// wave read (1 KB), where the k-major layout gives 4-byte lanes (256 B per load instruction): the
+// blend's bases stream at HBM rate with a quarter of the load instructions in flight.
+constexpr int kTiledUnroll = 4;  // tile groups whose loads are issued before their products
+
+// D[frame][m] over the k of one base: v_mfma_f32_32x32x2_f32 with lane (c, h) holding base[8g + 4h + j]
+// [32t + c] (B operand) and coef[frame b0 + c][8g + 4h + j] (A operand) for the j-th MFMA of a group
+// (the lane halves' k of one MFMA are 8g + j and 8g + 4 + j); wave w takes the groups g = w mod 4.
+__device__ __forceinline__ void blend_tiled_mfma_part(floatx16& acc, const float* __restrict__ coef, int ncoef,
+                                                      const float4* __restrict__ tb, int K, int t, int bA,
+                                                      bool bok, int w, int hi, int lane) {
+    const int nkg = (K + 7) / 8;
+    const float4* __restrict__ p = tb + (int64_t)t * nkg * 64 + lane;
+    const float* __restrict__ cr = coef + (int64_t)bA * ncoef;
+    for (int g0 = w; g0 < nkg; g0 += 4 * kTiledUnroll) {
+        float4 v[kTiledUnroll];
+        float a[kTiledUnroll][4];
+#pragma unroll
+        for (int u = 0; u < kTiledUnroll; u++) {
+            const int g = g0 + 4 * u;
+            v[u] = g < nkg ? p[(int64_t)g * 64] : make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+            for (int j = 0; j < 4; j++) {
+                const int k = 8 * g + 4 * hi + j;
+                a[u][j] = (bok && k < K) ? cr[k] : 0.f;
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < kTiledUnroll; u++) {
+            acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a[u][0], v[u].x, acc, 0, 0, 0);
+            acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a[u][1], v[u].y, acc, 0, 0, 0);
+            acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a[u][2], v[u].z, acc, 0, 0, 0);
+            acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a[u][3], v[u].w, acc, 0, 0, 0);
+        }
+    }
+}
+
+// k_lbs_blend_mfma over the tiled bases: one workgroup per 32 coordinates x 32 frames, the same
+// wave-order reduction and epilogue.
+__global__ __launch_bounds__(256) void k_lbs_blend_tiled(int B, int M, int NB, int NP,
+                                                         const float* __restrict__ vt, int64_t vt_stride,
+                                                         const float* __restrict__ betas,
+                                                         const float4* __restrict__ sd_tiled,
+                                                         const float* __restrict__ feat,
+                                                         const float4* __restrict__ pd_tiled,
+                                                         float* __restrict__ v_shaped,
+                                                         float* __restrict__ v_posed) {
+    __shared__ float red[4][2][16][64];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, hi = lane >> 5, l32 = lane & 31;
+    const int t = blockIdx.x, m0 = t * 32, b0 = blockIdx.y * 32;
+    const int m = m0 + l32, bA = b0 + l32;
+    const bool mok = m < M, bok = bA < B;
+    floatx16 as, ap;
+#pragma unroll
+    for (int r = 0; r < 16; r++) { as[r] = 0.f; ap[r] = 0.f; }
+    if (NB > 0) blend_tiled_mfma_part(as, betas, NB, sd_tiled, NB, t, bA, bok, w, hi, lane);
+    if (NP > 0 && v_posed) blend_tiled_mfma_part(ap, feat, NP, pd_tiled, NP, t, bA, bok, w, hi, lane);
+#pragma unroll
+    for (int r = 0; r < 16; r++) {
+        red[w][0][r][lane] = as[r];
+        red[w][1][r][lane] = ap[r];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+        const int r = 4 * w + i;
+        const int b = b0 + (r & 3) + 8 * (r >> 2) + 4 * hi;
+        if (!mok || b >= B) continue;
+        float S = red[0][0][r][lane], Pz = red[0][1][r][lane];
+#pragma unroll
+        for (int u = 1; u < 4; u++) { S += red[u][0][r][lane]; Pz += red[u][1][r][lane]; }
+        const float tv = vt[(int64_t)b * vt_stride + m];
+        const float vs = NB > 0 ? tv + S : tv;
+        v_shaped[(int64_t)b * M + m] = vs;
+        if (v_posed) v_posed[(int64_t)b * M + m] = Pz + vs;
+    }
+}
+
+// One frame over the tiled bases (the per-frame drop-in path): lane (c, h) of wave w sums
+// coef[8g + 4h + j] base[8g + 4h + j][32t + c] over its groups g = w mod 4 (four fmaf per 16-byte
+// load), then the two lane halves and the four waves are added in a fixed order through LDS.
+__device__ __forceinline__ float blend_tiled_one(const float* __restrict__ coef, const float4* __restrict__ tb,
+                                                 int K, int t, int w, int hi, int lane) {
+    const int nkg = (K + 7) / 8;
+    const float4* __restrict__ p = tb + (int64_t)t * nkg * 64 + lane;
+    float acc = 0.f;
+    for (int g0 = w; g0 < nkg; g0 += 4 * kTiledUnroll) {
+        float4 v[kTiledUnroll];
+        float a[kTiledUnroll][4];
+#pragma unroll
+        for (int u = 0; u < kTiledUnroll; u++) {
+            const int g = g0 + 4 * u;
+            v[u] = g < nkg ? p[(int64_t)g * 64] : make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+            for (int j = 0; j < 4; j++) {
+                const int k = 8 * g + 4 * hi + j;
+                a[u][j] = k < K ? coef[k] : 0.f;
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < kTiledUnroll; u++) {
+            acc = fmaf(a[u][0], v[u].x, acc);
+            acc = fmaf(a[u][1], v[u].y, acc);
+            acc = fmaf(a[u][2], v[u].z, acc);
+            acc = fmaf(a[u][3], v[u].w, acc);
+        }
+    }
+    return acc;
+}
+
+__global__ __launch_bounds__(256) void k_lbs_blend_tiled1(int M, int NB, int NP, const float* __restrict__ vt,
+                                                          const float* __restrict__ betas,
+                                                          const float4* __restrict__ sd_tiled,
+                                                          const float* __restrict__ feat,
+                                                          const float4* __restrict__ pd_tiled,
+                                                          float* __restrict__ v_shaped,
+                                                          float* __restrict__ v_posed) {
+    __shared__ float red[2][4][64];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, hi = lane >> 5, l32 = lane & 31;
+    const int t = blockIdx.x, m = t * 32 + l32;
+    red[0][w][lane] = NB > 0 ? blend_tiled_one(betas, sd_tiled, NB, t, w, hi, lane) : 0.f;
+    red[1][w][lane] = (NP > 0 && v_posed) ? blend_tiled_one(feat, pd_tiled, NP, t, w, hi, lane) : 0.f;
+    __syncthreads();
+    if (w == 0 && hi == 0 && m < M) {
+        float S = 0.f, Pz = 0.f;
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            S += red[0][u][l32] + red[0][u][l32 + 32];
+            Pz += red[1][u][l32] + red[1][u][l32 + 32];
+        }
+        const float vs = NB > 0 ? vt[m] + S : vt[m];
+        v_shaped[m] = vs;
+        if (v_posed) v_posed[m] = Pz + vs;
+    }
+}
+
 // blend launcher: the matrix-core kernel for more than kLbsFrames frames, the streaming one otherwise
+// (tiled bases, when the caller prepared them: B > kLbsFrames and B = 1)
 static void launch_blend(int B, int M, int NB, int NP, const float* vt, int64_t vt_stride, const float* betas,
                          const float* sd_t, const float* feat, const float* pd, float* vs, float* vp,
-                         hipStream_t s);
+                         hipStream_t s, const GsrLbsSparse* sp = nullptr);
 
 static size_t lbs_blend_lds(int NB, int NP, int nf, int split) {
     const size_t coef = sizeof(float) * (size_t)(NB + NP) * nf;
@@ -302,11 +442,29 @@ static void lbs_blend_attr(size_t lds) {
 
 static void launch_blend(int B, int M, int NB, int NP, const float* vt, int64_t vt_stride, const float* betas,
                          const float* sd_t, const float* feat, const float* pd, float* vs, float* vp,
-                         hipStream_t s) {
+                         hipStream_t s, const GsrLbsSparse* sp) {
     static const bool valu_only = [] {  // timing A/B only
         const char* e = getenv("GSR_BLEND_VALU");
         return e && e[0] == '1';
     }();
+    static const bool tiled_on = [] {  // GSR_BLEND_TILED=0: the k-major kernels even with tiled bases (A/B)
+        const char* e = getenv("GSR_BLEND_TILED");
+        return !(e && e[0] == '0');
+    }();
+    const bool tiled = tiled_on && sp && (NB == 0 || sp->shapedirs_tiled) &&
+                       (NP == 0 || !vp || sp->posedirs_tiled) && (NB > 0 || (NP > 0 && vp));
+    if (tiled && B > kLbsFrames && !valu_only) {
+        hipLaunchKernelGGL(k_lbs_blend_tiled, dim3((M + 31) / 32, (B + 31) / 32), dim3(256), 0, s, B, M, NB,
+                           vp ? NP : 0, vt, vt_stride, betas, reinterpret_cast<const float4*>(sp->shapedirs_tiled),
+                           feat, reinterpret_cast<const float4*>(sp->posedirs_tiled), vs, vp);
+        return;
+    }
+    if (tiled && B == 1) {
+        hipLaunchKernelGGL(k_lbs_blend_tiled1, dim3((M + 31) / 32), dim3(256), 0, s, M, NB, vp ? NP : 0, vt, betas,
+                           reinterpret_cast<const float4*>(sp->shapedirs_tiled), feat,
+                           reinterpret_cast<const float4*>(sp->posedirs_tiled), vs, vp);
+        return;
+    }
     if (B > kLbsFrames && !valu_only) {
         hipLaunchKernelGGL(k_lbs_blend_mfma, dim3((M + 31) / 32, (B + 31) / 32), dim3(256), 0, s, B, M, NB,
                            vp ? NP : 0, vt, vt_stride, betas, sd_t, feat, pd, vs, vp);
@@ -845,6 +1003,22 @@ int hip_check(const char* what) {
 
 using namespace gsr;
 
+// The tiled layout of a k-major base (GsrLbsSparse.*_tiled): one float4 per thread.
+__global__ __launch_bounds__(256) void k_lbs_tile_base(int K, int M, int64_t n4, const float* __restrict__ base,
+                                                       float4* __restrict__ tiled) {
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= n4) return;
+    const int nkg = (K + 7) / 8;
+    const int lane = (int)(i & 63);
+    const int64_t tg = i >> 6;
+    const int g = (int)(tg % nkg), t = (int)(tg / nkg);
+    const int m = 32 * t + (lane & 31), k0 = 8 * g + 4 * (lane >> 5);
+    float v[4];
+#pragma unroll
+    for (int j = 0; j < 4; j++) v[j] = (m < M && k0 + j < K) ? base[(int64_t)(k0 + j) * M + m] : 0.f;
+    tiled[i] = make_float4(v[0], v[1], v[2], v[3]);
+}
+
 extern "C" {
 
 size_t gsr_lbs_workspace_bytes(int B, int V, int J, int NB) {
@@ -873,6 +1047,8 @@ int check_sparse(const GsrLbsSparse* sp, int J, const char* who) {
         return api_fail(GSR_ERR_ARG, (std::string(who) + ": jreg_row without jreg_col / jreg_val").c_str());
     if (sp->skin_k && (sp->skin_k < 0 || sp->skin_k > GSR_LBS_SKIN_MAX_K || !sp->skin_joint || !sp->skin_weight))
         return api_fail(GSR_ERR_ARG, (std::string(who) + ": skin_k must be in [1, 16] with its arrays").c_str());
+    if (((uintptr_t)sp->shapedirs_tiled | (uintptr_t)sp->posedirs_tiled) & 15)
+        return api_fail(GSR_ERR_ARG, (std::string(who) + ": tiled bases must be 16-byte aligned").c_str());
     (void)J;
     return 0;
 }
@@ -932,7 +1108,7 @@ int gsr_lbs_sp(int B, int V, int J, int NB, const float* v_template, int64_t v_t
                        pose2rot, a.rot, a.feat);
     if (int rc = hip_check("lbs_rodrigues")) return rc;
     if (lbs_blend_lds(NB, NP, kLbsFrames, kLbsSplit) > 160 * 1024) return api_fail(GSR_ERR_ARG, "gsr_lbs: NB + 9(J-1) too large for LDS");
-    launch_blend(B, M, NB, NP, v_template, v_template_stride, betas, shapedirs_t, a.feat, posedirs, vs, a.vp, s);
+    launch_blend(B, M, NB, NP, v_template, v_template_stride, betas, shapedirs_t, a.feat, posedirs, vs, a.vp, s, sp);
     if (int rc = hip_check("lbs_blend")) return rc;
     launch_joints(B, V, J, J_regressor, sp, vs, joints_offset, jr, s);
     if (int rc = hip_check("lbs_joints")) return rc;
@@ -979,10 +1155,24 @@ int gsr_blend_joints_sp(int B, int V, int J, int NB, const float* v_template, in
     if (lbs_blend_lds(NB, 0, kLbsFrames, kLbsSplit) > 160 * 1024) return api_fail(GSR_ERR_ARG, "gsr_blend_joints: NB too large for LDS");
     hipStream_t s = (hipStream_t)stream;
     const int M = V * 3;
-    launch_blend(B, M, NB, 0, v_template, v_template_stride, betas, shapedirs_t, nullptr, nullptr, v_shaped, nullptr, s);
+    launch_blend(B, M, NB, 0, v_template, v_template_stride, betas, shapedirs_t, nullptr, nullptr, v_shaped, nullptr, s, sp);
     if (int rc = hip_check("blend_shapes")) return rc;
     launch_joints(B, V, J, J_regressor, sp, v_shaped, joints_offset, joints, s);
     return hip_check("vertices2joints");
+}
+
+size_t gsr_lbs_tiled_floats(int K, int M) {
+    if (K <= 0 || M <= 0) return 0;
+    return (size_t)((M + 31) / 32) * (size_t)((K + 7) / 8) * 256;
+}
+
+int gsr_lbs_tile_bases(int K, int M, const float* base, float* tiled, void* stream) {
+    if (K <= 0 || M <= 0 || !base || !tiled) return api_fail(GSR_ERR_ARG, "gsr_lbs_tile_bases: bad arguments");
+    if (((uintptr_t)tiled & 15) != 0) return api_fail(GSR_ERR_ARG, "gsr_lbs_tile_bases: tiled must be 16-byte aligned");
+    const int64_t n4 = (int64_t)gsr_lbs_tiled_floats(K, M) / 4;
+    hipLaunchKernelGGL(k_lbs_tile_base, dim3((unsigned)((n4 + 255) / 256)), dim3(256), 0, (hipStream_t)stream, K, M,
+                       n4, base, reinterpret_cast<float4*>(tiled));
+    return hip_check("lbs_tile_base");
 }
 
 int gsr_splice_head(int B, int V_body, int N_head, const int32_t* head_index, const float* head_verts,

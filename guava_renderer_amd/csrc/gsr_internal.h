@@ -43,6 +43,7 @@ enum Ctrl : int {
     kCtrlRenderHead = 4, // render worklist dequeue counter
     kCtrlBwdHead = 5,    // render-backward worklist dequeue counter
     kCtrlNonEmpty = 6,   // tiles of the batch with a non-empty list
+    kCtrlFwdOnly = 7,    // set by a GSR_FORWARD_ONLY forward: the backward-only rows were not written
     kCtrlQStart = 16,    // queue map 2: first strip_list tile of each XCD queue (8 words), then
                          // the queue's tile count (8 words)
     kCtrlXcdQueue = 1024,  // 8 per-XCD render dequeue counters, 4 KiB apart
@@ -175,6 +176,7 @@ struct Inputs {
     const float* bg; int64_t s_bg;
     float scale_mod;
     int prefiltered, antialiasing;
+    int fwd_only;         // GSR_FORWARD_ONLY: preprocess writes only what binning and compositing read
     uint32_t xcd_map;     // render work-queue mapping (queue_item): 1 = tile-affine (strip order tile-major)
 };
 

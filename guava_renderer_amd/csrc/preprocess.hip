@@ -62,8 +62,9 @@ __global__ __launch_bounds__(kScanBlock) void k_preprocess(Dims d, Inputs in, Ge
                 const float sc[3] = {sp[0], sp[1], sp[2]};
                 const float q[4] = {rp[0], rp[1], rp[2], rp[3]};
                 cov3d_fwd(sc, in.scale_mod, q, c3);
+                if (!in.fwd_only)
 #pragma unroll
-                for (int k = 0; k < 6; k++) g.cov3D[6 * gid + k] = c3[k];
+                    for (int k = 0; k < 6; k++) g.cov3D[6 * gid + k] = c3[k];
             }
             // computeCov2D (forward.cu:74-109)
             float t[3];
@@ -106,9 +107,11 @@ __global__ __launch_bounds__(kScanBlock) void k_preprocess(Dims d, Inputs in, Ge
                 if (nt != 0) {
                     const float op = in.opac[in.s_opac * b + i];
                     g.depth[gid] = pv[2];
-                    g.invdepth[gid] = 1.0f / pv[2];
-                    g.means2D[gid] = make_float2(pix0, pix1);
-                    g.conic[gid] = make_float4(conic0, conic1, conic2, op * h_conv);
+                    if (!in.fwd_only) {  // (rows read by the backward only; binning reads the record)
+                        g.invdepth[gid] = 1.0f / pv[2];
+                        g.means2D[gid] = make_float2(pix0, pix1);
+                        g.conic[gid] = make_float4(conic0, conic1, conic2, op * h_conv);
+                    }
                     radius = ir;
                     tiles = nt;
                     rect = make_uint2(rmin[0] | (rmin[1] << 16), rmax[0] | (rmax[1] << 16));
@@ -120,7 +123,7 @@ __global__ __launch_bounds__(kScanBlock) void k_preprocess(Dims d, Inputs in, Ge
                 }
             }
         }
-        g.radii[gid] = radius;
+        if (!in.fwd_only) g.radii[gid] = radius;
         g.tiles[gid] = tiles;
         g.rect[gid] = rect;
         if (o.radii) o.radii[gid] = radius;
@@ -143,6 +146,7 @@ __global__ __launch_bounds__(kScanBlock) void k_preprocess(Dims d, Inputs in, Ge
     }
     __syncthreads();
     if (threadIdx.x == 0) {
+        if (in.fwd_only && blockIdx.x == 0 && b == 0) g.ctrl[kCtrlFwdOnly] = 1u;
         uint32_t s = 0, km = 0, nkm = 0;
 #pragma unroll
         for (int w = 0; w < kScanBlock / 64; w++) {

@@ -191,7 +191,7 @@ __device__ __forceinline__ bool preprocess_bwd_frame(const Dims& d, const Inputs
 // frame order and writes each attribute gradient once -- no [B][P][k] buffers and no separate sum.
 __global__ __launch_bounds__(kScanBlock) void k_preprocess_bwd(Dims d, Inputs in, GeomArena g, Grads gr) {
     const int i = blockIdx.x * kScanBlock + threadIdx.x;
-    if (i >= d.P) return;
+    if (i >= d.P || g.ctrl[kCtrlFwdOnly]) return;  // (a GSR_FORWARD_ONLY workspace: no backward rows)
     const bool geo = in.scales && in.rot && gr.dL_dscale && gr.dL_drot;
     if (!gr.reduce) {
         const int b = blockIdx.y;

@@ -71,7 +71,7 @@ template <bool EXACT, bool INVD, int SPLIT = 0, int ABL = 0>
 __global__ __launch_bounds__(GSR_TILE_PIX) __attribute__((amdgpu_waves_per_eu(2))) void k_render_bwd(
     Dims d, Inputs in, GeomArena g, ImageArena im, BinArena bn, Grads gr) {
     __shared__ float lds_all[(GSR_TILE_PIX / 64) * kBwdLdsWave];
-    if (g.ctrl[kCtrlOverflow]) return;
+    if (g.ctrl[kCtrlOverflow] || g.ctrl[kCtrlFwdOnly]) return;
     const uint32_t ne = g.ctrl[kCtrlNonEmpty];
     const int lane = threadIdx.x & 63;
     float* wl = lds_all + (threadIdx.x >> 6) * kBwdLdsWave;  // w tile [slot][pixel]

@@ -249,6 +249,18 @@ def _host(x):
     return x.detach().cpu().numpy() if torch.is_tensor(x) else np.asarray(x)
 
 
+def tile_base(base_kmajor, stream=None):
+    """The 1-KB tiled layout of a k-major blend-shape base [K, M] on the device (gsr_lbs_tile_bases,
+    include/gsr_deform.h GsrLbsSparse.*_tiled), for 16-byte loads in the blend kernels."""
+    K, M = base_kmajor.shape
+    L = _lib.load()
+    out = torch.empty((int(L.gsr_lbs_tiled_floats(K, M)),), dtype=torch.float32, device=base_kmajor.device)
+    b = base_kmajor.contiguous()
+    _lib.check(L.gsr_lbs_tile_bases(K, M, b.data_ptr(), out.data_ptr(), stream or _stream(base_kmajor.device)),
+               "gsr_lbs_tile_bases")
+    return out
+
+
 def sparse_lbs_assets(J_regressor, lbs_weights, device):
     """GsrLbsSparse (include/gsr_deform.h) of one model's dense assets, built once on the host: the
     J_regressor's nonzeros as CSR rows (vertex order) and, when every vertex has at most 16 nonzero
@@ -305,6 +317,13 @@ class EHMDeformer:
         if os.environ.get("GSR_LBS_SPARSE", "1") != "0":
             for name, a in (("body", body), ("flame", flame)):
                 self.sparse[name] = sparse_lbs_assets(a["J_regressor"], a["lbs_weights"], dev)
+        # the blend-shape bases as 16-byte tiles (GSR_BLEND_TILED=0 in the library: the k-major kernels)
+        for name, a in (("body", self.body), ("flame", self.flame)):
+            if name in self.sparse:
+                sp, keep = self.sparse[name]
+                tl = [tile_base(x) if x.numel() else None for x in (a["shapedirs_t"], _f32(a["posedirs"]))]
+                keep += tl
+                sp.shapedirs_tiled, sp.posedirs_tiled = (x.data_ptr() if x is not None else None for x in tl)
         self.head_index = t(np.asarray(smplx2flame_ind, np.int32))
         self.l_eyelid, self.r_eyelid = t(np.asarray(l_eyelid, np.float32)), t(np.asarray(r_eyelid, np.float32))
         self.bad = torch.zeros(1, dtype=torch.int32, device=dev)

@@ -49,5 +49,5 @@ class AvatarPipeline:
         d = self.deform(body_params, flame_params)
         col, inv, radii = self.rast.forward(d["xyz"], self.gauss.colors, self.gauss.opacity,
                                             d["scaling"], d["rotation"], views, projs, tanfov, self.bg,
-                                            refine=refine)
+                                            refine=refine, forward_only=True)
         return col, inv, radii, d

@@ -67,6 +67,14 @@ const char* gsr_last_error(void);
 #define GSR_NUMERICS_EXACT 0u
 #define GSR_NUMERICS_FAST_EXP 1u
 #define GSR_NUMERICS_SPLIT_BF16 2u
+/* Not numerics, in the same flag word of gsr_forward_batch / gsr_forward_batch_refine:
+ * GSR_FORWARD_ONLY -- no backward will read this call's workspace (inference: main/test.py,
+ * render_motion.py).  Preprocess then writes only what binning and compositing read (depth, render
+ * record, tile rect and count; plus the caller's radii) and skips the rows kept for the backward
+ * (cov3D, means2D, conic, inverse depth, radii in the workspace): 56 of 108 bytes per visible
+ * Gaussian.  Images are unchanged.  A gsr_backward_batch* on such a workspace computes nothing and
+ * its gradients stay as the caller zeroed them (the Python mirror raises first). */
+#define GSR_FORWARD_ONLY 0x100u
 
 /* Scratch sizes used by gsr_forward (the three resizer requests).  Unlike the reference's
  * GeometryState, the geometry arena also holds the per-frame depth sort and the (depth chunk x tile)

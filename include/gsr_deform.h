@@ -72,7 +72,12 @@ int gsr_lbs(int B, int V, int J, int NB, const float* v_template, int64_t v_temp
  *   re-associated (per-lane chains + a fixed tree), deterministic run to run.
  *   skin_k in [1, 16] (0: the dense lbs_weights_t), skin_joint / skin_weight [skin_k, V]: per vertex
  *   its nonzero (joint, weight) pairs in increasing joint order, padded with weight 0 -- the dense
- *   skinning's fmaf chains minus their zero terms, so the vertices and transforms are identical. */
+ *   skinning's fmaf chains minus their zero terms, so the vertices and transforms are identical.
+ *   shapedirs_tiled / posedirs_tiled (or NULL): the blend-shape bases shapedirs_t [NB][3V] and
+ *   posedirs [9(J-1)][3V] re-laid as 1-KB tiles of 32 coordinates x 8 k for 16-byte loads:
+ *   float4 (t * ceil(K/8) + g) * 64 + 32 h + c, component j = base[8g + 4h + j][32t + c], zero-padded
+ *   to K multiple of 8 and 3V multiple of 32 (gsr_lbs_tile_bases).  Used for B = 1 and B > 16; the
+ *   k sums are re-associated (fixed order, deterministic). */
 typedef struct {
     const int32_t* jreg_row;
     const int32_t* jreg_col;
@@ -81,7 +86,13 @@ typedef struct {
     int32_t pad_;
     const int32_t* skin_joint;
     const float* skin_weight;
+    const float* shapedirs_tiled;
+    const float* posedirs_tiled;
 } GsrLbsSparse;
+/* Floats of a tiled base (GsrLbsSparse.*_tiled) for K x M, and the re-layout of a k-major base
+ * [K][M] (device pointers) into it. */
+size_t gsr_lbs_tiled_floats(int K, int M);
+int gsr_lbs_tile_bases(int K, int M, const float* base, float* tiled, void* stream);
 #define GSR_LBS_SKIN_MAX_K 16
 
 /* gsr_lbs with the sparse assets (sp may be NULL: gsr_lbs). */

@@ -217,3 +217,34 @@ def test_deferred_error_stays_with_its_count():
         int(_C.rasterize_gaussians(*args(False))[0])
     with pytest.raises(RuntimeError, match="prefiltered"):
         int(bad)
+
+
+def test_forward_only_batch_same_images_and_backward_refused():
+    """GSR_FORWARD_ONLY (BatchRasterizer.forward(forward_only=True), the AvatarPipeline's inference
+    call): preprocess skips the rows only the backward reads, binning takes the conic and mean from
+    the render record -- the images, inverse depth, radii and instance count are bit-identical, and
+    a backward on that workspace raises instead of reading stale rows."""
+    from guava_renderer_amd import camera, scenes
+    from guava_renderer_amd._lib import GsrError
+    from guava_renderer_amd.batch import BatchRasterizer
+    B, P, W, H = 3, 12000, 160, 128
+    sc = scenes.avatar_cloud(P, seed=4)
+    t = lambda x: torch.tensor(np.ascontiguousarray(x), device=DEV)  # noqa: E731
+    cams = [camera.camera(W, H, yaw=y, pitch=-0.3 * y) for y in (0.0, 0.4, -0.7)]
+    views = t(np.stack([c["viewmatrix"].reshape(16) for c in cams]))
+    projs = t(np.stack([c["projmatrix"].reshape(16) for c in cams]))
+    tanf = t(np.array([[c["tanfovx"], c["tanfovy"]] for c in cams], np.float32))
+    args = [t(sc[k]) for k in ("means3D", "colors", "opacities", "scales", "rotations")]
+    args += [views, projs, tanf, torch.zeros((B, 32), device=DEV)]
+    r = BatchRasterizer(B, P, W, H, R_capacity=40 * P * B, device=DEV)
+    ref = [x.clone() for x in r.forward(*args)]
+    R_ref = r.status()[0]
+    for x in r.out_color, r.out_invdepth, r.radii:
+        x.fill_(7)
+    got = r.forward(*args, forward_only=True)
+    torch.cuda.synchronize()
+    assert r.status()[0] == R_ref
+    for a, b in zip(ref, got):
+        assert torch.equal(a, b)
+    with pytest.raises(GsrError):
+        r.backward(*args, torch.zeros((B, 32, H, W), device=DEV))
