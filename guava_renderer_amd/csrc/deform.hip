@@ -289,45 +289,31 @@ constexpr int kTiledUnroll = 4;  // tile groups whose loads are issued before th
 // D[frame][m] over the k of one base: v_mfma_f32_32x32x2_f32 with lane (c, h) holding base[8g + 4h + j]
 // [32t + c] (B operand) and coef[frame b0 + c][8g + 4h + j] (A operand) for the j-th MFMA of a group
 // (the lane halves' k of one MFMA are 8g + j and 8g + 4 + j); wave w takes the groups g = w mod 4.
-// The coefficients go through LDS: per chunk of kCoefChunk k the workgroup stages its 32 frames' rows
-// transposed (coalesced row reads; ct[k][frame], pitch kCoefPitch), so an A operand is one LDS read of
-// 32 consecutive words per half-wave instead of a global load touching 32 rows.
-constexpr int kCoefChunk = 128, kCoefPitch = 33;
 __device__ __forceinline__ void blend_tiled_mfma_part(floatx16& acc, const float* __restrict__ coef, int ncoef,
-                                                      const float4* __restrict__ tb, int K, int t, int b0, int B,
-                                                      int w, int hi, int lane, float* ct) {
+                                                      const float4* __restrict__ tb, int K, int t, int bA,
+                                                      bool bok, int w, int hi, int lane) {
     const int nkg = (K + 7) / 8;
     const float4* __restrict__ p = tb + (int64_t)t * nkg * 64 + lane;
-    const int c = lane & 31;
-    for (int k0 = 0; k0 < K; k0 += kCoefChunk) {
-        const int nk = min(kCoefChunk, K - k0);
-        __syncthreads();  // the previous chunk's readers are done
-        for (int idx = threadIdx.x; idx < 32 * kCoefChunk; idx += 256) {
-            const int f = idx / kCoefChunk, kk = idx - f * kCoefChunk;
-            ct[kk * kCoefPitch + f] = (kk < nk && b0 + f < B) ? coef[(int64_t)(b0 + f) * ncoef + k0 + kk] : 0.f;
+    const float* __restrict__ cr = coef + (int64_t)bA * ncoef;
+    for (int g0 = w; g0 < nkg; g0 += 4 * kTiledUnroll) {
+        float4 v[kTiledUnroll];
+        float a[kTiledUnroll][4];
+#pragma unroll
+        for (int u = 0; u < kTiledUnroll; u++) {
+            const int g = g0 + 4 * u;
+            v[u] = g < nkg ? p[(int64_t)g * 64] : make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+            for (int j = 0; j < 4; j++) {
+                const int k = 8 * g + 4 * hi + j;
+                a[u][j] = (bok && k < K) ? cr[k] : 0.f;
+            }
         }
-        __syncthreads();
-        const int g_lo = k0 / 8, g_hi = min(nkg, (k0 + kCoefChunk) / 8);
-        for (int g0 = g_lo + w; g0 < g_hi; g0 += 4 * kTiledUnroll) {
-            float4 v[kTiledUnroll];
-            float a[kTiledUnroll][4];
 #pragma unroll
-            for (int u = 0; u < kTiledUnroll; u++) {
-                const int g = g0 + 4 * u;
-                v[u] = g < g_hi ? p[(int64_t)g * 64] : make_float4(0.f, 0.f, 0.f, 0.f);
-#pragma unroll
-                for (int j = 0; j < 4; j++) {
-                    const int kk = 8 * g + 4 * hi + j - k0;  // (rows past K were staged as 0)
-                    a[u][j] = g < g_hi ? ct[kk * kCoefPitch + c] : 0.f;
-                }
-            }
-#pragma unroll
-            for (int u = 0; u < kTiledUnroll; u++) {
-                acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a[u][0], v[u].x, acc, 0, 0, 0);
-                acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a[u][1], v[u].y, acc, 0, 0, 0);
-                acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a[u][2], v[u].z, acc, 0, 0, 0);
-                acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a[u][3], v[u].w, acc, 0, 0, 0);
-            }
+        for (int u = 0; u < kTiledUnroll; u++) {
+            acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a[u][0], v[u].x, acc, 0, 0, 0);
+            acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a[u][1], v[u].y, acc, 0, 0, 0);
+            acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a[u][2], v[u].z, acc, 0, 0, 0);
+            acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a[u][3], v[u].w, acc, 0, 0, 0);
         }
     }
 }
@@ -342,20 +328,16 @@ __global__ __launch_bounds__(256) void k_lbs_blend_tiled(int B, int M, int NB, i
                                                          const float4* __restrict__ pd_tiled,
                                                          float* __restrict__ v_shaped,
                                                          float* __restrict__ v_posed) {
-    // coefficient chunks (blend_tiled_mfma_part), then the per-wave partial tiles [wave][part][reg][lane]
-    __shared__ float lds[4 * 2 * 16 * 64];
-    static_assert(kCoefChunk * kCoefPitch <= 4 * 2 * 16 * 64, "coefficient chunk fits the reduction tile");
-    float (*red)[2][16][64] = reinterpret_cast<float (*)[2][16][64]>(lds);
+    __shared__ float red[4][2][16][64];
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, hi = lane >> 5, l32 = lane & 31;
     const int t = blockIdx.x, m0 = t * 32, b0 = blockIdx.y * 32;
-    const int m = m0 + l32;
-    const bool mok = m < M;
+    const int m = m0 + l32, bA = b0 + l32;
+    const bool mok = m < M, bok = bA < B;
     floatx16 as, ap;
 #pragma unroll
     for (int r = 0; r < 16; r++) { as[r] = 0.f; ap[r] = 0.f; }
-    if (NB > 0) blend_tiled_mfma_part(as, betas, NB, sd_tiled, NB, t, b0, B, w, hi, lane, lds);
-    if (NP > 0 && v_posed) blend_tiled_mfma_part(ap, feat, NP, pd_tiled, NP, t, b0, B, w, hi, lane, lds);
-    __syncthreads();  // the last coefficient chunk's readers are done
+    if (NB > 0) blend_tiled_mfma_part(as, betas, NB, sd_tiled, NB, t, bA, bok, w, hi, lane);
+    if (NP > 0 && v_posed) blend_tiled_mfma_part(ap, feat, NP, pd_tiled, NP, t, bA, bok, w, hi, lane);
 #pragma unroll
     for (int r = 0; r < 16; r++) {
         red[w][0][r][lane] = as[r];
@@ -912,12 +894,6 @@ __global__ __launch_bounds__(256) void k_deform_gaussians(
         if (a >= 0 && a < V && c >= 0 && c < V && d >= 0 && d < V) { t0 = a; t1 = c; t2 = d; }
     }
     const int b1 = min(B, (int)(blockIdx.y + 1) * fpw);
-    // means and scales leave through LDS as 16-byte stores of the workgroup's contiguous 3 KB rows
-    // (12-byte rows per thread were three 4-byte stores at a 12-byte stride)
-    __shared__ float4 st4[2][192];
-    float* st = reinterpret_cast<float*>(st4);
-    const int i0 = blockIdx.x * blockDim.x;
-    const int nrow = min((int)blockDim.x, P - i0);  // Gaussians of this workgroup
     for (int b = blockIdx.y * fpw; b < b1; b++) {
         const float* vb = verts + (int64_t)b * V * 3;
         if (shared_frames) {
@@ -925,8 +901,8 @@ __global__ __launch_bounds__(256) void k_deform_gaussians(
             if (t0 >= 0) face_frame(vb, t0, t1, t2, fr_lds + threadIdx.x * kFrStride);
             __syncthreads();
         }
+        if (i >= P) continue;
         const int64_t o = (int64_t)b * P + i;
-        float mo[3] = {0.f, 0.f, 0.f}, so[3] = {0.f, 0.f, 0.f};
         if (i < V) {
             const float4* tv = reinterpret_cast<const float4*>(vtrans + ((int64_t)b * V + i) * 16);
             const float4 r0 = tv[0], r1 = tv[1], r2 = tv[2];
@@ -938,59 +914,41 @@ __global__ __launch_bounds__(256) void k_deform_gaussians(
             const float nn = fmaxf(sqrtf(((q.w * q.w + q.x * q.x) + q.y * q.y) + q.z * q.z), 1e-12f);
             reinterpret_cast<float4*>(rots)[o] = make_float4(q.w / nn, q.x / nn, q.y / nn, q.z / nn);
             for (int c = 0; c < 3; c++) {
-                mo[c] = vb[3 * i + c];
-                so[c] = vscale[b * s_vscale + 3 * (int64_t)i + c];
+                means[3 * o + c] = vb[3 * i + c];
+                scales[3 * o + c] = vscale[b * s_vscale + 3 * (int64_t)i + c];
             }
-        } else if (uv && f < 0) {
-            const float nan = __int_as_float(0x7fc00000);
-            for (int c = 0; c < 3; c++) { mo[c] = nan; so[c] = nan; }
-            reinterpret_cast<float4*>(rots)[o] = make_float4(nan, nan, nan, nan);
-        } else if (uv) {
-            float fr[14];
-            if (shared_frames) {
-                const float* src = fr_lds + (f - fmin) * kFrStride;
-#pragma unroll
-                for (int k = 0; k < 14; k++) fr[k] = src[k];
-            } else {
-                face_frame(vb, j0, j1, j2, fr);
-            }
-            const float s = fr[9];
-            const float* qu = urot + b * s_urot + 4 * (int64_t)n;  // wxyz
-            const float4 q = quat_product(make_float4(fr[10], fr[11], fr[12], fr[13]), make_float4(qu[1], qu[2], qu[3], qu[0]));
-            if (!GSR_DEFORM_NOSTORE || q.w == 12345.f) reinterpret_cast<float4*>(rots)[o] = make_float4(q.w, q.x, q.y, q.z);
-            const float* l = lxyz + b * s_lxyz + 3 * (int64_t)n;
-            const float lx = l[0], ly = l[1], lz = l[2];
-            const float cx = (w0 * vb[3 * j0] + w1 * vb[3 * j1]) + w2 * vb[3 * j2];
-            const float cy = (w0 * vb[3 * j0 + 1] + w1 * vb[3 * j1 + 1]) + w2 * vb[3 * j2 + 1];
-            const float cz = (w0 * vb[3 * j0 + 2] + w1 * vb[3 * j1 + 2]) + w2 * vb[3 * j2 + 2];
-            mo[0] = dot3(fr[0], fr[1], fr[2], lx, ly, lz) * s + cx;
-            mo[1] = dot3(fr[3], fr[4], fr[5], lx, ly, lz) * s + cy;
-            mo[2] = dot3(fr[6], fr[7], fr[8], lx, ly, lz) * s + cz;
-            const float* us = uscale + b * s_uscale + 3 * (int64_t)n;
-            for (int c = 0; c < 3; c++) so[c] = us[c] * s;
-        }
-        if (GSR_DEFORM_NOSTORE) continue;  // timing ablation: no means / scales stores
-        // rows [i0, i0 + nrow) of frame b are floats [3 (b P + i0), +3 nrow) of means and scales
-        const int64_t f0 = 3 * ((int64_t)b * P + i0);
-        const bool vec = ((reinterpret_cast<uintptr_t>(means) | reinterpret_cast<uintptr_t>(scales)) & 15) == 0 &&
-                         (f0 & 3) == 0;  // (uniform)
-        if (!vec) {
-            if (i < P)
-                for (int c = 0; c < 3; c++) { means[3 * o + c] = mo[c]; scales[3 * o + c] = so[c]; }
             continue;
         }
-        __syncthreads();  // the previous frame's stage readers are done
-        if (i < P)
-            for (int c = 0; c < 3; c++) { st[3 * threadIdx.x + c] = mo[c]; st[768 + 3 * threadIdx.x + c] = so[c]; }
-        __syncthreads();
-        const int n4 = (3 * nrow) / 4;  // whole float4s; the rest (at most 3 floats) by scalar stores
-        if ((int)threadIdx.x < n4) {
-            reinterpret_cast<float4*>(means + f0)[threadIdx.x] = st4[0][threadIdx.x];
-            reinterpret_cast<float4*>(scales + f0)[threadIdx.x] = st4[1][threadIdx.x];
-        } else if ((int)threadIdx.x < n4 + (3 * nrow - 4 * n4)) {
-            const int e = 4 * n4 + ((int)threadIdx.x - n4);
-            means[f0 + e] = st[e];
-            scales[f0 + e] = st[768 + e];
+        if (f < 0) {
+            const float nan = __int_as_float(0x7fc00000);
+            for (int c = 0; c < 3; c++) { means[3 * o + c] = nan; scales[3 * o + c] = nan; }
+            reinterpret_cast<float4*>(rots)[o] = make_float4(nan, nan, nan, nan);
+            continue;
+        }
+        float fr[14];
+        if (shared_frames) {
+            const float* src = fr_lds + (f - fmin) * kFrStride;
+#pragma unroll
+            for (int k = 0; k < 14; k++) fr[k] = src[k];
+        } else {
+            face_frame(vb, j0, j1, j2, fr);
+        }
+        const float s = fr[9];
+        const float* qu = urot + b * s_urot + 4 * (int64_t)n;  // wxyz
+        const float4 q = quat_product(make_float4(fr[10], fr[11], fr[12], fr[13]), make_float4(qu[1], qu[2], qu[3], qu[0]));
+        if (!GSR_DEFORM_NOSTORE || q.w == 12345.f) reinterpret_cast<float4*>(rots)[o] = make_float4(q.w, q.x, q.y, q.z);
+        const float* l = lxyz + b * s_lxyz + 3 * (int64_t)n;
+        const float lx = l[0], ly = l[1], lz = l[2];
+        const float cx = (w0 * vb[3 * j0] + w1 * vb[3 * j1]) + w2 * vb[3 * j2];
+        const float cy = (w0 * vb[3 * j0 + 1] + w1 * vb[3 * j1 + 1]) + w2 * vb[3 * j2 + 1];
+        const float cz = (w0 * vb[3 * j0 + 2] + w1 * vb[3 * j1 + 2]) + w2 * vb[3 * j2 + 2];
+        const float mx = dot3(fr[0], fr[1], fr[2], lx, ly, lz) * s + cx;
+        const float my = dot3(fr[3], fr[4], fr[5], lx, ly, lz) * s + cy;
+        const float mz = dot3(fr[6], fr[7], fr[8], lx, ly, lz) * s + cz;
+        const float* us = uscale + b * s_uscale + 3 * (int64_t)n;
+        if (!GSR_DEFORM_NOSTORE || mx == 12345.f) {
+            means[3 * o] = mx; means[3 * o + 1] = my; means[3 * o + 2] = mz;
+            for (int c = 0; c < 3; c++) scales[3 * o + c] = us[c] * s;
         }
     }
 }
