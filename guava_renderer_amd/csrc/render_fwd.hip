@@ -55,6 +55,10 @@ namespace gsr {
 #ifndef GSR_BATCH_NSLOT
 #define GSR_BATCH_NSLOT 3  // pipeline slots of the batched (throughput) kernels
 #endif
+#ifndef GSR_HALF_REC_DIRECT
+#define GSR_HALF_REC_DIRECT 1  // half-strip (single-frame) waves: each lane loads its Gaussian's 32-B record
+                               // with two 16-B loads (no LDS broadcast on the k-step's dependency chain)
+#endif
 #ifndef GSR_FILL16
 #define GSR_FILL16 1  // empty tiles as 16-byte stores (0: per-strip dword stores, the round-2 form; PMC A/B)
 #endif
@@ -506,7 +510,11 @@ __device__ __forceinline__ void render_fwd_body(const Dims& d, const Inputs& in,
                 if (!S##hb) { gb_ = (uint32_t)d.P; pb_ = pa_; }                                     \
             }                                                                                       \
             S##pa = pa_; S##pb = pb_;                                                               \
-            if (GSR_REC_PATH == 3) {  /* lanes 0..7: dword `lane` of both records, SGPR offsets */ \
+            if (HALF && GSR_HALF_REC_DIRECT) {  /* lane half h: survivor h's whole record */        \
+                const uint32_t gl_ = hi ? gb_ : ga_;                                                \
+                S##a0 = rec_load(rrs, gl_ * 32);                                                    \
+                S##a1 = rec_load(rrs, gl_ * 32 + 16);                                               \
+            } else if (GSR_REC_PATH == 3) {  /* lanes 0..7: dword `lane` of both records, SGPR offsets */ \
                 S##r = __builtin_amdgcn_raw_buffer_load_b32(rrs, rec_voff, (int)(ga_ * 32), 0);     \
                 S##r2 = __builtin_amdgcn_raw_buffer_load_b32(rrs, rec_voff, (int)(gb_ * 32), 0);    \
             } else {                                                                                \
@@ -525,7 +533,8 @@ __device__ __forceinline__ void render_fwd_body(const Dims& d, const Inputs& in,
         // through the wave's LDS slot (GSR_ALPHA_LDS), then the alpha arithmetic (GSR_ALPHA_MATH)
 #define GSR_ALPHA_LDS(S)                                                                            \
         {                                                                                           \
-            if (HALF) {  /* each lane its own Gaussian's record: a in lanes 0-31, b in 32-63 */     \
+            if (HALF && GSR_HALF_REC_DIRECT) {  /* (loaded straight into a0 / a1 by GSR_FETCH) */    \
+            } else if (HALF) {  /* each lane its own Gaussian's record: a in lanes 0-31, b in 32-63 */ \
                 rec_lds[rec_widx] = S##r; rec_lds[rec_widx + 8] = S##r2;                            \
                 __builtin_amdgcn_wave_barrier();                                                    \
                 S##a0 = __builtin_bit_cast(float4, *(const uint4x*)&rec_lds[8 * hi]);               \
@@ -1148,13 +1157,16 @@ __device__ __forceinline__ void render_fwd_body(const Dims& d, const Inputs& in,
 #ifndef GSR_RENDER_WPE
 #define GSR_RENDER_WPE 5
 #endif
+#ifndef GSR_HALF_WPE
+#define GSR_HALF_WPE 3  // half-strip waves (one frame): launched GSR_RENDER_HALF_WG = 3 per CU
+#endif
 #ifndef GSR_QONLY_WPE
 #define GSR_QONLY_WPE 6  // quad-only waves (one frame): no 32-register strip accumulators
 #endif
 template <bool EXACT, bool STATS, bool TL, int SPLIT = 0, int NSLOT = GSR_BATCH_NSLOT, bool HALF = false,
           bool QUAD = false, bool QONLY = false, bool HTAIL = false>
 __global__ __launch_bounds__(GSR_TILE_PIX)
-__attribute__((amdgpu_waves_per_eu(QONLY ? GSR_QONLY_WPE : (NSLOT == 5 && !HALF && GSR_BATCH_NSLOT != 5) ? 3 : GSR_RENDER_WPE))) void k_render_fwd(
+__attribute__((amdgpu_waves_per_eu(QONLY ? GSR_QONLY_WPE : HALF ? GSR_HALF_WPE : (NSLOT == 5 && GSR_BATCH_NSLOT != 5) ? 3 : GSR_RENDER_WPE))) void k_render_fwd(
     Dims d, Inputs in, GeomArena g, ImageArena im, BinArena bn, Outputs o) {
     render_fwd_body<EXACT, STATS, TL, false, 0, SPLIT, NSLOT, HALF, QUAD, QONLY, HTAIL>(d, in, g, im, bn, o);
 }
@@ -1194,7 +1206,7 @@ void launch_render_fwd(const Dims& d, const Inputs& in_, const GeomArena& g, con
     static const bool latency_mode = [] { const char* e = getenv("GSR_RENDER_LATENCY"); return !(e && e[0] == '0'); }();
     // GSR_RENDER_HALF=0: single-frame launches use full-strip waves (A/B); GSR_RENDER_HALF_WG: WGs per CU
     static const bool half_mode = [] { const char* e = getenv("GSR_RENDER_HALF"); return !(e && e[0] == '0'); }();
-    static const int half_wg = [] { const char* e = getenv("GSR_RENDER_HALF_WG"); return e ? atoi(e) : 3; }();
+    static const int half_wg = [] { const char* e = getenv("GSR_RENDER_HALF_WG"); return e ? atoi(e) : GSR_HALF_WPE; }();
     // GSR_RENDER_QONLY=1: single-frame launches use quad-only waves instead of the half-strip waves
     // (measured the same, 0.271 ms per C2 frame either way: off by default); GSR_RENDER_QONLY_WG: WGs per CU
     static const bool qonly_mode = [] { const char* e = getenv("GSR_RENDER_QONLY"); return e && e[0] == '1'; }();
