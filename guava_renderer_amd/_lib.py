@@ -19,6 +19,7 @@ EXPORTS = ("gsr_version", "gsr_last_error", "gsr_geometry_bytes",
            # include/gsr_deform.h
            "gsr_lbs_workspace_bytes", "gsr_lbs", "gsr_lbs_sp", "gsr_blend_joints", "gsr_blend_joints_sp",
            "gsr_lbs_tiled_floats", "gsr_lbs_tile_bases",
+           "gsr_scratch_geometry", "gsr_scratch_binning", "gsr_scratch_image",
            "gsr_splice_head",
            "gsr_pack_rows", "gsr_deform_gaussians",
            # include/gsr_ssim.h
@@ -53,6 +54,12 @@ class RefineEpilogue(ctypes.Structure):
     """gsr_refine_epilogue (include/gsr.h)."""
     _fields_ = [("weight", _vp), ("bias", _vp), ("n_out", _i), ("negative_slope", _f),
                 ("out_refine", _vp), ("keep_channels", _i)]
+
+
+class Scratch(ctypes.Structure):
+    """gsr_scratch (include/gsr.h): preallocated buffers for the three forward resizers."""
+    _fields_ = [("geometry", _vp), ("geometry_cap", _sz), ("binning", _vp), ("binning_cap", _sz),
+                ("image", _vp), ("image_cap", _sz)]
 
 
 class RowSegment(ctypes.Structure):

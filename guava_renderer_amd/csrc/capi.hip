@@ -234,6 +234,9 @@ int gsr_mark_visible(int P, const float* means3D, const float* viewmatrix, const
     return 0;
 }
 
+// gsr_forward_async without a status block (prefiltered 0): the async path, nothing copied back
+static uint32_t* const kNoStatus = reinterpret_cast<uint32_t*>(uintptr_t(1));
+
 // status_host == nullptr: the reference's synchronous contract (R read back after the scan, the
 // binning buffer sized to R, num_rendered returned).  Otherwise the binning buffer is sized to
 // the upper bound P x tiles (R cannot exceed it), nothing waits on the device, and the control
@@ -295,7 +298,8 @@ static int forward_single(gsr_alloc_fn geometryBuffer, gsr_alloc_fn binningBuffe
         carve_bin(bb, cap, &bn);
         int rc = run_binning_and_render(d, in, g, im, bn, o, numerics, debug, s);
         if (rc < 0) return rc;
-        HIP_TRY(hipMemcpyAsync(status_host, g.ctrl, 4 * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+        if (status_host != kNoStatus)
+            HIP_TRY(hipMemcpyAsync(status_host, g.ctrl, 4 * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
         return 0;
     }
     { StageTimer st_(1, s); launch_scan_blocksums(d, g, (int64_t)0xFFFFFFF0u, s); }
@@ -359,12 +363,26 @@ int gsr_forward_async(gsr_alloc_fn geometryBuffer, gsr_alloc_fn binningBuffer, g
                       const float* projmatrix, const float* cam_pos, float tan_fovx, float tan_fovy,
                       int prefiltered, float* out_color, float* depth, int antialiasing, int* radii,
                       int debug, uint32_t* status_host, uint32_t numerics, void* stream) {
-    if (!status_host) return fail(GSR_ERR_ARG, "gsr_forward_async: null status_host");
+    if (!status_host && prefiltered) return fail(GSR_ERR_ARG, "gsr_forward_async: null status_host with prefiltered");
     if (debug) return fail(GSR_ERR_ARG, "gsr_forward_async: debug mode synchronises; use gsr_forward");
     return forward_single(geometryBuffer, binningBuffer, imageBuffer, alloc_ctx, P, D, M, background, width,
                           height, means3D, shs, colors_precomp, opacities, scales, scale_modifier, rotations,
                           cov3D_precomp, viewmatrix, projmatrix, cam_pos, tan_fovx, tan_fovy, prefiltered,
-                          out_color, depth, antialiasing, radii, debug, status_host, numerics, (hipStream_t)stream);
+                          out_color, depth, antialiasing, radii, debug, status_host ? status_host : kNoStatus,
+                          numerics, (hipStream_t)stream);
+}
+
+char* gsr_scratch_geometry(void* scratch, size_t bytes) {
+    const gsr_scratch* sc = static_cast<const gsr_scratch*>(scratch);
+    return sc && bytes <= sc->geometry_cap ? sc->geometry : nullptr;
+}
+char* gsr_scratch_binning(void* scratch, size_t bytes) {
+    const gsr_scratch* sc = static_cast<const gsr_scratch*>(scratch);
+    return sc && bytes <= sc->binning_cap ? sc->binning : nullptr;
+}
+char* gsr_scratch_image(void* scratch, size_t bytes) {
+    const gsr_scratch* sc = static_cast<const gsr_scratch*>(scratch);
+    return sc && bytes <= sc->image_cap ? sc->image : nullptr;
 }
 
 int gsr_backward_ex(int P, int D, int M, int R, const float* background, int width, int height,

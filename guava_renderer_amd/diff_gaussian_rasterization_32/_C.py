@@ -256,6 +256,95 @@ def rasterize_gaussians(background, means3D, colors, opacity, scales, rotations,
     return rendered, out_color, radii, geom.t, binning.t, img.t, out_invdepth
 
 
+class _Scratch:
+    """The three scratch arenas of inference forwards on one (device, stream), kept between calls
+    (stream order makes the reuse safe) and handed to the C ABI through its preallocated-scratch
+    resizers (include/gsr.h gsr_scratch_*): no host callback and no allocation per call."""
+
+    def __init__(self, device):
+        self.device = device
+        self.bufs = [torch.empty((0,), dtype=torch.uint8, device=device) for _ in range(3)]
+        self.s = _lib.Scratch()
+        self.sizes = {}
+
+    def fit(self, L, P, W, H, bound):
+        key = (P, W, H)
+        need = self.sizes.get(key)
+        if need is None:
+            need = self.sizes[key] = (L.gsr_geometry_bytes(P, W, H), L.gsr_binning_bytes(bound),
+                                      L.gsr_image_bytes(W, H))
+        for i, n in enumerate(need):
+            if self.bufs[i].numel() < n:
+                self.bufs[i] = torch.empty((int(n),), dtype=torch.uint8, device=self.device)
+        s = self.s
+        s.geometry, s.geometry_cap = self.bufs[0].data_ptr(), self.bufs[0].numel()
+        s.binning, s.binning_cap = self.bufs[1].data_ptr(), self.bufs[1].numel()
+        s.image, s.image_cap = self.bufs[2].data_ptr(), self.bufs[2].numel()
+        return s
+
+
+_SCRATCH = {}
+_SCRATCH_FNS = None
+
+
+def rasterize_inference(background, means3D, colors, opacity, scales, rotations, scale_modifier, cov3D_precomp,
+                        viewmatrix, projmatrix, tan_fovx, tan_fovy, image_height, image_width, antialiasing,
+                        numerics=None):
+    """The forward of an inference call (no gradient, debug and prefiltered off): the images of
+    rasterize_gaussians -- (color[32,H,W], radii[P], invdepth[1,H,W]), bit-identical -- without its
+    per-call host work: the scratch arenas are kept per (device, stream) and passed preallocated
+    (no allocator callbacks), no status copy (no error is possible without prefiltered), and no
+    autograd node.  Returns None when it does not apply (the caller takes rasterize_gaussians)."""
+    global _SCRATCH_FNS
+    if means3D.ndimension() != 2 or means3D.size(1) != 3:
+        raise RuntimeError("means3D must have dimensions (num_points, 3)")
+    P, H, W = int(means3D.size(0)), int(image_height), int(image_width)
+    dev = means3D.device
+    if P == 0 or dev.type != "cuda" or colors is None or colors.numel() == 0:
+        return None
+    L = _lib.load()
+    bound = L.gsr_forward_async_bound(P, W, H)
+    if bound >= 0x7FFFFFFF or L.gsr_binning_bytes(bound) > ASYNC_BINNING_MB << 20:
+        return None
+    if numerics is None:
+        numerics = DEFAULT_NUMERICS
+    ts = (background, means3D, colors, opacity, scales, rotations, viewmatrix, projmatrix)
+    for t_ in ts:
+        if t_ is not None and t_.numel() and (t_.device != dev or t_.dtype != torch.float32):
+            return None  # (the general path raises the reference's errors)
+    background, means3D, colors, opacity, scales, rotations, viewmatrix, projmatrix = (
+        t_.contiguous() if t_ is not None and t_.numel() else t_ for t_ in ts)
+    if colors.data_ptr() % 16:
+        colors = colors.clone()
+    cov = cov3D_precomp if (cov3D_precomp is not None and cov3D_precomp.numel()) else None
+    if cov is not None:
+        if cov.device != dev or cov.dtype != torch.float32:
+            return None
+        cov = cov.contiguous()
+    stream = torch.cuda.current_stream(dev)
+    key = (dev, stream.cuda_stream)
+    sc = _SCRATCH.get(key)
+    if sc is None:
+        sc = _SCRATCH[key] = _Scratch(dev)
+    s = sc.fit(L, P, W, H, bound)
+    if _SCRATCH_FNS is None:
+        addr = lambda f: ctypes.cast(f, ctypes.c_void_p).value  # noqa: E731
+        _SCRATCH_FNS = tuple(_lib.ALLOC_FN(addr(f)) for f in (L.gsr_scratch_geometry, L.gsr_scratch_binning,
+                                                                L.gsr_scratch_image))
+    fopts = dict(dtype=torch.float32, device=dev)
+    out_color = torch.empty((NUM_CHANNELS, H, W), **fopts)
+    out_invdepth = torch.empty((1, H, W), **fopts)
+    radii = torch.empty((P,), dtype=torch.int32, device=dev)
+    _lib.check(L.gsr_forward_async(*_SCRATCH_FNS, ctypes.addressof(s), P, 0, 0, _ptr(background), W, H,
+                                   means3D.data_ptr(), None, colors.data_ptr(), _ptr(opacity), _ptr(scales),
+                                   float(scale_modifier), _ptr(rotations), _ptr(cov), _ptr(viewmatrix),
+                                   _ptr(projmatrix), None, float(tan_fovx), float(tan_fovy), 0,
+                                   out_color.data_ptr(), out_invdepth.data_ptr(), int(bool(antialiasing)),
+                                   radii.data_ptr(), 0, None, int(numerics), ctypes.c_void_p(stream.cuda_stream)),
+               "rasterize_gaussians")
+    return out_color, radii, out_invdepth
+
+
 def rasterize_gaussians_backward(background, means3D, radii, colors, opacities, scales, rotations,
                                  scale_modifier, cov3D_precomp, viewmatrix, projmatrix, tan_fovx,
                                  tan_fovy, dL_dout_color, dL_dout_invdepth, sh, degree, campos,

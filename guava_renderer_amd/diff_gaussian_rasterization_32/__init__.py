@@ -22,12 +22,16 @@ __init__.py): `rasterize_gaussians` (:21-42), `_RasterizeGaussians` (:44-141),
 models/UbodyAvatar/gaussian_render.py, render_motion.py and main/test.py run unchanged.
 The native `_C` module is backed by the HIP kernels of libgsr.so; there is no CPU path.
 """
+import os
 from typing import NamedTuple
 
 import torch
 import torch.nn as nn
 
 from . import _C
+
+# GSR_INFERENCE_PATH=0: inference calls take the autograd Function too (A/B of _C.rasterize_inference)
+_INFERENCE_PATH = os.environ.get("GSR_INFERENCE_PATH", "1") != "0"
 
 
 def cpu_deep_copy_tuple(input_tuple):
@@ -43,6 +47,17 @@ def rasterize_gaussians(means3D, means2D, sh, colors_precomp, opacities, scales,
     # without a host synchronisation and its transient buffer is released with the call
     inputs = (means3D, means2D, sh, colors_precomp, opacities, scales, rotations, cov3Ds_precomp)
     record = torch.is_grad_enabled() and any(isinstance(t, torch.Tensor) and t.requires_grad for t in inputs)
+    if (_INFERENCE_PATH and not record and not raster_settings.debug and not raster_settings.prefiltered
+            and (sh is None or sh.numel() == 0)):
+        # nothing will call backward: the same images without the autograd node and the per-call
+        # scratch allocations (_C.rasterize_inference; None when it does not apply)
+        out = _C.rasterize_inference(raster_settings.bg, means3D, colors_precomp, opacities, scales, rotations,
+                                     raster_settings.scale_modifier, cov3Ds_precomp, raster_settings.viewmatrix,
+                                     raster_settings.projmatrix, raster_settings.tanfovx, raster_settings.tanfovy,
+                                     raster_settings.image_height, raster_settings.image_width,
+                                     raster_settings.antialiasing)
+        if out is not None:
+            return out
     return _RasterizeGaussians.apply(means3D, means2D, sh, colors_precomp, opacities, scales,
                                      rotations, cov3Ds_precomp, raster_settings, record)
 

@@ -115,7 +115,8 @@ int gsr_forward_ex(gsr_alloc_fn geometryBuffer, gsr_alloc_fn binningBuffer, gsr_
  * status_host (4 uint32, host-visible, e.g. pinned) receives {num_rendered, overflow, error bits,
  * 0} at the end of the stream's work: read it after synchronising (error bit 0 = a culled point
  * with prefiltered set, the reference's trap; overflow only if the bound hit 2^31 - 1).  Returns
- * 0 or -status.  debug must be 0. */
+ * 0 or -status.  debug must be 0.  status_host may be NULL when prefiltered is 0 (no error is then
+ * possible and num_rendered is not wanted, e.g. inference): nothing is copied back. */
 int64_t gsr_forward_async_bound(int P, int width, int height);
 int gsr_forward_async(gsr_alloc_fn geometryBuffer, gsr_alloc_fn binningBuffer, gsr_alloc_fn imageBuffer,
                       void* alloc_ctx, int P, int D, int M, const float* background, int width, int height,
@@ -125,6 +126,19 @@ int gsr_forward_async(gsr_alloc_fn geometryBuffer, gsr_alloc_fn binningBuffer, g
                       const float* projmatrix, const float* cam_pos, float tan_fovx, float tan_fovy,
                       int prefiltered, float* out_color, float* depth, int antialiasing, int* radii,
                       int debug, uint32_t* status_host, uint32_t numerics, void* stream);
+
+/* Preallocated scratch for the three gsr_alloc_fn resizers: pass gsr_scratch_geometry /
+ * gsr_scratch_binning / gsr_scratch_image as the callbacks and a gsr_scratch* as alloc_ctx; each
+ * returns its buffer when `bytes` fits its capacity and NULL otherwise (the call then fails with
+ * GSR_ERR_ALLOC).  No host callback runs during the forward (a caller keeps one scratch per stream). */
+typedef struct {
+    char* geometry; size_t geometry_cap;
+    char* binning; size_t binning_cap;
+    char* image; size_t image_cap;
+} gsr_scratch;
+char* gsr_scratch_geometry(void* scratch, size_t bytes);
+char* gsr_scratch_binning(void* scratch, size_t bytes);
+char* gsr_scratch_image(void* scratch, size_t bytes);
 
 /* Rasterizer::backward.  Gradient buffers are accumulated into and must be zeroed by the caller
  * (the reference's torch::zeros, rasterize_points.cu:163-179): dL_dmean2D [P,3], dL_dconic [P,4],

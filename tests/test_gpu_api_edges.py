@@ -248,3 +248,38 @@ def test_forward_only_batch_same_images_and_backward_refused():
         assert torch.equal(a, b)
     with pytest.raises(GsrError):
         r.backward(*args, torch.zeros((B, 32, H, W), device=DEV))
+
+
+def test_inference_path_equals_general_forward():
+    """GaussianRasterizer_32 with nothing to differentiate takes _C.rasterize_inference (scratch
+    arenas kept per stream, no allocator callbacks, no status copy, no autograd node): its images,
+    radii and inverse depth equal _C.rasterize_gaussians' bit for bit, across calls that grow and
+    reuse the scratch; with gradients on, the autograd path is still taken."""
+    from diff_gaussian_rasterization_32 import GaussianRasterizationSettings, GaussianRasterizer_32
+    from guava_renderer_amd.diff_gaussian_rasterization_32 import _C
+    for P, W, H, seed in ((3000, 96, 80, 31), (9000, 160, 128, 32), (3000, 96, 80, 33)):
+        d = make_scene("random", P, W, H, seed=seed)
+        t = torch_inputs(d)
+        s = GaussianRasterizationSettings(
+            image_height=H, image_width=W, tanfovx=d["tanfovx"], tanfovy=d["tanfovy"], bg=t["bg"],
+            scale_modifier=1.0, viewmatrix=t["viewmatrix"], projmatrix=t["projmatrix"], sh_degree=0,
+            campos=t["campos"], prefiltered=False, debug=False, antialiasing=False)
+        means2D = torch.zeros_like(t["means3D"], requires_grad=True)
+        with torch.no_grad():
+            col, radii, inv = GaussianRasterizer_32(s)(
+                means3D=t["means3D"], means2D=means2D, opacities=t["opacities"], colors_precomp=t["colors"],
+                scales=t["scales"], rotations=t["rotations"])
+        assert col.grad_fn is None
+        ref = _C.rasterize_gaussians(t["bg"], t["means3D"], t["colors"], t["opacities"], t["scales"],
+                                     t["rotations"], 1.0, torch.Tensor([]), t["viewmatrix"], t["projmatrix"],
+                                     d["tanfovx"], d["tanfovy"], H, W, torch.Tensor([]), 0, t["campos"], False,
+                                     False, False)
+        torch.cuda.synchronize()
+        assert torch.equal(col, ref[1]) and torch.equal(radii, ref[2]) and torch.equal(inv, ref[6])
+    # gradients wanted: the autograd Function (its backward runs)
+    col, _, _ = GaussianRasterizer_32(s)(
+        means3D=t["means3D"], means2D=means2D, opacities=t["opacities"], colors_precomp=t["colors"],
+        scales=t["scales"], rotations=t["rotations"])
+    assert col.grad_fn is not None
+    col.sum().backward()
+    assert means2D.grad is not None
