@@ -24,7 +24,7 @@ for r in $(seq 1 ${R:-2}); do
         *) export GSR_LIB=guava_renderer_amd/lib/ab/libgsr_$V.so ;;
       esac
       tag=$(echo "$V" | tr -c 'A-Za-z0-9_\n' '_')
-      timeout -k 10 300 python bench.py --pipeline ${PIPE:-avatar} --batch ${BATCH:-32} --inflight 1 --no-cpu-baseline \
+      timeout -k 10 300 python bench.py --pipeline ${PIPE:-avatar} --batch ${BATCH:-32} --inflight ${INFL:-1} --no-cpu-baseline \
         --no-extras --steps ${STEPS:-100} --warmup 10 > $O/$tag.json 2> $O/$tag.err
       rc=$?
       [ $rc -eq 0 ] || { echo "$V rc=$rc"; tail -5 $O/$tag.err; exit $rc; }
