@@ -55,6 +55,9 @@ namespace gsr {
 #ifndef GSR_BATCH_NSLOT
 #define GSR_BATCH_NSLOT 3  // pipeline slots of the batched (throughput) kernels
 #endif
+#ifndef GSR_TAKE_VCC
+#define GSR_TAKE_VCC 1  // strip kernels: the blend step on per-lane values (take_vcc), no lane-mask (SGPR) state
+#endif
 #ifndef GSR_HALF_REC_DIRECT
 #define GSR_HALF_REC_DIRECT 1  // half-strip (single-frame) waves: each lane loads its Gaussian's 32-B record
                                // with two 16-B loads (no LDS broadcast on the k-step's dependency chain)
@@ -109,6 +112,22 @@ __device__ __forceinline__ float take_step(float alpha, float inv_depth, uint32_
     T = contrib ? test_T : T;
     last = contrib ? pos : last;
     done = done || term;
+    return w;
+}
+
+// take_step without lane-mask state (GSR_TAKE_VCC): `alpha` already 0 below 1/255 (alpha stage), and
+// Tc = T for a live pixel, 0 once it stopped, so every branch of take_step is a value select on one
+// compare: a stopped pixel's test_T = 0 < 1e-4 takes nothing again, a skipped Gaussian gives
+// test_T = T * 1 = T.  Same products and decisions as take_step (T the pixel's output transmittance).
+__device__ __forceinline__ float take_vcc(float alpha, float inv_depth, uint32_t pos, float& Tc, float& T, float& invd,
+                                          uint32_t& last) {
+    const float test_T = Tc * (1.0f - alpha);
+    const bool term = test_T < 0.0001f;
+    const float w = term ? 0.0f : alpha * Tc;
+    Tc = term ? 0.0f : test_T;
+    T = term ? T : test_T;
+    invd = fmaf(inv_depth, w, invd);
+    last = w > 0.0f ? pos : last;
     return w;
 }
 
@@ -412,6 +431,9 @@ __device__ __forceinline__ void render_fwd_body(const Dims& d, const Inputs& in,
         const int py = sy0 + lpix / kStripW;
         const float pfx = (float)px, pfy = (float)py;
         bool done = !(px < d.W && py < d.H);
+        // GSR_TAKE_VCC: the throughput strip loop keeps Tc (T while live, 0 once stopped) in place of done
+        constexpr bool VCC = GSR_TAKE_VCC && !HALF && !STATS && !TL && !QUAD && !QONLY && ABL == 0;
+        float Tc = done ? 0.0f : 1.0f;
         float T = 1.0f, invd = 0.f;
         uint32_t last = 0, stop = 0;
         const uint32_t smask_bit = 1u << (28 + strip);
@@ -558,6 +580,10 @@ __device__ __forceinline__ void render_fwd_body(const Dims& d, const Inputs& in,
             } else {                                                                                \
                 S##al = alpha_of<EXACT>(S##a0, S##a1, pfx, pfy);                                    \
                 S##bl = alpha_of<EXACT>(S##b0, S##b1, pfx, pfy);                                    \
+                if (VCC) {  /* below 1/255: never taken (forward.cu:362-363) */                     \
+                    S##al = S##al < 1.0f / 255.0f ? 0.0f : S##al;                                   \
+                    S##bl = S##bl < 1.0f / 255.0f ? 0.0f : S##bl;                                   \
+                }                                                                                   \
                 S##ai = S##a0.w;                                                                    \
                 S##bi = S##b0.w;                                                                    \
             }                                                                                       \
@@ -598,9 +624,11 @@ __device__ __forceinline__ void render_fwd_body(const Dims& d, const Inputs& in,
                                                          !(S##bl < 1.0f / 255.0f))) != 0ull) {       \
             const float f_ = S##f;                                                                  \
             const bool was_done_ = done;                                                            \
-            const float wa_ = take_step(S##al, S##ai, (uint32_t)S##pa, T, invd, last, done);        \
+            const float wa_ = VCC ? take_vcc(S##al, S##ai, (uint32_t)S##pa, Tc, T, invd, last)      \
+                                  : take_step(S##al, S##ai, (uint32_t)S##pa, T, invd, last, done);  \
             const bool done_a_ = done;                                                              \
-            const float wb_ = take_step(S##bl, S##bi, (uint32_t)S##pb, T, invd, last, done);        \
+            const float wb_ = VCC ? take_vcc(S##bl, S##bi, (uint32_t)S##pb, Tc, T, invd, last)      \
+                                  : take_step(S##bl, S##bi, (uint32_t)S##pb, T, invd, last, done);  \
             if (STATS) {                                                                            \
                 if (!was_done_ && done_a_) stop = (uint32_t)S##pa;                                  \
                 else if (!done_a_ && done) stop = (uint32_t)S##pb;                                  \
@@ -687,7 +715,7 @@ __device__ __forceinline__ void render_fwd_body(const Dims& d, const Inputs& in,
                     if (nl_ <= 16) { to_quad = true; break; }
                     if (HTAIL && nl_ <= 32) { to_half = true; break; }
                 } else {
-                    if (!__any(!done)) break;  // every pixel of the strip finished
+                    if (!(VCC ? __any(Tc != 0.0f) : __any(!done))) break;  // every pixel of the strip finished
                 }
             }
             if (QUAD && (to_quad || to_half)) {
@@ -718,7 +746,7 @@ __device__ __forceinline__ void render_fwd_body(const Dims& d, const Inputs& in,
                 GSR_FETCH(D)
                 GSR_STEP(A, E)
                 GSR_FETCH(E)
-                if (!__any(!done)) break;
+                if (!(VCC ? __any(Tc != 0.0f) : __any(!done))) break;
             }
         }
         // ---- half tail ----
