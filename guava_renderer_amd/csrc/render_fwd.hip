@@ -56,7 +56,7 @@ namespace gsr {
 #define GSR_BATCH_NSLOT 3  // pipeline slots of the batched (throughput) kernels
 #endif
 #ifndef GSR_TAKE_VCC
-#define GSR_TAKE_VCC 1  // strip kernels: the blend step on per-lane values (take_vcc), no lane-mask (SGPR) state
+#define GSR_TAKE_VCC 0  // 1: the blend step on per-lane values (take_vcc), no lane-mask state (measured +1.6%: off)
 #endif
 #ifndef GSR_HALF_REC_DIRECT
 #define GSR_HALF_REC_DIRECT 1  // half-strip (single-frame) waves: each lane loads its Gaussian's 32-B record
