@@ -684,7 +684,51 @@ __global__ __launch_bounds__(1024) void k_tile_place(Dims d, GeomArena g, ImageA
     }
 }
 
+// One frame (the per-frame drop-in path): k_tile_scan and k_tile_place in one workgroup -- the
+// work-list bucket starts are this frame's own histogram's prefix (one launch instead of two).
+__global__ __launch_bounds__(1024) void k_tile_scan_place1(Dims d, GeomArena g, ImageArena im) {
+    __shared__ uint32_t sh[1024 / 64 + 1];
+    __shared__ uint32_t h[kLptBuckets];
+    const bool ovf = g.ctrl[kCtrlOverflow] != 0;
+    if (threadIdx.x < kLptBuckets) h[threadIdx.x] = 0;
+    const int per = (d.T + 1023) / 1024;
+    const int beg = threadIdx.x * per, end = min(d.T, beg + per);
+    const uint32_t* cnt = im.tile_count;
+    uint32_t s = 0;
+    if (!ovf)
+        for (int t = beg; t < end; t++) s += cnt[t];
+    uint32_t total;
+    uint32_t ex = block_excl_scan<uint32_t, 1024>(s, &total, sh) + (ovf ? 0u : g.fstat[kFsRBase]);
+    for (int t = beg; t < end; t++) {
+        const uint32_t c = ovf ? 0u : cnt[t];
+        im.ranges[t] = c ? make_uint2(ex, ex + c) : make_uint2(0u, 0u);
+        atomicAdd(&h[c ? __clz(c) : kLptBuckets - 1], 1u);
+        ex += c;
+    }
+    __syncthreads();
+    if (threadIdx.x < kLptBuckets) im.lpt_hist[threadIdx.x] = h[threadIdx.x];
+    __syncthreads();
+    if (threadIdx.x == 0) {  // bucket starts, longest lists first, empty tiles last
+        uint32_t acc = 0;
+        for (int bk = 0; bk < kLptBuckets; bk++) {
+            const uint32_t t = h[bk];
+            if (bk == kLptBuckets - 1) g.ctrl[kCtrlNonEmpty] = acc;
+            h[bk] = acc;
+            acc += t;
+        }
+    }
+    __syncthreads();
+    for (int t = threadIdx.x; t < d.T; t += 1024) {
+        const uint32_t c = ovf ? 0u : cnt[t];
+        im.work_list[atomicAdd(&h[c ? __clz(c) : kLptBuckets - 1], 1u)] = (uint32_t)t;
+    }
+}
+
 void launch_tile_scan(const Dims& d, const GeomArena& g, const ImageArena& im, hipStream_t s) {
+    if (d.B == 1) {
+        hipLaunchKernelGGL(k_tile_scan_place1, dim3(1), dim3(1024), 0, s, d, g, im);
+        return;
+    }
     hipLaunchKernelGGL(k_tile_scan, dim3(d.B), dim3(1024), 0, s, d, g, im);
     hipLaunchKernelGGL(k_tile_place, dim3(d.B), dim3(1024), (size_t)d.B * kLptBuckets * 4, s, d, g, im);
 }
@@ -1111,6 +1155,48 @@ __global__ __launch_bounds__(1024) void k_strip_place(Dims d, ImageArena im, int
     }
 }
 
+// One frame, maps 0 / 1: k_strip_hist and k_strip_place in one workgroup (one launch instead of two).
+__global__ __launch_bounds__(1024) void k_strip_order1(Dims d, ImageArena im, int tile_major) {
+    __shared__ uint32_t h[kStripBuckets];
+    for (int i = threadIdx.x; i < kStripBuckets; i += 1024) h[i] = 0;
+    __syncthreads();
+    for (int t = threadIdx.x; t < d.T; t += 1024) {
+        if (!im.tile_count[t]) continue;
+        if (tile_major) {
+            atomicAdd(&h[strip_bucket(tile_strip_max(im, t))], 1u);
+        } else {
+#pragma unroll
+            for (int sp = 0; sp < kStrips; sp++) atomicAdd(&h[strip_bucket(im.strip_cnt[(int64_t)t * kStrips + sp])], 1u);
+        }
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < kStripBuckets; i += 1024) im.strip_hist[i] = h[i];
+    __syncthreads();
+    if (threadIdx.x == 0) {  // bucket-major starts, most survivors first
+        uint32_t acc = 0;
+        for (int bk = 0; bk < kStripBuckets; bk++) {
+            const uint32_t c = h[bk];
+            h[bk] = acc;
+            acc += c;
+        }
+    }
+    __syncthreads();
+    for (int t = threadIdx.x; t < d.T; t += 1024) {
+        if (!im.tile_count[t]) continue;
+        if (tile_major) {
+            const uint32_t pos = atomicAdd(&h[strip_bucket(tile_strip_max(im, t))], 1u);
+#pragma unroll
+            for (int sp = 0; sp < kStrips; sp++) im.strip_list[kStrips * pos + sp] = ((uint32_t)t << 2) | (uint32_t)sp;
+        } else {
+#pragma unroll
+            for (int sp = 0; sp < kStrips; sp++) {
+                const uint32_t bk = strip_bucket(im.strip_cnt[(int64_t)t * kStrips + sp]);
+                im.strip_list[atomicAdd(&h[bk], 1u)] = ((uint32_t)t << 2) | (uint32_t)sp;
+            }
+        }
+    }
+}
+
 void launch_strip_list_tile(const Dims& d, const ImageArena& im, uint32_t* out, hipStream_t s) {
     if (d.B == 0 || d.T == 0) return;
     ImageArena i2 = im;
@@ -1133,6 +1219,10 @@ void launch_strip_order(const Dims& d, const GeomArena& g, const ImageArena& im,
     const int tile_major = strip_order_tile_major();
     // (one frame: the tile-affine walk of one longest-first list, measured 1.5% faster there)
     const int map = tile_major ? (d.B == 1 ? 1 : xcd_queue_map()) : 0;
+    if (d.B == 1 && map != 2) {
+        hipLaunchKernelGGL(k_strip_order1, dim3(1), dim3(1024), 0, s, d, im, tile_major);
+        return;
+    }
     hipLaunchKernelGGL(k_strip_hist, dim3(d.B), dim3(1024), 0, s, d, im, tile_major, map);
     if (map == 2) {
         // (frame-major segments -- one or two frames' records per XCD L2 at a time -- measured 7%

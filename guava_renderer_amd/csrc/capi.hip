@@ -285,7 +285,6 @@ static int forward_single(gsr_alloc_fn geometryBuffer, gsr_alloc_fn binningBuffe
     Outputs o{out_color, depth, radii, g_render_counters, g_timeline, g_timeline_cap};
 
     HIP_TRY(hipMemsetAsync(g.ctrl, 0, ctrl_words(d) * 4, s));
-    HIP_TRY(hipMemsetAsync(g.bstart, 0, (size_t)d.B * (d.NB + 1) * 4, s));
     { StageTimer st_(0, s); launch_preprocess(d, in, g, o, s); }
     STAGE(debug, s, "preprocess");
     if (status_host) {
@@ -549,7 +548,6 @@ int gsr_forward_batch_refine(int B, int P, int width, int height, const float* m
         o.slope = refine->negative_slope;
     }
     HIP_TRY(hipMemsetAsync(g.ctrl, 0, ctrl_words(d) * 4, s));
-    HIP_TRY(hipMemsetAsync(g.bstart, 0, (size_t)d.B * (d.NB + 1) * 4, s));
     { StageTimer st_(0, s); launch_preprocess(d, in, g, o, s); }
     { StageTimer st_(1, s); launch_scan_blocksums(d, g, R_capacity, s); }
     int rc = run_binning_and_render(d, in, g, im, bn, o, numerics, 0, s);

@@ -28,6 +28,9 @@ __global__ __launch_bounds__(kScanBlock) void k_preprocess(Dims d, Inputs in, Ge
     const int b = blockIdx.y;
     const int i = blockIdx.x * kScanBlock + threadIdx.x;
     const int64_t gid = (int64_t)b * d.P + i;
+    // the frame's depth-bucket counters start at zero (first read by k_bucket_count, after
+    // k_frame_totals): zeroed here instead of by a separate memset launch
+    for (int k = i; k <= d.NB; k += d.nblk * kScanBlock) g.bstart[(int64_t)b * (d.NB + 1) + k] = 0u;
     uint32_t tiles = 0;
     if (i < d.P) {
         const float* view = in.view + 16 * b;
