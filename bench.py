@@ -247,7 +247,12 @@ class Workload:
                     head = RefineHead(t(rng.uniform(-0.18, 0.18, (16, 32)).astype(np.float32)),
                                       t(rng.uniform(-0.18, 0.18, 16).astype(np.float32)), keep_channels=4)
                 pipes = self.pipes
-                self.step_on = lambda i: pipes[i].render(self.bpt, self.fpt, views, projs, tanf, refine=head)
+                # fused: Gaussian assembly inside the projection kernel (gsr_forward_batch_deformed);
+                # no refiner epilogue on that entry, so --refine keeps the two-step path
+                fused = head is None and os.environ.get("GSR_AVATAR_FUSED", "0") == "1"
+                self.config_extra = {"fused_deform": fused}
+                self.step_on = lambda i: pipes[i].render(self.bpt, self.fpt, views, projs, tanf, refine=head,
+                                                         fused=fused)
             else:
                 self._frame_pipeline(probe, numerics)
         elif a.pipeline == "train":
@@ -625,7 +630,9 @@ def main():
                                          "(all 32 channels carry gradient) -> frame-reduced raster bwd -> "
                                          "grad all-reduce -> Adam",
                                 "frame": "deformed frames -> GaussianRasterizer_32 once per frame (gaussian_render.py:37-67)"
-                                }[a.pipeline] + (" + fused refiner conv_body_first" if a.refine else ""),
+                                }[a.pipeline] + (" + fused refiner conv_body_first" if a.refine else "")
+                               + (" (assembly fused into the projection kernel)"
+                                  if getattr(w, "config_extra", {}).get("fused_deform") else ""),
                    "gaussians": P, "image": [W, H], "channels": C,
                    "frames_per_step_per_gpu": B, "global_batch": B * world,
                    "parallelism": f"frame-sharded x{world}" + (

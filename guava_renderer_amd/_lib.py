@@ -19,7 +19,7 @@ EXPORTS = ("gsr_version", "gsr_last_error", "gsr_geometry_bytes",
            # include/gsr_deform.h
            "gsr_lbs_workspace_bytes", "gsr_lbs", "gsr_lbs_sp", "gsr_blend_joints", "gsr_blend_joints_sp",
            "gsr_lbs_tiled_floats", "gsr_lbs_tile_bases",
-           "gsr_scratch_geometry", "gsr_scratch_binning", "gsr_scratch_image",
+           "gsr_scratch_geometry", "gsr_scratch_binning", "gsr_scratch_image", "gsr_forward_batch_deformed",
            "gsr_splice_head",
            "gsr_pack_rows", "gsr_deform_gaussians",
            # include/gsr_ssim.h
@@ -60,6 +60,15 @@ class Scratch(ctypes.Structure):
     """gsr_scratch (include/gsr.h): preallocated buffers for the three forward resizers."""
     _fields_ = [("geometry", _vp), ("geometry_cap", _sz), ("binning", _vp), ("binning_cap", _sz),
                 ("image", _vp), ("image_cap", _sz)]
+
+
+class DeformInputs(ctypes.Structure):
+    """GsrDeformInputs (include/gsr_deform.h): the assembly inputs of gsr_forward_batch_deformed."""
+    _fields_ = [("V", _i), ("F", _i), ("N", _i), ("pad_", _i), ("verts", _vp), ("vert_transforms", _vp),
+                ("faces", _vp), ("vtx_rotations", _vp), ("vtx_rot_stride", _i64), ("vtx_scales", _vp),
+                ("vtx_scale_stride", _i64), ("binding_face", _vp), ("face_bary", _vp), ("local_xyz", _vp),
+                ("local_stride", _i64), ("uv_rotations", _vp), ("uv_rot_stride", _i64), ("uv_scales", _vp),
+                ("uv_scale_stride", _i64), ("bad_index_flag", _vp)]
 
 
 class RowSegment(ctypes.Structure):
@@ -145,6 +154,9 @@ def load(path=None):
     L.gsr_forward_batch_refine.argtypes = list(L.gsr_forward_batch.argtypes[:-2]) + [
         ctypes.POINTER(RefineEpilogue), _u32, _vp]
     L.gsr_forward_batch_refine.restype = _i
+    L.gsr_forward_batch_deformed.argtypes = [_i, _i, _i, ctypes.POINTER(DeformInputs), _vp, _i64, _vp, _i64, _f,
+                                             _vp, _vp, _vp, _vp, _i64, _vp, _i64, _vp, _vp, _vp, _i, _u32, _vp]
+    L.gsr_forward_batch_deformed.restype = _i
     L.gsr_refine_prepare.argtypes = [_i, _vp, _vp, _i, _i, _vp, _vp]
     L.gsr_refine_prepare.restype = _i
     L.gsr_backward_batch.argtypes = [_i, _i, _i, _i, _vp, _i64, _vp, _i64, _vp, _i64, _vp, _i64, _vp,

@@ -98,11 +98,12 @@ class BatchRasterizer:
     def _inputs(self, means3D, colors, opacities, scales, rotations, viewmatrices, projmatrices,
                 tanfov, backgrounds):
         B, P, dev = self.B, self.P, self.device
-        m, sm = _frame_arg(means3D, B, P, 3, "means3D", dev)
+        none = (None, 0)  # geometry the fused avatar forward assembles on the device
+        m, sm = none if means3D is None else _frame_arg(means3D, B, P, 3, "means3D", dev)
         c, sc = _frame_arg(colors, B, P, C, "colors", dev, align16=True)
         o, so = _frame_arg(opacities, B, P, 1, "opacities", dev)
-        s, ss = _frame_arg(scales, B, P, 3, "scales", dev)
-        r, sr = _frame_arg(rotations, B, P, 4, "rotations", dev)
+        s, ss = none if scales is None else _frame_arg(scales, B, P, 3, "scales", dev)
+        r, sr = none if rotations is None else _frame_arg(rotations, B, P, 4, "rotations", dev)
         v = _frame_mat(viewmatrices, B, 16, "viewmatrices", dev)
         pm = _frame_mat(projmatrices, B, 16, "projmatrices", dev)
         tf = _frame_mat(tanfov, B, 2, "tanfov", dev)
@@ -118,8 +119,8 @@ class BatchRasterizer:
         else:
             raise ValueError(f"backgrounds: expected [{C}] or [{B},{C}], got {list(backgrounds.shape)}")
         keep = (m, c, o, s, r, v, pm, tf, bg)  # alive until the launches are enqueued
-        args = (B, P, self.W, self.H, m.data_ptr(), sm, c.data_ptr(), sc, o.data_ptr(), so,
-                s.data_ptr(), ss, r.data_ptr(), sr)
+        ptr = lambda t: None if t is None else t.data_ptr()  # noqa: E731
+        args = (B, P, self.W, self.H, ptr(m), sm, c.data_ptr(), sc, o.data_ptr(), so, ptr(s), ss, ptr(r), sr)
         return keep, args, (v.data_ptr(), pm.data_ptr(), tf.data_ptr(), bg.data_ptr(), bs)
 
     def _after_forward(self):
@@ -191,6 +192,39 @@ class BatchRasterizer:
             _lib.check(self.L.gsr_forward_batch_refine(*args, ctypes.byref(ep), nm, self._stream()),
                        "gsr_forward_batch_refine")
         del keep
+        self._after_forward()
+        return self.out_color, self.out_invdepth, self.radii
+
+    def forward_deformed(self, deformer, verts, vert_transforms, viewmatrices, projmatrices, tanfov, backgrounds,
+                         scale_modifier=1.0, antialiasing=False, numerics=None):
+        """The avatar pipeline's fused forward (include/gsr_deform.h gsr_forward_batch_deformed): the
+        B frames of `deformer` (deform.GaussianDeformer) on the deformed mesh verts [B,V,3] /
+        vert_transforms [B,V,4,4], rendered without materialising the deformed Gaussians (their
+        assembly feeds the projection in registers).  Same images as deformer.forward() + forward();
+        forward-only (a backward() after it raises)."""
+        self.poll()
+        nm = self.numerics if numerics is None else int(numerics)
+        self._fwd_only = True
+        dfm = deformer
+        B, P = self.B, self.P
+        if dfm.V + dfm.N != P:
+            raise ValueError(f"deformer has {dfm.V + dfm.N} Gaussians, the rasterizer {P}")
+        if tuple(verts.shape) != (B, dfm.V, 3) or tuple(vert_transforms.shape) != (B, dfm.V, 4, 4):
+            raise ValueError("verts / vert_transforms: expected [B,V,3] / [B,V,4,4]")
+        vb = verts.detach().to(torch.float32).contiguous()
+        vt = vert_transforms.detach().to(torch.float32).contiguous()
+        keep, head, (v, pm, tf, bg, bs) = self._inputs(None, dfm.colors, dfm.opacity, None, None, viewmatrices,
+                                                       projmatrices, tanfov, backgrounds)
+        di = _lib.DeformInputs(dfm.V, dfm.faces.shape[0], dfm.N, 0, vb.data_ptr(), vt.data_ptr(),
+                               dfm.faces.data_ptr(), dfm.v_rot.data_ptr(), 0, dfm.v_scale.data_ptr(), 0,
+                               dfm.bind.data_ptr(), dfm.bary.data_ptr(), dfm.u_local.data_ptr(), 0,
+                               dfm.u_rot.data_ptr(), 0, dfm.u_scale.data_ptr(), 0, dfm.bad.data_ptr())
+        _lib.check(self.L.gsr_forward_batch_deformed(
+            B, self.W, self.H, ctypes.byref(di), head[6], head[7], head[8], head[9], float(scale_modifier),
+            v, pm, tf, bg, bs, self.workspace.data_ptr(), self.R_capacity, self.out_color.data_ptr(),
+            self.out_invdepth.data_ptr(), self.radii.data_ptr(), int(bool(antialiasing)), nm, self._stream()),
+            "gsr_forward_batch_deformed")
+        del keep, vb, vt
         self._after_forward()
         return self.out_color, self.out_invdepth, self.radii
 

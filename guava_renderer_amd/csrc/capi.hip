@@ -9,6 +9,7 @@
 #include <vector>
 
 #include "../../include/gsr.h"
+#include "../../include/gsr_deform.h"
 #include "gsr_internal.h"
 
 using namespace gsr;
@@ -170,6 +171,10 @@ size_t carve_bin(char* base, int64_t R, BinArena* b) {
     if (b) *b = a;
     return align_up(off) + 256;
 }
+
+// the fused assembly + projection of the avatar pipeline (deform.hip)
+void launch_deform_preprocess(const Dims& d, const Inputs& in, const GeomArena& g, const Outputs& o,
+                              const GsrDeformInputs& dg, hipStream_t s);
 
 }  // namespace gsr
 
@@ -496,16 +501,15 @@ int gsr_forward_batch(int B, int P, int width, int height, const float* means3D,
                                     antialiasing, nullptr, numerics, stream);
 }
 
-int gsr_forward_batch_refine(int B, int P, int width, int height, const float* means3D,
-                             int64_t means_stride, const float* colors, int64_t colors_stride,
-                             const float* opacities, int64_t opac_stride, const float* scales,
-                             int64_t scales_stride, const float* rotations, int64_t rot_stride,
-                             float scale_modifier, const float* viewmatrices, const float* projmatrices,
-                             const float* tanfov, const float* backgrounds, int64_t bg_stride,
-                             char* workspace, int64_t R_capacity, float* out_color, float* out_invdepth,
-                             int* radii, int antialiasing, const gsr_refine_epilogue* refine,
-                             uint32_t numerics, void* stream) {
-    hipStream_t s = (hipStream_t)stream;
+static int forward_batch_impl(int B, int P, int width, int height, const float* means3D,
+                              int64_t means_stride, const float* colors, int64_t colors_stride,
+                              const float* opacities, int64_t opac_stride, const float* scales,
+                              int64_t scales_stride, const float* rotations, int64_t rot_stride,
+                              float scale_modifier, const float* viewmatrices, const float* projmatrices,
+                              const float* tanfov, const float* backgrounds, int64_t bg_stride,
+                              char* workspace, int64_t R_capacity, float* out_color, float* out_invdepth,
+                              int* radii, int antialiasing, const gsr_refine_epilogue* refine,
+                              uint32_t numerics, const GsrDeformInputs* dg, hipStream_t s) {
     if (numerics & ~kForwardBatchKnown) return fail(GSR_ERR_ARG, "unknown numerics flags");
     if (refine) {
         if (!refine->out_refine || refine->n_out < 1 || refine->keep_channels < 0 ||
@@ -548,11 +552,58 @@ int gsr_forward_batch_refine(int B, int P, int width, int height, const float* m
         o.slope = refine->negative_slope;
     }
     HIP_TRY(hipMemsetAsync(g.ctrl, 0, ctrl_words(d) * 4, s));
-    { StageTimer st_(0, s); launch_preprocess(d, in, g, o, s); }
+    if (dg) {
+        in.fwd_only = 1;  // (the deformed attributes are not kept: no backward can use the workspace)
+        StageTimer st_(0, s);
+        launch_deform_preprocess(d, in, g, o, *dg, s);
+    } else {
+        StageTimer st_(0, s);
+        launch_preprocess(d, in, g, o, s);
+    }
     { StageTimer st_(1, s); launch_scan_blocksums(d, g, R_capacity, s); }
     int rc = run_binning_and_render(d, in, g, im, bn, o, numerics, 0, s);
     if (rc < 0) return rc;
     return 0;
+}
+
+int gsr_forward_batch_refine(int B, int P, int width, int height, const float* means3D,
+                             int64_t means_stride, const float* colors, int64_t colors_stride,
+                             const float* opacities, int64_t opac_stride, const float* scales,
+                             int64_t scales_stride, const float* rotations, int64_t rot_stride,
+                             float scale_modifier, const float* viewmatrices, const float* projmatrices,
+                             const float* tanfov, const float* backgrounds, int64_t bg_stride,
+                             char* workspace, int64_t R_capacity, float* out_color, float* out_invdepth,
+                             int* radii, int antialiasing, const gsr_refine_epilogue* refine,
+                             uint32_t numerics, void* stream) {
+    return forward_batch_impl(B, P, width, height, means3D, means_stride, colors, colors_stride, opacities,
+                              opac_stride, scales, scales_stride, rotations, rot_stride, scale_modifier,
+                              viewmatrices, projmatrices, tanfov, backgrounds, bg_stride, workspace, R_capacity,
+                              out_color, out_invdepth, radii, antialiasing, refine, numerics, nullptr,
+                              (hipStream_t)stream);
+}
+
+int gsr_forward_batch_deformed(int B, int width, int height, const GsrDeformInputs* dg, const float* colors,
+                               int64_t colors_stride, const float* opacities, int64_t opac_stride,
+                               float scale_modifier, const float* viewmatrices, const float* projmatrices,
+                               const float* tanfov, const float* backgrounds, int64_t bg_stride,
+                               char* workspace, int64_t R_capacity, float* out_color, float* out_invdepth,
+                               int* radii, int antialiasing, uint32_t numerics, void* stream) {
+    if (!dg || dg->V < 0 || dg->N < 0 || dg->F < 0 || dg->V + dg->N == 0 || !dg->verts)
+        return fail(GSR_ERR_ARG, "gsr_forward_batch_deformed: bad deform inputs");
+    if (dg->V > 0 && (!dg->vert_transforms || !dg->vtx_rotations || !dg->vtx_scales))
+        return fail(GSR_ERR_ARG, "gsr_forward_batch_deformed: vertex Gaussians need transforms, rotations, scales");
+    if (dg->N > 0 && (!dg->faces || !dg->binding_face || !dg->face_bary || !dg->local_xyz || !dg->uv_rotations ||
+                      !dg->uv_scales || dg->F == 0))
+        return fail(GSR_ERR_ARG, "gsr_forward_batch_deformed: UV Gaussians need faces and binding data");
+    auto bad_stride = [](int64_t st, int64_t full) { return st != 0 && st != full; };
+    if (bad_stride(dg->vtx_rot_stride, 4LL * dg->V) || bad_stride(dg->vtx_scale_stride, 3LL * dg->V) ||
+        bad_stride(dg->local_stride, 3LL * dg->N) || bad_stride(dg->uv_rot_stride, 4LL * dg->N) ||
+        bad_stride(dg->uv_scale_stride, 3LL * dg->N))
+        return fail(GSR_ERR_ARG, "gsr_forward_batch_deformed: strides must be 0 or a whole frame");
+    return forward_batch_impl(B, dg->V + dg->N, width, height, nullptr, 0, colors, colors_stride, opacities,
+                              opac_stride, nullptr, 0, nullptr, 0, scale_modifier, viewmatrices, projmatrices,
+                              tanfov, backgrounds, bg_stride, workspace, R_capacity, out_color, out_invdepth, radii,
+                              antialiasing, nullptr, numerics | GSR_FORWARD_ONLY, dg, (hipStream_t)stream);
 }
 
 int gsr_refine_prepare(int n, const float* rows, const float* weight, int n_out, int keep_channels,

@@ -33,6 +33,7 @@
 #include "../../include/gsr.h"
 #include "../../include/gsr_deform.h"
 #include "gsr_internal.h"
+#include "preprocess_dev.h"
 
 namespace gsr {
 
@@ -951,6 +952,118 @@ __global__ __launch_bounds__(256) void k_deform_gaussians(
             for (int c = 0; c < 3; c++) scales[3 * o + c] = us[c] * s;
         }
     }
+}
+
+// The avatar pipeline's fused forward (gsr_forward_batch_deformed): k_deform_gaussians' assembly of
+// each (Gaussian, frame) -- the same face-frame sharing and the same expressions -- handed in
+// registers to the projection of k_preprocess (preprocess_dev.h), which writes the geometry rows
+// and the per-block summaries of the frame.  Gaussian blocks of kScanBlock = 256 (the workgroup) are
+// preprocess's blocks, so the block summaries index as k_preprocess's.
+__global__ __launch_bounds__(256) void k_deform_preprocess(int fpw, GsrDeformInputs dg, Dims d, Inputs in,
+                                                           GeomArena g, Outputs o) {
+    __shared__ float fr_lds[256 * kFrStride];
+    __shared__ int range[2];
+    const int V = dg.V, F = dg.F, N = dg.N, P = V + N;
+    const int32_t* __restrict__ faces = dg.faces;
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    const bool uv = i >= V && i < P;
+    const int n = i - V;
+    int f = -1, j0 = 0, j1 = 0, j2 = 0;
+    if (uv) {
+        const int bf = dg.binding_face[n];
+        if (bf >= 0 && bf < F) {
+            const int a = faces[3 * bf], c = faces[3 * bf + 1], e = faces[3 * bf + 2];
+            if (a >= 0 && a < V && c >= 0 && c < V && e >= 0 && e < V) { f = bf; j0 = a; j1 = c; j2 = e; }
+        }
+        if (f < 0 && dg.bad_index_flag) atomicOr(dg.bad_index_flag, 1u);
+    }
+    float w0 = 0.f, w1 = 0.f, w2 = 0.f;
+    if (uv) { w0 = dg.face_bary[3 * n]; w1 = dg.face_bary[3 * n + 1]; w2 = dg.face_bary[3 * n + 2]; }
+    if (threadIdx.x == 0) { range[0] = INT_MAX; range[1] = -1; }
+    __syncthreads();
+    if (f >= 0) { atomicMin(&range[0], f); atomicMax(&range[1], f); }
+    __syncthreads();
+    const int fmin = range[0], nf = range[1] - range[0] + 1;
+    const bool shared_frames = range[1] >= 0 && nf <= 256;
+    int t0 = -1, t1 = 0, t2 = 0;
+    if (shared_frames && (int)threadIdx.x < nf) {
+        const int ff = fmin + threadIdx.x;
+        const int a = faces[3 * ff], c = faces[3 * ff + 1], e = faces[3 * ff + 2];
+        if (a >= 0 && a < V && c >= 0 && c < V && e >= 0 && e < V) { t0 = a; t1 = c; t2 = e; }
+    }
+    const int b1 = min(d.B, (int)(blockIdx.y + 1) * fpw);
+    for (int b = blockIdx.y * fpw; b < b1; b++) {
+        const float* vb = dg.verts + (int64_t)b * V * 3;
+        if (shared_frames) {
+            if (b > (int)blockIdx.y * fpw) __syncthreads();
+            if (t0 >= 0) face_frame(vb, t0, t1, t2, fr_lds + threadIdx.x * kFrStride);
+            __syncthreads();
+        }
+        // the frame's depth-bucket counters (k_preprocess's duty)
+        for (int k = i; k <= d.NB; k += d.nblk * kScanBlock) g.bstart[(int64_t)b * (d.NB + 1) + k] = 0u;
+        const int64_t gid = (int64_t)b * P + i;
+        uint32_t tiles = 0;
+        if (i < P) {
+            float mo[3], so[3], qq[4];
+            if (i < V) {
+                const float4* tv = reinterpret_cast<const float4*>(dg.vert_transforms + ((int64_t)b * V + i) * 16);
+                const float4 r0 = tv[0], r1 = tv[1], r2 = tv[2];
+                const float m[9] = {r0.x, r0.y, r0.z, r1.x, r1.y, r1.z, r2.x, r2.y, r2.z};
+                const float4 qd = rotmat_to_unitquat(m);
+                const float* qv = dg.vtx_rotations + b * dg.vtx_rot_stride + 4 * (int64_t)i;  // wxyz
+                const float4 q = quat_product(qd, make_float4(qv[1], qv[2], qv[3], qv[0]));
+                const float nn = fmaxf(sqrtf(((q.w * q.w + q.x * q.x) + q.y * q.y) + q.z * q.z), 1e-12f);
+                qq[0] = q.w / nn; qq[1] = q.x / nn; qq[2] = q.y / nn; qq[3] = q.z / nn;
+                for (int c = 0; c < 3; c++) {
+                    mo[c] = vb[3 * i + c];
+                    so[c] = dg.vtx_scales[b * dg.vtx_scale_stride + 3 * (int64_t)i + c];
+                }
+            } else if (f < 0) {
+                const float nan = __int_as_float(0x7fc00000);
+                for (int c = 0; c < 3; c++) { mo[c] = nan; so[c] = nan; }
+                for (int c = 0; c < 4; c++) qq[c] = nan;
+            } else {
+                float fr[14];
+                if (shared_frames) {
+                    const float* src = fr_lds + (f - fmin) * kFrStride;
+#pragma unroll
+                    for (int k = 0; k < 14; k++) fr[k] = src[k];
+                } else {
+                    face_frame(vb, j0, j1, j2, fr);
+                }
+                const float s = fr[9];
+                const float* qu = dg.uv_rotations + b * dg.uv_rot_stride + 4 * (int64_t)n;  // wxyz
+                const float4 q = quat_product(make_float4(fr[10], fr[11], fr[12], fr[13]),
+                                              make_float4(qu[1], qu[2], qu[3], qu[0]));
+                qq[0] = q.w; qq[1] = q.x; qq[2] = q.y; qq[3] = q.z;
+                const float* l = dg.local_xyz + b * dg.local_stride + 3 * (int64_t)n;
+                const float lx = l[0], ly = l[1], lz = l[2];
+                const float cx = (w0 * vb[3 * j0] + w1 * vb[3 * j1]) + w2 * vb[3 * j2];
+                const float cy = (w0 * vb[3 * j0 + 1] + w1 * vb[3 * j1 + 1]) + w2 * vb[3 * j2 + 1];
+                const float cz = (w0 * vb[3 * j0 + 2] + w1 * vb[3 * j1 + 2]) + w2 * vb[3 * j2 + 2];
+                mo[0] = dot3(fr[0], fr[1], fr[2], lx, ly, lz) * s + cx;
+                mo[1] = dot3(fr[3], fr[4], fr[5], lx, ly, lz) * s + cy;
+                mo[2] = dot3(fr[6], fr[7], fr[8], lx, ly, lz) * s + cz;
+                const float* us = dg.uv_scales + b * dg.uv_scale_stride + 3 * (int64_t)n;
+                for (int c = 0; c < 3; c++) so[c] = us[c] * s;
+            }
+            tiles = preprocess_one(d, in, g, o, b, gid, mo, nullptr, so, qq, in.opac[in.s_opac * b + i]);
+        }
+        preprocess_block_sums(d, g, b, blockIdx.x, tiles, gid);
+    }
+    if (threadIdx.x == 0 && blockIdx.x == 0 && blockIdx.y == 0) g.ctrl[kCtrlFwdOnly] = 1u;
+}
+
+void launch_deform_preprocess(const Dims& d, const Inputs& in, const GeomArena& g, const Outputs& o,
+                              const GsrDeformInputs& dg, hipStream_t s) {
+    if (d.P == 0 || d.B == 0) return;
+    static const int fpw = [] {
+        const char* e = getenv("GSR_DEFORM_FRAMES");
+        const int v = e ? atoi(e) : kDeformFrames;
+        return v >= 1 && v <= 64 ? v : 1;
+    }();
+    hipLaunchKernelGGL(k_deform_preprocess, dim3(d.nblk, (d.B + fpw - 1) / fpw), dim3(256), 0, s, fpw, dg, d, in,
+                       g, o);
 }
 
 struct PackTable {

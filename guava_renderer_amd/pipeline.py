@@ -42,10 +42,19 @@ class AvatarPipeline:
         e = self.ehm(body_params, flame_params)
         return self.gauss(e["vertices"], e["ver_transform_mat"])
 
-    def render(self, body_params, flame_params, views, projs, tanfov, refine=None):
+    def render(self, body_params, flame_params, views, projs, tanfov, refine=None, fused=False):
         """views / projs [B,16] (graphics_utils.py:44-50 layout), tanfov [B,2] ->
         (color [B,32,H,W], invdepth [B,H,W], radii [B,P], deformed assets).  refine: optional
-        batch.RefineHead (the refiner's first conv fused into the render; output in refine.out)."""
+        batch.RefineHead (the refiner's first conv fused into the render; output in refine.out).
+        fused: the Gaussian assembly runs inside the projection kernel (gsr_forward_batch_deformed);
+        the images are the same, the deformed assets are not materialised (returned as None)."""
+        if fused:
+            if refine is not None:
+                raise ValueError("fused=True has no refiner epilogue; pass fused=False with refine")
+            e = self.ehm(body_params, flame_params)
+            col, inv, radii = self.rast.forward_deformed(self.gauss, e["vertices"], e["ver_transform_mat"], views,
+                                                         projs, tanfov, self.bg)
+            return col, inv, radii, None
         d = self.deform(body_params, flame_params)
         col, inv, radii = self.rast.forward(d["xyz"], self.gauss.colors, self.gauss.opacity,
                                             d["scaling"], d["rotation"], views, projs, tanfov, self.bg,

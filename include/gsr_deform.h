@@ -128,6 +128,35 @@ int gsr_splice_head(int B, int V_body, int N_head, const int32_t* head_index, co
                     const float* body_joints, int J_body, int bj0, int bj1, float* body_v_shaped,
                     uint32_t* bad_index_flag, void* stream);
 
+/* The avatar pipeline's fused forward (round 4): gsr_forward_batch for the Gaussians of
+ * gsr_deform_gaussians WITHOUT materialising them -- one kernel assembles each (Gaussian, frame)'s
+ * mean, rotation and scale from the deformed mesh (ubody_gaussian.py:252-278) and projects it
+ * (forward.cu:151-269) from registers, so the 40 B per Gaussian-frame the assembly would write and
+ * preprocess would read never reach HBM.  P = V + N Gaussians, vertex ones first; colors / opacities
+ * [P,k] (stride 0) or [B,P,k] as in gsr_forward_batch.  Images identical to gsr_deform_gaussians +
+ * gsr_forward_batch (same kernels' arithmetic).  Forward-only (GSR_FORWARD_ONLY is implied: no backward
+ * can use the workspace, the deformed attributes are not kept). */
+typedef struct {
+    int V, F, N, pad_;
+    const float* verts;            /* [B,V,3] deformed mesh (EHM vertices) */
+    const float* vert_transforms;  /* [B,V,4,4] */
+    const int32_t* faces;          /* [F,3] */
+    const float* vtx_rotations; int64_t vtx_rot_stride;   /* [V,4] wxyz (stride 0) or per frame */
+    const float* vtx_scales; int64_t vtx_scale_stride;
+    const int32_t* binding_face;   /* [N] */
+    const float* face_bary;        /* [N,3] */
+    const float* local_xyz; int64_t local_stride;
+    const float* uv_rotations; int64_t uv_rot_stride;
+    const float* uv_scales; int64_t uv_scale_stride;
+    uint32_t* bad_index_flag;      /* ORed with 1 on an out-of-range binding (those Gaussians NaN) */
+} GsrDeformInputs;
+int gsr_forward_batch_deformed(int B, int width, int height, const GsrDeformInputs* dg, const float* colors,
+                               int64_t colors_stride, const float* opacities, int64_t opac_stride,
+                               float scale_modifier, const float* viewmatrices, const float* projmatrices,
+                               const float* tanfov, const float* backgrounds, int64_t bg_stride,
+                               char* workspace, int64_t R_capacity, float* out_color, float* out_invdepth,
+                               int* radii, int antialiasing, uint32_t numerics, void* stream);
+
 /* One segment of gsr_pack_rows: for every frame b, dst[b * dst_stride + c] = src[b * src_stride + c]
  * for c in [0, width) (src == NULL writes zeros; src_stride 0 broadcasts one row to every frame). */
 typedef struct {

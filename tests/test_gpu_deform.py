@@ -345,3 +345,64 @@ def test_config5_cross_reenactment_avatar_pipeline():
     np.testing.assert_array_equal(radii[f].cpu().numpy(), o_radii)
     np.testing.assert_array_equal(col[f].cpu().numpy(), o_col)
     np.testing.assert_array_equal(inv[f].cpu().numpy(), o_inv.reshape(W, W))
+    # the fused forward (assembly inside the projection kernel, gsr_forward_batch_deformed): the
+    # same images from the same EHM output, without materialising the deformed Gaussians
+    c0, i0, r0 = col.clone(), inv.clone(), radii.clone()
+    col2, inv2, radii2, d2 = pipe.render(gbp, gfp, views, projs, tanf, fused=True)
+    torch.cuda.synchronize()
+    assert d2 is None and not pipe.rast.status()[1]
+    assert torch.equal(radii2, r0) and torch.equal(col2, c0) and torch.equal(inv2, i0)
+
+
+def test_fused_deform_forward_equals_two_step_and_flags_bad_index():
+    """gsr_forward_batch_deformed vs gsr_deform_gaussians + gsr_forward_batch on a small avatar
+    (B=3, shared and per-frame cameras): identical images, invdepth and radii; an out-of-range
+    binding face is flagged and its Gaussian dropped (NaN centre, radius 0) without a fault; a
+    backward after the fused forward is refused."""
+    from guava_renderer_amd import deform, scenes
+    from guava_renderer_amd._lib import GsrError
+    from guava_renderer_amd.batch import BatchRasterizer
+    rng = np.random.default_rng(3)
+    V, F, N, B, W = 400, 600, 1500, 3, 96
+    faces = np.stack([rng.choice(V, 3, replace=False) for _ in range(F)]).astype(np.int32)
+    bind = rng.integers(0, F, N).astype(np.int32)
+    bind[17] = F + 3  # out of range
+
+    def quats(n):
+        q = rng.normal(size=(n, 4)).astype(np.float32)
+        return q / np.linalg.norm(q, axis=1, keepdims=True)
+
+    dfm = deform.GaussianDeformer(
+        {"rotations": _t(quats(V)), "scales": _t(rng.uniform(0.005, 0.03, (V, 3)).astype(np.float32)),
+         "opacities": _t(rng.uniform(0.2, 0.95, (V, 1)).astype(np.float32)),
+         "colors": _t(rng.uniform(0, 1, (V, 32)).astype(np.float32))},
+        {"rotations": _t(quats(N)), "scales": _t(rng.uniform(0.1, 1.5, (N, 3)).astype(np.float32)),
+         "opacities": _t(rng.uniform(0.2, 0.95, (N, 1)).astype(np.float32)),
+         "colors": _t(rng.uniform(0, 1, (N, 32)).astype(np.float32)),
+         "local_pos": _t(rng.normal(scale=0.01, size=(N, 3)).astype(np.float32)), "binding_face": _t(bind),
+         "face_bary": _t(rng.dirichlet(np.ones(3), N).astype(np.float32))}, _t(faces))
+    verts = _t(rng.normal(scale=0.25, size=(B, V, 3)).astype(np.float32))
+    T = np.broadcast_to(np.eye(4, dtype=np.float32), (B, V, 4, 4)).copy()
+    T[..., :3, :3] += rng.normal(scale=0.1, size=(B, V, 3, 3)).astype(np.float32)
+    T = _t(T)
+    cams = scenes.frame_cameras(B, W, W, seed=5)
+    views = _t(np.stack([c["viewmatrix"].reshape(16) for c in cams]))
+    projs = _t(np.stack([c["projmatrix"].reshape(16) for c in cams]))
+    tanf = _t(np.array([[c["tanfovx"], c["tanfovy"]] for c in cams], np.float32))
+    bg = _t(rng.uniform(0, 1, (B, 32)).astype(np.float32))
+    P = V + N
+    rast = BatchRasterizer(B, P, W, W, R_capacity=64 * P * B, device=DEV)
+    d = dfm(verts, T)
+    col, inv, radii = rast.forward(d["xyz"], dfm.colors, dfm.opacity, d["scaling"], d["rotation"], views, projs,
+                                   tanf, bg, forward_only=True)
+    c0, i0, r0 = col.clone(), inv.clone(), radii.clone()
+    assert dfm.bad_index()
+    dfm.bad.zero_()
+    col2, inv2, radii2 = rast.forward_deformed(dfm, verts, T, views, projs, tanf, bg)
+    torch.cuda.synchronize()
+    assert dfm.bad_index() and not rast.status()[1]
+    assert (r0 > 0).sum() > P // 2 and r0[:, V + 17].eq(0).all()
+    assert torch.equal(radii2, r0) and torch.equal(col2, c0) and torch.equal(inv2, i0)
+    with pytest.raises(GsrError):
+        rast.backward(d["xyz"], dfm.colors, dfm.opacity, d["scaling"], d["rotation"], views, projs, tanf, bg,
+                      torch.ones_like(col2), torch.zeros_like(inv2))
