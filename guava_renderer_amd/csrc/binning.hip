@@ -482,8 +482,25 @@ void launch_depth_sort(const Dims& d, const GeomArena& g, hipStream_t s) {
 }
 
 // ---------------------------------------------------------------- 3. instance count table
+// Inclusive scan over aligned 8-lane groups: DPP row_shr inside the 16-lane rows, a lane whose source
+// lies in the previous group adds nothing (three VALU steps, no LDS permutes).
+__device__ __forceinline__ int scan8(int v) {
+    const int l8 = threadIdx.x & 7;
+    int t = __builtin_amdgcn_update_dpp(0, v, 0x111, 0xF, 0xF, false);  // row_shr:1
+    v += l8 >= 1 ? t : 0;
+    t = __builtin_amdgcn_update_dpp(0, v, 0x112, 0xF, 0xF, false);  // row_shr:2
+    v += l8 >= 2 ? t : 0;
+    t = __builtin_amdgcn_update_dpp(0, v, 0x114, 0xF, 0xF, false);  // row_shr:4
+    v += l8 >= 4 ? t : 0;
+    return v;
+}
+
 // Tile histogram of one chunk of d.chunk depth-ordered Gaussians: each rect adds +1/-1 at its four
 // corners of a (gx+1) x (gy+1) difference array in LDS; a 2-D prefix sum gives the per-tile counts.
+// GROUP8 (default): the prefix sums by 8-lane groups, one row (then one column) per group, each lane
+// summing a run of ceil(n/8) cells and the 8 run sums scanned with DPP -- every row at once instead
+// of one row per wave at a time with a 6-step LDS-permute scan (the kernel's VALU and LDS waits).
+template <bool GROUP8>
 __global__ __launch_bounds__(kScanBlock) void k_chunk_count(Dims d, GeomArena g) {
     extern __shared__ int diff[];  // (gx+1)*(gy+1)
     if (g.ctrl[kCtrlOverflow]) return;
@@ -509,6 +526,37 @@ __global__ __launch_bounds__(kScanBlock) void k_chunk_count(Dims d, GeomArena g)
     // 2-D inclusive prefix of the difference array, one wave per row (lanes along x), then one wave
     // per column (lanes along y; the odd pitch W1 keeps the column reads conflict-free), 64
     // elements per step with the carry in a register; then the table row is written coalesced
+    if (GROUP8) {
+        const int g8 = threadIdx.x >> 3, l8 = threadIdx.x & 7;
+        const int cx = (d.gx + 7) >> 3, cy = (d.gy + 7) >> 3;
+        for (int y = g8; y < d.gy; y += kScanBlock / 8) {  // (whole 8-lane groups take a row or not)
+            int* rowp = diff + y * W1;
+            const int x0 = l8 * cx, x1 = min(d.gx, x0 + cx);
+            int s = 0;
+            for (int x = x0; x < x1; x++) s += rowp[x];
+            int run = scan8(s) - s;
+            for (int x = x0; x < x1; x++) { run += rowp[x]; rowp[x] = run; }
+        }
+        __syncthreads();
+        for (int x = g8; x < d.gx; x += kScanBlock / 8) {
+            const int y0 = l8 * cy, y1 = min(d.gy, y0 + cy);
+            int s = 0;
+            for (int y = y0; y < y1; y++) s += diff[y * W1 + x];
+            int run = scan8(s) - s;
+            for (int y = y0; y < y1; y++) { run += diff[y * W1 + x]; diff[y * W1 + x] = run; }
+        }
+        __syncthreads();
+        uint32_t* row = g.table + ((int64_t)b * d.nchunk + c) * d.T;
+        const int sy = kScanBlock / d.gx, sx = kScanBlock - sy * d.gx;
+        int y = threadIdx.x / d.gx, x = threadIdx.x - y * d.gx;
+        for (int t = threadIdx.x; t < d.T; t += kScanBlock) {
+            row[t] = (uint32_t)diff[y * W1 + x];
+            x += sx;
+            y += sy;
+            if (x >= d.gx) { x -= d.gx; y++; }
+        }
+        return;
+    }
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     constexpr int kWaves = kScanBlock / 64;
     for (int y = wv; y < d.gy; y += kWaves) {
@@ -611,9 +659,12 @@ void launch_chunk_count(const Dims& d, const GeomArena& g, const ImageArena& im,
     static size_t attr = 0;
     if (lds > 65536 && attr < lds) {
         attr = lds;
-        hipFuncSetAttribute((const void*)k_chunk_count, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        hipFuncSetAttribute((const void*)k_chunk_count<true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        hipFuncSetAttribute((const void*)k_chunk_count<false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     }
-    hipLaunchKernelGGL(k_chunk_count, dim3(d.nchunk, d.B), dim3(kScanBlock), lds, s, d, g);
+    static const bool g8 = [] { const char* e = getenv("GSR_CHUNK_SCAN8"); return !(e && e[0] == '0'); }();
+    if (g8) hipLaunchKernelGGL(k_chunk_count<true>, dim3(d.nchunk, d.B), dim3(kScanBlock), lds, s, d, g);
+    else hipLaunchKernelGGL(k_chunk_count<false>, dim3(d.nchunk, d.B), dim3(kScanBlock), lds, s, d, g);
     hipLaunchKernelGGL(k_column_scan_wide, dim3((d.T + 63) / 64, d.B), dim3(64 * kColWaves), 0, s, d, g, im);
 }
 

@@ -29,7 +29,8 @@ for f in glob.glob(o + "/**/*counter_collection.csv", recursive=True):
             acc[m.group(1)][r["Counter_Name"]].append(float(r["Counter_Value"]))
 res = {k: {c: (sum(v[1:]) / (len(v) - 1) if len(v) > 1 else v[0]) for c, v in cs.items()} for k, cs in acc.items()}
 json.dump(res, open(o + "/summary.json", "w"), indent=1)
-for k in ("k_render_fwd", "k_ordered_scatter", "k_chunk_count"):
+import os
+for k in os.environ.get("KERNELS", "k_render_fwd k_ordered_scatter k_chunk_count").split():
     c = res.get(k)
     if not c:
         continue
@@ -44,6 +45,9 @@ for k in ("k_render_fwd", "k_ordered_scatter", "k_chunk_count"):
         "wait_lds_frac": g("SQ_WAIT_INST_LDS") / max(g("SQ_WAVE_CYCLES"), 1),
         "wait_any_frac": g("SQ_WAIT_ANY") / max(g("SQ_WAVE_CYCLES"), 1),
         "lds_bank_conflict_per_lds_inst": g("SQ_LDS_BANK_CONFLICT") / max(g("SQ_INSTS_LDS"), 1),
+        "valu_insts": g("SQ_INSTS_VALU"), "salu_insts": g("SQ_INSTS_SALU"), "vmem_insts": g("SQ_INSTS_VMEM"),
+        "active_valu_per_wave_cycle": g("SQ_ACTIVE_INST_VALU") / max(g("SQ_WAVE_CYCLES"), 1),
+        "busy_cycles": g("SQ_BUSY_CYCLES"),
     }
     print(k, {a: round(b, 3) for a, b in out.items()})
 PY
