@@ -1052,52 +1052,6 @@ __global__ __launch_bounds__(256) void k_strip_count(Dims d, ImageArena im, BinA
     }
 }
 
-// 16 lanes per tile (four tiles per wave): the same counts with a quarter of the waves; a mean list
-// (~750 entries) is 1-2 rounds of 8 uint4 loads per lane either way, so one wave per tile left
-// most of its lanes' loads masked.
-__global__ __launch_bounds__(256) void k_strip_count16(Dims d, ImageArena im, BinArena bn) {
-    const int tile_g = (int)((blockIdx.x * 256u + threadIdx.x) >> 4);
-    const int lane = threadIdx.x & 15;
-    const bool ok = tile_g < d.B * d.T;
-    uint32_t c[kStrips] = {};
-    if (ok) {
-        const uint2 r = im.ranges[tile_g];
-        const uint32_t a4 = min((r.x + 3u) & ~3u, r.y), b4 = max(r.y & ~3u, a4);
-        if (r.x + (uint32_t)lane < a4) { const uint32_t e = bn.point_list[r.x + lane];
-#pragma unroll
-            for (int s = 0; s < kStrips; s++) c[s] += (e >> (28 + s)) & 1u; }
-        if (b4 + (uint32_t)lane < r.y) { const uint32_t e = bn.point_list[b4 + lane];
-#pragma unroll
-            for (int s = 0; s < kStrips; s++) c[s] += (e >> (28 + s)) & 1u; }
-        const uint4* __restrict__ q = reinterpret_cast<const uint4*>(bn.point_list + a4);
-        const uint32_t n4 = (b4 - a4) >> 2;
-        for (uint32_t i = lane; i < n4; i += 128) {
-            uint4 e[8];
-#pragma unroll
-            for (int u = 0; u < 8; u++) e[u] = i + 16u * u < n4 ? q[i + 16u * u] : make_uint4(0u, 0u, 0u, 0u);
-#pragma unroll
-            for (int u = 0; u < 8; u++)
-#pragma unroll
-                for (int s = 0; s < kStrips; s++)
-                    c[s] += ((e[u].x >> (28 + s)) & 1u) + ((e[u].y >> (28 + s)) & 1u) + ((e[u].z >> (28 + s)) & 1u) +
-                            ((e[u].w >> (28 + s)) & 1u);
-        }
-    }
-#pragma unroll
-    for (int s = 0; s < kStrips; s++) {
-        uint32_t v = c[s];
-#pragma unroll
-        for (int off = 8; off > 0; off >>= 1) v += __shfl_xor(v, off);
-        c[s] = v;
-    }
-    if (ok && lane < kStrips) {
-        uint32_t v = c[0];
-#pragma unroll
-        for (int s = 1; s < kStrips; s++) v = lane == s ? c[s] : v;
-        im.strip_cnt[(int64_t)tile_g * kStrips + lane] = v;
-    }
-}
-
 // Per frame: histogram of its non-empty tiles' strips over the buckets.
 __device__ __forceinline__ uint32_t tile_strip_max(const ImageArena& im, int64_t tg) {
     uint32_t m = 0;
@@ -1312,9 +1266,7 @@ void launch_strip_order(const Dims& d, const GeomArena& g, const ImageArena& im,
                         hipStream_t s) {
     if (d.B == 0 || d.T == 0) return;
     const int nt = d.B * d.T;
-    static const bool sub16 = [] { const char* e = getenv("GSR_STRIP_COUNT16"); return e && e[0] == '1'; }();
-    if (sub16) hipLaunchKernelGGL(k_strip_count16, dim3((nt + 15) / 16), dim3(256), 0, s, d, im, b);
-    else hipLaunchKernelGGL(k_strip_count, dim3((nt + 3) / 4), dim3(256), 0, s, d, im, b);
+    hipLaunchKernelGGL(k_strip_count, dim3((nt + 3) / 4), dim3(256), 0, s, d, im, b);
     const int tile_major = strip_order_tile_major();
     // (one frame: the tile-affine walk of one longest-first list, measured 1.5% faster there)
     const int map = tile_major ? (d.B == 1 ? 1 : xcd_queue_map()) : 0;

@@ -286,60 +286,16 @@ __global__ __launch_bounds__(256) void k_lbs_blend_mfma(int B, int M, int NB, in
 // wave read (1 KB), where the k-major layout gives 4-byte lanes (256 B per load instruction): the
 // blend's bases stream at HBM rate with a quarter of the load instructions in flight.
 constexpr int kTiledUnroll = 4;  // tile groups whose loads are issued before their products
-#ifndef GSR_BLEND_PREFETCH
-#define GSR_BLEND_PREFETCH 1
-#endif
 
 // D[frame][m] over the k of one base: v_mfma_f32_32x32x2_f32 with lane (c, h) holding base[8g + 4h + j]
 // [32t + c] (B operand) and coef[frame b0 + c][8g + 4h + j] (A operand) for the j-th MFMA of a group
 // (the lane halves' k of one MFMA are 8g + j and 8g + 4 + j); wave w takes the groups g = w mod 4.
-// The next step's loads are issued before this step's products (two register stages): a wave's
-// load round trip then overlaps its own MFMAs instead of only the other waves'.
-__device__ __forceinline__ void blend_tiled_load(float4 (&v)[kTiledUnroll], float (&a)[kTiledUnroll][4],
-                                                 const float4* __restrict__ p, const float* __restrict__ cr,
-                                                 int g0, int nkg, int K, bool bok, int hi) {
-#pragma unroll
-    for (int u = 0; u < kTiledUnroll; u++) {
-        const int g = g0 + 4 * u;
-        v[u] = g < nkg ? p[(int64_t)g * 64] : make_float4(0.f, 0.f, 0.f, 0.f);
-#pragma unroll
-        for (int j = 0; j < 4; j++) {
-            const int k = 8 * g + 4 * hi + j;
-            a[u][j] = (bok && k < K) ? cr[k] : 0.f;
-        }
-    }
-}
-
 __device__ __forceinline__ void blend_tiled_mfma_part(floatx16& acc, const float* __restrict__ coef, int ncoef,
                                                       const float4* __restrict__ tb, int K, int t, int bA,
                                                       bool bok, int w, int hi, int lane) {
     const int nkg = (K + 7) / 8;
     const float4* __restrict__ p = tb + (int64_t)t * nkg * 64 + lane;
     const float* __restrict__ cr = coef + (int64_t)bA * ncoef;
-    if (GSR_BLEND_PREFETCH) {
-        float4 v[kTiledUnroll], vn[kTiledUnroll];
-        float a[kTiledUnroll][4], an[kTiledUnroll][4];
-        blend_tiled_load(v, a, p, cr, w, nkg, K, bok, hi);
-        for (int g0 = w; g0 < nkg; g0 += 4 * kTiledUnroll) {
-            const bool more = g0 + 4 * kTiledUnroll < nkg;  // (wave-uniform)
-            if (more) blend_tiled_load(vn, an, p, cr, g0 + 4 * kTiledUnroll, nkg, K, bok, hi);
-#pragma unroll
-            for (int u = 0; u < kTiledUnroll; u++) {
-                acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a[u][0], v[u].x, acc, 0, 0, 0);
-                acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a[u][1], v[u].y, acc, 0, 0, 0);
-                acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a[u][2], v[u].z, acc, 0, 0, 0);
-                acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a[u][3], v[u].w, acc, 0, 0, 0);
-            }
-            if (!more) break;
-#pragma unroll
-            for (int u = 0; u < kTiledUnroll; u++) {
-                v[u] = vn[u];
-#pragma unroll
-                for (int j = 0; j < 4; j++) a[u][j] = an[u][j];
-            }
-        }
-        return;
-    }
     for (int g0 = w; g0 < nkg; g0 += 4 * kTiledUnroll) {
         float4 v[kTiledUnroll];
         float a[kTiledUnroll][4];
