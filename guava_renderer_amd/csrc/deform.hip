@@ -286,27 +286,51 @@ __global__ __launch_bounds__(256) void k_lbs_blend_mfma(int B, int M, int NB, in
 // wave read (1 KB), where the k-major layout gives 4-byte lanes (256 B per load instruction): the
 // blend's bases stream at HBM rate with a quarter of the load instructions in flight.
 constexpr int kTiledUnroll = 4;  // tile groups whose loads are issued before their products
+#ifndef GSR_BLEND_COEF_VEC
+#define GSR_BLEND_COEF_VEC 1
+#endif
 
 // D[frame][m] over the k of one base: v_mfma_f32_32x32x2_f32 with lane (c, h) holding base[8g + 4h + j]
 // [32t + c] (B operand) and coef[frame b0 + c][8g + 4h + j] (A operand) for the j-th MFMA of a group
 // (the lane halves' k of one MFMA are 8g + j and 8g + 4 + j); wave w takes the groups g = w mod 4.
+// The coefficient gathers (lane = frame row, 4 consecutive k) are 16- or 8-byte loads when the rows'
+// stride and base allow (vw = 4 / 2, wave-uniform): 16 scattered dword loads per step were the
+// texture path's load (TA 48% / TD 58% busy at 37% of HBM), four times the base tile's loads.
+__device__ __forceinline__ int coef_vec_width(const float* coef, int ncoef) {
+    if (((uintptr_t)coef & 15) == 0 && (ncoef & 3) == 0) return 4;
+    if (((uintptr_t)coef & 7) == 0 && (ncoef & 1) == 0) return 2;
+    return 1;
+}
+
 __device__ __forceinline__ void blend_tiled_mfma_part(floatx16& acc, const float* __restrict__ coef, int ncoef,
                                                       const float4* __restrict__ tb, int K, int t, int bA,
-                                                      bool bok, int w, int hi, int lane) {
+                                                      bool bok, int w, int hi, int lane, int nw = 4) {
     const int nkg = (K + 7) / 8;
+    const int nfull = GSR_BLEND_COEF_VEC ? K / 8 : 0;  // groups whose 8 k are all < K
+    const int vw = coef_vec_width(coef, ncoef);
     const float4* __restrict__ p = tb + (int64_t)t * nkg * 64 + lane;
     const float* __restrict__ cr = coef + (int64_t)bA * ncoef;
-    for (int g0 = w; g0 < nkg; g0 += 4 * kTiledUnroll) {
+    for (int g0 = w; g0 < nkg; g0 += nw * kTiledUnroll) {
         float4 v[kTiledUnroll];
         float a[kTiledUnroll][4];
 #pragma unroll
         for (int u = 0; u < kTiledUnroll; u++) {
-            const int g = g0 + 4 * u;
+            const int g = g0 + nw * u;
             v[u] = g < nkg ? p[(int64_t)g * 64] : make_float4(0.f, 0.f, 0.f, 0.f);
+            const int k0 = 8 * g + 4 * hi;
+            if (g < nfull && vw == 4) {
+                const float4 c = bok ? *reinterpret_cast<const float4*>(cr + k0) : make_float4(0.f, 0.f, 0.f, 0.f);
+                a[u][0] = c.x; a[u][1] = c.y; a[u][2] = c.z; a[u][3] = c.w;
+            } else if (g < nfull && vw == 2) {
+                const float2 c0 = bok ? *reinterpret_cast<const float2*>(cr + k0) : make_float2(0.f, 0.f);
+                const float2 c1 = bok ? *reinterpret_cast<const float2*>(cr + k0 + 2) : make_float2(0.f, 0.f);
+                a[u][0] = c0.x; a[u][1] = c0.y; a[u][2] = c1.x; a[u][3] = c1.y;
+            } else {
 #pragma unroll
-            for (int j = 0; j < 4; j++) {
-                const int k = 8 * g + 4 * hi + j;
-                a[u][j] = (bok && k < K) ? cr[k] : 0.f;
+                for (int j = 0; j < 4; j++) {
+                    const int k = k0 + j;
+                    a[u][j] = (bok && k < K) ? cr[k] : 0.f;
+                }
             }
         }
 #pragma unroll
@@ -320,8 +344,11 @@ __device__ __forceinline__ void blend_tiled_mfma_part(floatx16& acc, const float
 }
 
 // k_lbs_blend_mfma over the tiled bases: one workgroup per 32 coordinates x 32 frames, the same
-// wave-order reduction and epilogue.
-__global__ __launch_bounds__(256) void k_lbs_blend_tiled(int B, int M, int NB, int NP,
+// wave-order reduction and epilogue.  NW waves split the k groups (g = w mod NW): 8 when the grid
+// has at most 512 workgroups (the FLAME head, 471: 4 waves per workgroup left the SIMDs under two
+// waves each, every wave a long serial load -> MFMA chain), else 4.
+template <int NW>
+__global__ __launch_bounds__(64 * NW) void k_lbs_blend_tiled(int B, int M, int NB, int NP,
                                                          const float* __restrict__ vt, int64_t vt_stride,
                                                          const float* __restrict__ betas,
                                                          const float4* __restrict__ sd_tiled,
@@ -329,7 +356,7 @@ __global__ __launch_bounds__(256) void k_lbs_blend_tiled(int B, int M, int NB, i
                                                          const float4* __restrict__ pd_tiled,
                                                          float* __restrict__ v_shaped,
                                                          float* __restrict__ v_posed) {
-    __shared__ float red[4][2][16][64];
+    __shared__ float red[NW][2][16][64];
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, hi = lane >> 5, l32 = lane & 31;
     const int t = blockIdx.x, m0 = t * 32, b0 = blockIdx.y * 32;
     const int m = m0 + l32, bA = b0 + l32;
@@ -337,8 +364,8 @@ __global__ __launch_bounds__(256) void k_lbs_blend_tiled(int B, int M, int NB, i
     floatx16 as, ap;
 #pragma unroll
     for (int r = 0; r < 16; r++) { as[r] = 0.f; ap[r] = 0.f; }
-    if (NB > 0) blend_tiled_mfma_part(as, betas, NB, sd_tiled, NB, t, bA, bok, w, hi, lane);
-    if (NP > 0 && v_posed) blend_tiled_mfma_part(ap, feat, NP, pd_tiled, NP, t, bA, bok, w, hi, lane);
+    if (NB > 0) blend_tiled_mfma_part(as, betas, NB, sd_tiled, NB, t, bA, bok, w, hi, lane, NW);
+    if (NP > 0 && v_posed) blend_tiled_mfma_part(ap, feat, NP, pd_tiled, NP, t, bA, bok, w, hi, lane, NW);
 #pragma unroll
     for (int r = 0; r < 16; r++) {
         red[w][0][r][lane] = as[r];
@@ -346,13 +373,13 @@ __global__ __launch_bounds__(256) void k_lbs_blend_tiled(int B, int M, int NB, i
     }
     __syncthreads();
 #pragma unroll
-    for (int i = 0; i < 4; i++) {
-        const int r = 4 * w + i;
+    for (int i = 0; i < 16 / NW; i++) {
+        const int r = (16 / NW) * w + i;
         const int b = b0 + (r & 3) + 8 * (r >> 2) + 4 * hi;
         if (!mok || b >= B) continue;
         float S = red[0][0][r][lane], Pz = red[0][1][r][lane];
 #pragma unroll
-        for (int u = 1; u < 4; u++) { S += red[u][0][r][lane]; Pz += red[u][1][r][lane]; }
+        for (int u = 1; u < NW; u++) { S += red[u][0][r][lane]; Pz += red[u][1][r][lane]; }
         const float tv = vt[(int64_t)b * vt_stride + m];
         const float vs = NB > 0 ? tv + S : tv;
         v_shaped[(int64_t)b * M + m] = vs;
@@ -455,9 +482,17 @@ static void launch_blend(int B, int M, int NB, int NP, const float* vt, int64_t 
     const bool tiled = tiled_on && sp && (NB == 0 || sp->shapedirs_tiled) &&
                        (NP == 0 || !vp || sp->posedirs_tiled) && (NB > 0 || (NP > 0 && vp));
     if (tiled && B > kLbsFrames && !valu_only) {
-        hipLaunchKernelGGL(k_lbs_blend_tiled, dim3((M + 31) / 32, (B + 31) / 32), dim3(256), 0, s, B, M, NB,
-                           vp ? NP : 0, vt, vt_stride, betas, reinterpret_cast<const float4*>(sp->shapedirs_tiled),
-                           feat, reinterpret_cast<const float4*>(sp->posedirs_tiled), vs, vp);
+        static const int nw_env = [] { const char* e = getenv("GSR_BLEND_NW"); return e ? atoi(e) : 0; }();
+        const dim3 grid((M + 31) / 32, (B + 31) / 32);
+        const int nw = nw_env == 4 || nw_env == 8 ? nw_env : (grid.x * grid.y <= 512 ? 8 : 4);
+        const float4* sdt = reinterpret_cast<const float4*>(sp->shapedirs_tiled);
+        const float4* pdt = reinterpret_cast<const float4*>(sp->posedirs_tiled);
+        if (nw == 8)
+            hipLaunchKernelGGL(k_lbs_blend_tiled<8>, grid, dim3(512), 0, s, B, M, NB, vp ? NP : 0, vt, vt_stride,
+                               betas, sdt, feat, pdt, vs, vp);
+        else
+            hipLaunchKernelGGL(k_lbs_blend_tiled<4>, grid, dim3(256), 0, s, B, M, NB, vp ? NP : 0, vt, vt_stride,
+                               betas, sdt, feat, pdt, vs, vp);
         return;
     }
     if (tiled && B == 1) {
