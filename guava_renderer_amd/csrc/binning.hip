@@ -863,9 +863,16 @@ __host__ __device__ __forceinline__ uint32_t strip_mask(float4 co, float4 pre, f
 // term is a popcount of per-wave ballots of "rect covers tile column tx" and "... row ty" (4 x
 // 64-bit masks per column and per row, in LDS), and base[] advances by the pass's per-tile totals.
 // The (chunk x tile) table and the per-workgroup base[] load shrink with the chunk, not the pass.
-template <int ABL>  // timing ablations (GSR_SCATTER_ABLATE): 1 = no strip test, 2 = no list store
+// WS (default; GSR_SCATTER_WAVESEARCH=0 for the per-lane search): each wave expands a contiguous run
+// of the pass's instances, 64 at a time; the owner of instance q0 + i is o0 + (slot boundaries in
+// (q0, q0 + i]) with o0 the owner of q0 (the previous step's last lane): every lane reads the end of
+// slot o0 + lane, marks it in a per-wave 64-entry LDS row when it falls in the window, and one
+// ballot of the row gives every lane its count -- in place of an 8-step binary search per instance.
+template <int ABL, bool WS>  // timing ablations (GSR_SCATTER_ABLATE): 1 = no strip test, 2 = no list store
 __global__ __launch_bounds__(kSlots) __attribute__((amdgpu_waves_per_eu(6))) void k_ordered_scatter(Dims d, GeomArena g, ImageArena im, BinArena bn, int xcd_order) {
     uint32_t sink = 0;
+    __shared__ uint32_t s_mark[kSlots];  // WS: one 64-entry row per wave
+    uint32_t tag = 0;
     extern __shared__ uint64_t masks[];  // colm[gx][4], rowm[gy][4], then uint32 tile bases[T]
     __shared__ uint32_t s_pref[kSlots];
     __shared__ uint32_t s_sh[kSlots / 64 + 1];
@@ -935,15 +942,44 @@ __global__ __launch_bounds__(kSlots) __attribute__((amdgpu_waves_per_eu(6))) voi
             for (int x = x0; x < x1; x++) atomicOr((unsigned long long*)&colm[4 * x + wv], bit);
             for (int y = y0; y < y1; y++) atomicOr((unsigned long long*)&rowm[4 * y + wv], bit);
         }
+        if (WS && pass == 0) s_mark[tid] = 0u;  // (tags start at 1; the barrier below orders it)
         __syncthreads();
-        for (uint32_t q = tid; q < total; q += kSlots) {
-            int lo = 0, hi = kSlots - 1;  // first slot whose inclusive count exceeds q
+        const uint32_t per = WS ? (total + kSlots - 1) / kSlots * 64u : 0u;  // instances per wave
+        const uint32_t qa = WS ? min(total, (uint32_t)wv * per) : (uint32_t)tid;
+        const uint32_t qb = WS ? min(total, qa + per) : total;
+        int o0 = 0;
+        if (WS && qa < qb) {  // owner of the wave's first instance (wave-uniform)
+            int lo = 0, hi = kSlots - 1;
 #pragma unroll
             for (int step = 0; step < 8; step++) {
                 const int mid = (lo + hi) >> 1;
-                if (s_pref[mid] > q) hi = mid; else lo = mid + 1;
+                if (s_pref[mid] > qa) hi = mid; else lo = mid + 1;
             }
-            const int o = lo;
+            o0 = lo;
+        }
+        for (uint32_t q0 = qa; q0 < qb; q0 += WS ? 64u : (uint32_t)kSlots) {
+            const uint32_t q = WS ? q0 + (uint32_t)lane : q0;
+            int o;
+            if (WS) {
+                uint32_t* mrow = s_mark + 64 * wv;
+                ++tag;
+                const int os = o0 + lane;
+                const uint32_t e = os < kSlots ? s_pref[os] : 0xFFFFFFFFu;  // end of slot os (> q0)
+                if (e - q0 < 64u) mrow[e - q0] = tag;  // slot os + 1 starts inside the window
+                const uint64_t M = __ballot(mrow[lane] == tag);  // (a wave's LDS ops complete in order)
+                const uint64_t upto = lane == 63 ? ~0ull : ((2ull << lane) - 1ull);
+                o = o0 + __popcll(M & upto);
+                o0 = __shfl(o, 63);
+                if (q >= qb) continue;
+            } else {
+                int lo = 0, hi = kSlots - 1;  // first slot whose inclusive count exceeds q
+#pragma unroll
+                for (int step = 0; step < 8; step++) {
+                    const int mid = (lo + hi) >> 1;
+                    if (s_pref[mid] > q) hi = mid; else lo = mid + 1;
+                }
+                o = lo;
+            }
             const uint32_t k = q - (o ? s_pref[o - 1] : 0u);
             const uint2 ro = s_rect[o];
             const int ox0 = ro.x & 0xFFFF, oy0 = ro.x >> 16, ow = (ro.y & 0xFFFF) - ox0;
@@ -982,18 +1018,21 @@ void launch_ordered_scatter(const Dims& d, const GeomArena& g, const ImageArena&
     static size_t attr = 0;
     if (lds > 65536 && attr < lds) {
         attr = lds;
-        for (const void* f : {(const void*)k_ordered_scatter<0>, (const void*)k_ordered_scatter<1>,
-                              (const void*)k_ordered_scatter<2>, (const void*)k_ordered_scatter<3>})
+        for (const void* f : {(const void*)k_ordered_scatter<0, true>, (const void*)k_ordered_scatter<1, true>,
+                              (const void*)k_ordered_scatter<2, true>, (const void*)k_ordered_scatter<3, true>,
+                              (const void*)k_ordered_scatter<0, false>})
             hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     }
     static const int abl = [] { const char* e = getenv("GSR_SCATTER_ABLATE"); return e ? atoi(e) : 0; }();
     static const int xo = [] { const char* e = getenv("GSR_SCATTER_XCD"); return (e && e[0] == '0') ? 0 : 1; }();
+    static const bool ws = [] { const char* e = getenv("GSR_SCATTER_WAVESEARCH"); return !(e && e[0] == '0'); }();
     const uint32_t N = (uint32_t)d.nchunk * (uint32_t)d.B;
     const dim3 gr = xo ? dim3(8u * ((N + 7u) / 8u)) : dim3(d.nchunk, d.B), bl(kSlots);
-    if (abl == 1) hipLaunchKernelGGL(k_ordered_scatter<1>, gr, bl, lds, s, d, g, im, b, xo);
-    else if (abl == 2) hipLaunchKernelGGL(k_ordered_scatter<2>, gr, bl, lds, s, d, g, im, b, xo);
-    else if (abl == 3) hipLaunchKernelGGL(k_ordered_scatter<3>, gr, bl, lds, s, d, g, im, b, xo);
-    else hipLaunchKernelGGL(k_ordered_scatter<0>, gr, bl, lds, s, d, g, im, b, xo);
+    if (abl == 1) hipLaunchKernelGGL((k_ordered_scatter<1, true>), gr, bl, lds, s, d, g, im, b, xo);
+    else if (abl == 2) hipLaunchKernelGGL((k_ordered_scatter<2, true>), gr, bl, lds, s, d, g, im, b, xo);
+    else if (abl == 3) hipLaunchKernelGGL((k_ordered_scatter<3, true>), gr, bl, lds, s, d, g, im, b, xo);
+    else if (!ws) hipLaunchKernelGGL((k_ordered_scatter<0, false>), gr, bl, lds, s, d, g, im, b, xo);
+    else hipLaunchKernelGGL((k_ordered_scatter<0, true>), gr, bl, lds, s, d, g, im, b, xo);
 }
 
 // ---------------------------------------------------------------- 6. strip work list
