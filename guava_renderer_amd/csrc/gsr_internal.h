@@ -137,7 +137,12 @@ inline Dims make_dims(int B, int P, int W, int H) {
     // k_bucket_count_lds (64 KB; <= 32 keys per bucket on average); beyond, ~8 keys per bucket
     // (global-atomic counting) so that the buckets stay small enough for in-place ranking
     const int nb_cap = P <= (1 << 19) ? (1 << 14) : (1 << 20);
-    while (nb < P / 8 && nb < nb_cap) nb <<= 1;
+    static const int kdiv = [] {  // GSR_BUCKET_DIV: keys per bucket target (tuning)
+        const char* e = getenv("GSR_BUCKET_DIV");
+        const int v = e ? atoi(e) : 8;
+        return v >= 2 && v <= 256 ? v : 8;
+    }();
+    while (nb < P / kdiv && nb < nb_cap) nb <<= 1;
     d.NB = nb;
     // count-table rows: kSlots Gaussians (one scatter pass) up to 1024 tiles; beyond, the dense
     // (row x tile) table and each row's base[] load outweigh the extra passes (1024-Gaussian rows)
