@@ -2,6 +2,7 @@
 include/*.h, the Python mirror keeps the reference's signatures and error behaviour
 (diff_gaussian_rasterization_32/__init__.py:143-207, rasterize_points.cu:58-60), and there is no
 CPU fallback (GPU-less calls with P > 0 raise)."""
+import ctypes
 import inspect
 import os
 import re
@@ -180,3 +181,33 @@ def test_deform_abi_validates_before_touching_memory():
     with pytest.raises(RuntimeError, match="GPU only"):
         deform.lbs_wobeta(torch.zeros(1, 3, 3), torch.zeros(1, 4, 3), torch.zeros(18, 12),
                           torch.zeros(3, 4), torch.tensor([-1, 0, 1]), torch.zeros(4, 3))
+
+
+def test_ctypes_structs_match_the_c_layout(tmp_path):
+    """The ctypes mirrors of the C ABI's structs (_lib.DeformInputs / Scratch / LbsSparse /
+    RowSegment) have the C compiler's size and field offsets (include/gsr*.h, x86-64)."""
+    import shutil
+    import subprocess
+    from guava_renderer_amd import _lib
+    if shutil.which("gcc") is None:
+        pytest.skip("no gcc")
+    inc = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "include")
+    structs = {"GsrDeformInputs": _lib.DeformInputs, "gsr_scratch": _lib.Scratch, "GsrLbsSparse": _lib.LbsSparse,
+               "GsrRowSegment": _lib.RowSegment, "gsr_refine_epilogue": _lib.RefineEpilogue}
+    lines = ['#include <stddef.h>', '#include <stdio.h>', '#include "gsr.h"', '#include "gsr_deform.h"',
+             "int main(void) {"]
+    for cname, py in structs.items():
+        lines.append(f'printf("{cname} size %zu\\n", sizeof({cname}));')
+        for f, _ in py._fields_:
+            lines.append(f'printf("{cname} {f} %zu\\n", offsetof({cname}, {f}));')
+    lines.append("return 0; }")
+    src = tmp_path / "layout.c"
+    src.write_text("\n".join(lines))
+    exe = tmp_path / "layout"
+    subprocess.run(["gcc", "-I", inc, str(src), "-o", str(exe)], check=True, capture_output=True)
+    out = subprocess.run([str(exe)], check=True, capture_output=True, text=True).stdout.split("\n")
+    got = {tuple(l.split()[:2]): int(l.split()[2]) for l in out if l.strip()}
+    for cname, py in structs.items():
+        assert got[(cname, "size")] == ctypes.sizeof(py), cname
+        for f, _ in py._fields_:
+            assert got[(cname, f)] == getattr(py, f).offset, (cname, f)
