@@ -658,19 +658,15 @@ def main():
     ksteps = work["mfma_ksteps"]
     if not split_head:
         mfma_flops = ksteps * 2 * (2 * 32 * 32 * 2)  # two v_mfma_f32_32x32x2f32 per wave k-step
-        # quad tail: two v_mfma_f32_16x16x4f32 per four survivors
-        mfma_flops += work.get("quad_survivors", 0) // 4 * 2 * (2 * 16 * 16 * 4)
-        mfma_flops += work.get("half_survivors", 0) // 2 * (2 * 32 * 32 * 2)  # half tail: one per two
     else:  # two v_mfma_f32_32x32x8_bf16 per wave k-step (every k-slot carries a split product)
         mfma_flops = ksteps * 2 * (2 * 32 * 32 * 8)
     out["render_work_per_frame"] = {k: round(v / B, 1) for k, v in work.items()}
     out["render_mfma"] = {"issued_tflops": round(mfma_flops / (render_ms * 1e-3) / 1e12, 2) if render_ms else None,
                           "peak_tflops": BF16_MFMA_PEAK_TFLOPS if split_head else F32_MFMA_PEAK_TFLOPS,
                           "instruction": "v_mfma_f32_32x32x8_bf16" if split_head else "v_mfma_f32_32x32x2_f32",
-                          # lane-pairs blended: 64 pixels per survivor in the strip layout, 16 slots in the quad tail
-                          "useful_frac": round(work["pairs_contributing"] / max(64 * work["strip_pairs_blended"] +
-                                                                                32 * work.get("half_survivors", 0) +
-                                                                                16 * work.get("quad_survivors", 0), 1), 4)}
+                          # lane-pairs blended: 64 pixels per survivor in the strip layout
+                          "useful_frac": round(work["pairs_contributing"] / max(64 * work["strip_pairs_blended"], 1),
+                                               4)}
     if issue is not None:
         # the compute wall beside the HBM one: per-launch instruction counts and per-SIMD pipe busy
         # of the contract kernel, from the committed PMC passes of this build

@@ -81,7 +81,9 @@ class LbsSparse(ctypes.Structure):
     """GsrLbsSparse (include/gsr_deform.h)."""
     _fields_ = [("jreg_row", _vp), ("jreg_col", _vp), ("jreg_val", _vp), ("skin_k", ctypes.c_int32),
                 ("pad_", ctypes.c_int32), ("skin_joint", _vp), ("skin_weight", _vp),
-                ("shapedirs_tiled", _vp), ("posedirs_tiled", _vp)]
+                ("shapedirs_tiled", _vp), ("posedirs_tiled", _vp), ("shapedirs_tiled_k", ctypes.c_int32),
+                ("shapedirs_tiled_m", ctypes.c_int32), ("posedirs_tiled_k", ctypes.c_int32),
+                ("posedirs_tiled_m", ctypes.c_int32)]
 
 
 class GsrError(RuntimeError):

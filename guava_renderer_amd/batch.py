@@ -211,6 +211,12 @@ class BatchRasterizer:
             raise ValueError(f"deformer has {dfm.V + dfm.N} Gaussians, the rasterizer {P}")
         if tuple(verts.shape) != (B, dfm.V, 3) or tuple(vert_transforms.shape) != (B, dfm.V, 4, 4):
             raise ValueError("verts / vert_transforms: expected [B,V,3] / [B,V,4,4]")
+        # every pointer below goes straight to the kernel: a host (or other-device) tensor must not
+        # reach it
+        for name, t_ in (("verts", verts), ("vert_transforms", vert_transforms), ("deformer.faces", dfm.faces),
+                         ("deformer.colors", dfm.colors), ("deformer.bind", dfm.bind)):
+            if t_.device != self.device:
+                raise ValueError(f"{name} is on {t_.device}, the rasterizer on {self.device}")
         vb = verts.detach().to(torch.float32).contiguous()
         vt = vert_transforms.detach().to(torch.float32).contiguous()
         keep, head, (v, pm, tf, bg, bs) = self._inputs(None, dfm.colors, dfm.opacity, None, None, viewmatrices,
@@ -373,8 +379,7 @@ def profile_read():
 
 
 COUNTERS = ("pairs_evaluated", "pairs_contributing", "strip_pairs_blended", "mfma_ksteps",
-            "gaussians_staged", "list_entries", "tiles_rendered", "dead_ksteps", "quad_survivors",
-            "half_survivors")
+            "gaussians_staged", "list_entries", "tiles_rendered", "dead_ksteps")
 
 
 def render_counters(fn, device="cuda"):

@@ -662,7 +662,7 @@ void launch_chunk_count(const Dims& d, const GeomArena& g, const ImageArena& im,
         hipFuncSetAttribute((const void*)k_chunk_count<true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
         hipFuncSetAttribute((const void*)k_chunk_count<false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     }
-    static const bool g8 = [] { const char* e = getenv("GSR_CHUNK_SCAN8"); return !(e && e[0] == '0'); }();
+    static const bool g8 = tune_env("GSR_CHUNK_SCAN8", 1) != 0;
     if (g8) hipLaunchKernelGGL(k_chunk_count<true>, dim3(d.nchunk, d.B), dim3(kScanBlock), lds, s, d, g);
     else hipLaunchKernelGGL(k_chunk_count<false>, dim3(d.nchunk, d.B), dim3(kScanBlock), lds, s, d, g);
     hipLaunchKernelGGL(k_column_scan_wide, dim3((d.T + 63) / 64, d.B), dim3(64 * kColWaves), 0, s, d, g, im);
@@ -1018,20 +1018,28 @@ void launch_ordered_scatter(const Dims& d, const GeomArena& g, const ImageArena&
     static size_t attr = 0;
     if (lds > 65536 && attr < lds) {
         attr = lds;
-        for (const void* f : {(const void*)k_ordered_scatter<0, true>, (const void*)k_ordered_scatter<1, true>,
-                              (const void*)k_ordered_scatter<2, true>, (const void*)k_ordered_scatter<3, true>,
+        for (const void* f : {(const void*)k_ordered_scatter<0, true>,
+#ifdef GSR_TUNING
+                              (const void*)k_ordered_scatter<1, true>, (const void*)k_ordered_scatter<2, true>,
+                              (const void*)k_ordered_scatter<3, true>,
+#endif
                               (const void*)k_ordered_scatter<0, false>})
             hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     }
-    static const int abl = [] { const char* e = getenv("GSR_SCATTER_ABLATE"); return e ? atoi(e) : 0; }();
-    static const int xo = [] { const char* e = getenv("GSR_SCATTER_XCD"); return (e && e[0] == '0') ? 0 : 1; }();
-    static const bool ws = [] { const char* e = getenv("GSR_SCATTER_WAVESEARCH"); return !(e && e[0] == '0'); }();
+    static const int abl = tune_env("GSR_SCATTER_ABLATE", 0);  // timing ablations: GSR_TUNING builds only
+    static const int xo = tune_env("GSR_SCATTER_XCD", 1) != 0 ? 1 : 0;
+    static const bool ws = tune_env("GSR_SCATTER_WAVESEARCH", 1) != 0;
     const uint32_t N = (uint32_t)d.nchunk * (uint32_t)d.B;
     const dim3 gr = xo ? dim3(8u * ((N + 7u) / 8u)) : dim3(d.nchunk, d.B), bl(kSlots);
+#ifdef GSR_TUNING
     if (abl == 1) hipLaunchKernelGGL((k_ordered_scatter<1, true>), gr, bl, lds, s, d, g, im, b, xo);
     else if (abl == 2) hipLaunchKernelGGL((k_ordered_scatter<2, true>), gr, bl, lds, s, d, g, im, b, xo);
     else if (abl == 3) hipLaunchKernelGGL((k_ordered_scatter<3, true>), gr, bl, lds, s, d, g, im, b, xo);
-    else if (!ws) hipLaunchKernelGGL((k_ordered_scatter<0, false>), gr, bl, lds, s, d, g, im, b, xo);
+    else
+#else
+    (void)abl;
+#endif
+    if (!ws) hipLaunchKernelGGL((k_ordered_scatter<0, false>), gr, bl, lds, s, d, g, im, b, xo);
     else hipLaunchKernelGGL((k_ordered_scatter<0, true>), gr, bl, lds, s, d, g, im, b, xo);
 }
 

@@ -5,11 +5,14 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <mutex>
 #include <string>
+#include <unordered_map>
 #include <vector>
 
 #include "../../include/gsr.h"
 #include "../../include/gsr_deform.h"
+
 #include "gsr_internal.h"
 
 using namespace gsr;
@@ -95,12 +98,12 @@ static void env_tuning(Inputs& in) {
 }
 
 int xcd_queue_map() {
-    static const int v = [] { const char* e = getenv("GSR_XCD_MAP"); return (e && e[0] == '1') ? 1 : 2; }();
+    static const int v = tune_env("GSR_XCD_MAP", 2) == 1 ? 1 : 2;
     return v;
 }
 
 int strip_order_tile_major() {
-    static const int v = [] { const char* e = getenv("GSR_STRIP_ORDER"); return (e && !strcmp(e, "strip")) ? 0 : 1; }();
+    static const int v = tune_env("GSR_STRIP_ORDER_TILE", 1) != 0 ? 1 : 0;  // 0: strips ordered alone (A/B)
     return v;
 }
 
@@ -501,6 +504,22 @@ int gsr_forward_batch(int B, int P, int width, int height, const float* means3D,
                                     antialiasing, nullptr, numerics, stream);
 }
 
+// Host-side record of which batch workspaces the last forward left forward-only (GSR_FORWARD_ONLY
+// or the fused deform path): a gsr_backward_batch* on such a workspace fails with GSR_ERR_ARG
+// instead of returning the caller's zeroed gradients (the device word kCtrlFwdOnly still keeps
+// the kernels from computing on it, e.g. for a workspace forwarded by another process).
+static std::mutex g_ws_mu;
+static std::unordered_map<const void*, bool> g_ws_fwd_only;
+static void note_workspace(const void* ws, bool fwd_only) {
+    std::lock_guard<std::mutex> lk(g_ws_mu);
+    g_ws_fwd_only[ws] = fwd_only;
+}
+static bool workspace_fwd_only(const void* ws) {
+    std::lock_guard<std::mutex> lk(g_ws_mu);
+    const auto it = g_ws_fwd_only.find(ws);
+    return it != g_ws_fwd_only.end() && it->second;
+}
+
 static int forward_batch_impl(int B, int P, int width, int height, const float* means3D,
                               int64_t means_stride, const float* colors, int64_t colors_stride,
                               const float* opacities, int64_t opac_stride, const float* scales,
@@ -563,6 +582,7 @@ static int forward_batch_impl(int B, int P, int width, int height, const float* 
     { StageTimer st_(1, s); launch_scan_blocksums(d, g, R_capacity, s); }
     int rc = run_binning_and_render(d, in, g, im, bn, o, numerics, 0, s);
     if (rc < 0) return rc;
+    note_workspace(workspace, in.fwd_only != 0);
     return 0;
 }
 
@@ -629,6 +649,8 @@ static int backward_batch(int B, int P, int width, int height, const float* mean
     if (B <= 0 || P <= 0 || !workspace || !tanfov) return fail(GSR_ERR_ARG, "bad batch arguments");
     if (numerics & ~kNumericsKnown) return fail(GSR_ERR_ARG, "unknown numerics flags");
     if (P >= kMaxGaussians) return fail(GSR_ERR_ARG, "P must be < 2^24");
+    if (workspace_fwd_only(workspace))
+        return fail(GSR_ERR_ARG, "backward_batch: the workspace's last forward was GSR_FORWARD_ONLY (no backward rows)");
     const Dims d = make_dims(B, P, width, height);
     GeomArena g;
     ImageArena im;

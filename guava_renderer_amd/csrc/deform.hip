@@ -471,18 +471,13 @@ static void lbs_blend_attr(size_t lds) {
 static void launch_blend(int B, int M, int NB, int NP, const float* vt, int64_t vt_stride, const float* betas,
                          const float* sd_t, const float* feat, const float* pd, float* vs, float* vp,
                          hipStream_t s, const GsrLbsSparse* sp) {
-    static const bool valu_only = [] {  // timing A/B only
-        const char* e = getenv("GSR_BLEND_VALU");
-        return e && e[0] == '1';
-    }();
-    static const bool tiled_on = [] {  // GSR_BLEND_TILED=0: the k-major kernels even with tiled bases (A/B)
-        const char* e = getenv("GSR_BLEND_TILED");
-        return !(e && e[0] == '0');
-    }();
+    static const bool valu_only = tune_env("GSR_BLEND_VALU", 0) == 1;  // timing A/B only
+    // GSR_BLEND_TILED=0: the k-major kernels even with tiled bases (A/B)
+    static const bool tiled_on = tune_env("GSR_BLEND_TILED", 1) != 0;
     const bool tiled = tiled_on && sp && (NB == 0 || sp->shapedirs_tiled) &&
                        (NP == 0 || !vp || sp->posedirs_tiled) && (NB > 0 || (NP > 0 && vp));
     if (tiled && B > kLbsFrames && !valu_only) {
-        static const int nw_env = [] { const char* e = getenv("GSR_BLEND_NW"); return e ? atoi(e) : 0; }();
+        static const int nw_env = tune_env("GSR_BLEND_NW", 0);
         const dim3 grid((M + 31) / 32, (B + 31) / 32);
         const int nw = nw_env == 4 || nw_env == 8 ? nw_env : (grid.x * grid.y <= 512 ? 8 : 4);
         const float4* sdt = reinterpret_cast<const float4*>(sp->shapedirs_tiled);
@@ -506,10 +501,7 @@ static void launch_blend(int B, int M, int NB, int NP, const float* vt, int64_t 
                            vp ? NP : 0, vt, vt_stride, betas, sd_t, feat, pd, vs, vp);
         return;
     }
-    static const bool single = [] {  // GSR_BLEND_SINGLE=0: B = 1 on the 16-frame kernel (A/B)
-        const char* e = getenv("GSR_BLEND_SINGLE");
-        return !(e && e[0] == '0');
-    }();
+    static const bool single = tune_env("GSR_BLEND_SINGLE", 1) != 0;  // 0: B = 1 on the 16-frame kernel (A/B)
     if (B == 1 && single) {
         const size_t lds = lbs_blend_lds(NB, vp ? NP : 0, 1, kLbsSplit1);
         lbs_blend_attr(lds);
@@ -706,7 +698,7 @@ __global__ __launch_bounds__(256) void k_lbs_skin_ell(int V, int J, int K, const
     float ww[KMAX];
 #pragma unroll
     for (int u = 0; u < KMAX; u++) {
-        jj[u] = u < K ? sj[(int64_t)u * V + v] : 0;
+        jj[u] = u < K ? min((int)sj[(int64_t)u * V + v], J - 1) : 0;  // (in range by contract; clamped)
         ww[u] = u < K ? sw[(int64_t)u * V + v] : 0.f;
     }
     float T[16];
@@ -1095,8 +1087,7 @@ void launch_deform_preprocess(const Dims& d, const Inputs& in, const GeomArena& 
     // 4 frames per workgroup: 118.9 us per 32 frames vs 169.7 / 132.5 / 121.3 / 131.6 at 1 / 2 / 8 / 16
     // (GSR_FUSED_FRAMES; fewer re-reads of the binding set-up against fewer workgroups in flight)
     static const int fpw = [] {
-        const char* e = getenv("GSR_FUSED_FRAMES");
-        const int v = e ? atoi(e) : 4;
+        const int v = tune_env("GSR_FUSED_FRAMES", 4);
         return v >= 1 && v <= 64 ? v : 1;
     }();
     hipLaunchKernelGGL(k_deform_preprocess, dim3(d.nblk, (d.B + fpw - 1) / fpw), dim3(256), 0, s, fpw, dg, d, in,
@@ -1191,7 +1182,8 @@ void launch_joints(int B, int V, int J, const float* J_regressor, const GsrLbsSp
                            J_regressor, vs, joints_offset, joints);
     }
 }
-int check_sparse(const GsrLbsSparse* sp, int J, const char* who) {
+// NB: shape coefficients of the call, V: its vertices (the pose base is 9(J-1) x 3V)
+int check_sparse(const GsrLbsSparse* sp, int J, int NB, int V, const char* who) {
     if (!sp) return 0;
     if (sp->jreg_row && (!sp->jreg_col || !sp->jreg_val))
         return api_fail(GSR_ERR_ARG, (std::string(who) + ": jreg_row without jreg_col / jreg_val").c_str());
@@ -1199,7 +1191,10 @@ int check_sparse(const GsrLbsSparse* sp, int J, const char* who) {
         return api_fail(GSR_ERR_ARG, (std::string(who) + ": skin_k must be in [1, 16] with its arrays").c_str());
     if (((uintptr_t)sp->shapedirs_tiled | (uintptr_t)sp->posedirs_tiled) & 15)
         return api_fail(GSR_ERR_ARG, (std::string(who) + ": tiled bases must be 16-byte aligned").c_str());
-    (void)J;
+    if (sp->shapedirs_tiled && NB > 0 && (sp->shapedirs_tiled_k != NB || sp->shapedirs_tiled_m != 3 * V))
+        return api_fail(GSR_ERR_ARG, (std::string(who) + ": shapedirs_tiled was tiled for another NB x 3V").c_str());
+    if (sp->posedirs_tiled && J > 1 && (sp->posedirs_tiled_k != 9 * (J - 1) || sp->posedirs_tiled_m != 3 * V))
+        return api_fail(GSR_ERR_ARG, (std::string(who) + ": posedirs_tiled was tiled for another 9(J-1) x 3V").c_str());
     return 0;
 }
 }  // namespace
@@ -1225,7 +1220,7 @@ int gsr_lbs_sp(int B, int V, int J, int NB, const float* v_template, int64_t v_t
                float* joint_transforms, float* v_shaped, char* workspace, const GsrLbsSparse* sp,
                void* stream) {
     if (B <= 0 || V <= 0) return api_fail(GSR_ERR_ARG, "gsr_lbs: B and V must be positive");
-    if (int rc = check_sparse(sp, J, "gsr_lbs")) return rc;
+    if (int rc = check_sparse(sp, J, betas ? NB : 0, V, "gsr_lbs")) return rc;
     if (J < 1 || J > GSR_LBS_MAX_JOINTS) return api_fail(GSR_ERR_ARG, "gsr_lbs: J must be in [1, 64]");
     if (!v_template || !pose || !J_regressor || !parents_host || !lbs_weights_t || !verts || !workspace)
         return api_fail(GSR_ERR_ARG, "gsr_lbs: null required pointer");
@@ -1294,7 +1289,7 @@ int gsr_blend_joints_sp(int B, int V, int J, int NB, const float* v_template, in
                         const float* joints_offset, float* v_shaped, float* joints, const GsrLbsSparse* sp,
                         void* stream) {
     if (B <= 0 || V <= 0 || J < 1) return api_fail(GSR_ERR_ARG, "gsr_blend_joints: bad sizes");
-    if (int rc = check_sparse(sp, J, "gsr_blend_joints")) return rc;
+    if (int rc = check_sparse(sp, 1, betas ? NB : 0, V, "gsr_blend_joints")) return rc;
     if (!v_template || !J_regressor || !v_shaped || !joints)
         return api_fail(GSR_ERR_ARG, "gsr_blend_joints: null required pointer");
     if (v_template_stride != 0 && v_template_stride != (int64_t)V * 3)
@@ -1384,8 +1379,7 @@ int gsr_deform_gaussians(int B, int V, int F, int N, const float* verts,
         return api_fail(GSR_ERR_ARG, "gsr_deform_gaussians: strides must be 0 or a whole frame");
     hipStream_t s = (hipStream_t)stream;
     static const int fpw = [] {
-        const char* e = getenv("GSR_DEFORM_FRAMES");
-        const int v = e ? atoi(e) : kDeformFrames;
+        const int v = tune_env("GSR_DEFORM_FRAMES", kDeformFrames);
         return v >= 1 && v <= 64 ? v : 1;
     }();
     const int P = V + N;

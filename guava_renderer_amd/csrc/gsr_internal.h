@@ -14,6 +14,20 @@
 
 namespace gsr {
 
+// Tuning and timing-ablation switches (GSR_RENDER_*, GSR_SCATTER_*, GSR_BWD_*, ...).  The product
+// library always takes the default: only the A/B builds of tools/build_ab.py (-DGSR_TUNING) read
+// them from the environment, and only those builds contain the ablation kernels (which produce
+// wrong images by construction).  A stray variable in a deployment therefore changes nothing
+// (tests/test_boundary.py::test_product_library_has_no_tuning_switches).
+#ifdef GSR_TUNING
+inline int tune_env(const char* name, int def) {
+    const char* e = getenv(name);
+    return e ? atoi(e) : def;
+}
+#else
+inline int tune_env(const char*, int def) { return def; }
+#endif
+
 constexpr int kScanBlock = 256;       // Gaussians per preprocess / binning workgroup
 constexpr int kSortSmallCap = 2048;   // keys per segment sorted by the 256-thread LDS sort
 constexpr int kSortLargeCap = 8192;   // keys per segment sorted by the 1024-thread LDS sort
@@ -138,17 +152,15 @@ inline Dims make_dims(int B, int P, int W, int H) {
     // (global-atomic counting) so that the buckets stay small enough for in-place ranking
     const int nb_cap = P <= (1 << 19) ? (1 << 14) : (1 << 20);
     static const int kdiv = [] {  // GSR_BUCKET_DIV: keys per bucket target (tuning)
-        const char* e = getenv("GSR_BUCKET_DIV");
-        const int v = e ? atoi(e) : 8;
-        return v >= 2 && v <= 256 ? v : 8;
+        const int v = tune_env("GSR_BUCKET_DIV", 16);
+        return v >= 2 && v <= 256 ? v : 16;
     }();
     while (nb < P / kdiv && nb < nb_cap) nb <<= 1;
     d.NB = nb;
     // count-table rows: kSlots Gaussians (one scatter pass) up to 1024 tiles; beyond, the dense
     // (row x tile) table and each row's base[] load outweigh the extra passes (1024-Gaussian rows)
     static const int passes_env = [] {  // GSR_CHUNK_PASSES: scatter passes per table row (tuning)
-        const char* e = getenv("GSR_CHUNK_PASSES");
-        const int v = e ? atoi(e) : 0;
+        const int v = tune_env("GSR_CHUNK_PASSES", 0);
         return v >= 1 && v <= 64 ? v : 0;
     }();
     d.chunk = (passes_env ? passes_env : (d.T > 1024 ? 4 : 1)) * kSlots;

@@ -484,7 +484,7 @@ void launch_render_bwd(const Dims& d, const Inputs& in_, const GeomArena& g, con
     // The forward's block-affine segments cost the backward 8%: it walks a tile-affine list of its
     // own (one longest-first list, built here from the forward's strip counts, ~10 us);
     // GSR_BWD_TILE_LIST=0 walks the forward's segments
-    static const bool own_list = [] { const char* e = getenv("GSR_BWD_TILE_LIST"); return !(e && e[0] == '0'); }();
+    static const bool own_list = tune_env("GSR_BWD_TILE_LIST", 1) != 0;
     ImageArena im = im_;
     if (in.xcd_map == 2u && own_list) {
         launch_strip_list_tile(d, im_, im_.strip_list_bwd, s);
@@ -497,7 +497,9 @@ void launch_render_bwd(const Dims& d, const Inputs& in_, const GeomArena& g, con
     hipMemsetAsync(g.gterm, 0, (size_t)d.B * d.P * kGtWords * sizeof(float), s);
     const bool invd = gr.invd != 0;
     const dim3 grid(min((nwaves + 3) / 4, persistent_grid(2))), blk(GSR_TILE_PIX);
-    static const int ablate = [] { const char* e = getenv("GSR_BWD_ABLATE"); return e ? atoi(e) : 0; }();
+#ifdef GSR_TUNING
+    // timing ablations (wrong gradients by construction): tools/build_ab.py builds only
+    static const int ablate = tune_env("GSR_BWD_ABLATE", 0);
     if (ablate >= 1 && ablate <= 6 && exact && invd) {
         if (ablate == 1) hipLaunchKernelGGL((k_render_bwd<true, true, 0, 1>), grid, blk, 0, s, d, in, g, im, b, gr);
         if (ablate == 2) hipLaunchKernelGGL((k_render_bwd<true, true, 0, 2>), grid, blk, 0, s, d, in, g, im, b, gr);
@@ -506,10 +508,11 @@ void launch_render_bwd(const Dims& d, const Inputs& in_, const GeomArena& g, con
         if (ablate == 6) hipLaunchKernelGGL((k_render_bwd<true, true, 0, 6>), grid, blk, 0, s, d, in, g, im, b, gr);
         return;
     }
+#endif
     // split-bf16 contractions; one feature table for the batch is split once (into the forward's
     // fsplit rows, which this launch owns until it ends)
     // GSR_BWD_SPLIT=0: f32 contractions even with the split switch on (A/B)
-    static const bool bwd_split = [] { const char* e = getenv("GSR_BWD_SPLIT"); return !(e && e[0] == '0'); }();
+    static const bool bwd_split = tune_env("GSR_BWD_SPLIT", 1) != 0;
     int sp = 0;
     if (split && bwd_split) {
         sp = 1;

@@ -2,25 +2,27 @@
 // the reference).
 //
 // Structure (gfx950):
-//  * The unit of work is one 64-pixel strip (8x8, strip_origin) of a 16x16 tile, owned by ONE wave (lane = pixel).
-//    Waves dequeue strips independently from k_tile_scan's longest-first tile list (4 strips per
-//    entry), so there is no workgroup barrier anywhere: a wave whose pixels all finished moves on
-//    at once, and every XCD gets work.
+//  * The unit of work is one 64-pixel strip (8x8, strip_origin) of a 16x16 tile, owned by ONE wave
+//    (lane = pixel).  Waves dequeue strips independently from eight per-XCD queues (queue_item), so
+//    there is no workgroup barrier anywhere: a wave whose pixels all finished moves on at once.
 //  * The wave walks the tile's depth-sorted list 64 entries at a time (one coalesced load of indices
-//    and strip masks, prefetched one chunk ahead).  The binning pass already decided, with an exact
-//    conservative ellipse/rectangle test, whether each Gaussian can reach alpha >= 1/255 anywhere
-//    in each strip; one ballot over the strip bit gives the chunk's survivors.  A culled pair cannot
-//    change any blend decision, so the result is identical to visiting every pair.
-//  * Survivors are taken two at a time in list order (one MFMA k-step).  Their 32-byte render
-//    records arrive by scalar loads (the Gaussian index is wave-uniform) and feed the blend as SGPR
-//    operands; each lane runs the branch-free blend step for its pixel (alpha, the T<1e-4 stop,
-//    n_contrib) giving the weight w = alpha*T (0 where the pixel does not take the Gaussian).  The
-//    32-channel accumulation C += f*w runs on the matrix cores as D[ch][px] += F^T[ch][k] W[k][px]
-//    with v_mfma_f32_32x32x2_f32 over the strip's two 32-pixel halves, the feature operand loaded
-//    straight from HBM/L2 (lanes 0-31 one Gaussian's 128-byte row, lanes 32-63 the other's).  The
-//    f32 MFMA is an exact k-ordered fma chain, i.e. bit-identical to fmaf(f, w, C) Gaussian by
-//    Gaussian (the oracle's contract); a zero weight leaves the accumulator unchanged.
-//  * No LDS: occupancy is set by registers alone.
+//    and strip masks).  The binning pass already decided, with an exact conservative
+//    ellipse/rectangle test, whether each Gaussian can reach alpha >= 1/255 anywhere in each strip;
+//    one ballot over the strip bit gives the chunk's survivors.  A culled pair cannot change any
+//    blend decision, so the result is identical to visiting every pair.
+//  * Survivors are taken two at a time in list order (one MFMA k-step) through a three-slot
+//    software pipeline: the records and feature words of step s+2 load while step s+1's alphas
+//    (the exp-heavy, transmittance-independent part) are computed and step s's serial blend runs.
+//    Each lane runs the branch-free blend step for its pixel (the 1/255 skip, the T < 1e-4 stop,
+//    n_contrib), giving the weight w = alpha T (0 where the pixel does not take the Gaussian).  The
+//    32-channel accumulation C += f w runs on the matrix cores as D[ch][px] += F[ch][k] W[k][px]
+//    with v_mfma_f32_32x32x2_f32 over the strip's two 32-pixel halves (lanes 0-31 carry one
+//    Gaussian's 128-byte feature row, lanes 32-63 the other's).  The f32 MFMA is an exact k-ordered
+//    fma chain, i.e. bit-identical to fmaf(f, w, C) Gaussian by Gaussian (the oracle's contract); a
+//    zero weight leaves the accumulator unchanged.
+//  * One frame (the per-frame drop-in path): every strip is two work items, one wave per 32-pixel
+//    half, each lane computing ONE alpha per k-step (HALF below): the longest strip's chain is what
+//    sets a single frame's time.
 //
 // Roofline: per frame the kernel must read 156 B per visible Gaussian (features + 2D attributes)
 // and write 140 B per pixel (32 channels, inverse depth, final_T, n_contrib).
@@ -28,42 +30,15 @@
 
 namespace gsr {
 
-// How a k-step's two render records reach the wave (every lane needs both, uniform):
-//  0: four wave-uniform 16-B vector loads (each returns 1 KB through the texture data path);
-//  3: two 4-B vector loads on lanes 0..7 (lane j: dword j of record a, of record b; the record
-//     offsets in SGPRs), broadcast through a per-wave LDS slot (ds_write2, four uniform-address
-//     ds_read_b128).
-// (Scalar loads and a v_readlane broadcast were measured and dropped: DESIGN.md §7.)
-#ifndef GSR_REC_PATH
-#define GSR_REC_PATH 3
-#endif
-#ifndef GSR_MFMA_K8
-#define GSR_MFMA_K8 1  // split-bf16 products on v_mfma_f32_32x32x8_bf16 (0: 32x32x16 with k 4..7 zero)
-#endif
-#ifndef GSR_SPLIT_FIRST
-#define GSR_SPLIT_FIRST 1  // split-bf16: split both weights before the lane-half swap (two swaps, no copies)
-#endif
-#ifndef GSR_SKIP_DEAD
-#define GSR_SKIP_DEAD 0  // 1: skip the blend + MFMAs of a k-step no live pixel takes (measured +2%: off)
-#endif
+// A k-step's two render records reach the wave through a per-wave LDS slot: lanes 0..7 load dword
+// `lane` of record a and of record b (4-B vector loads, the record offsets in SGPRs), write them with
+// one ds_write2 and every lane reads them back as uniform-address ds_read_b128.  (Wave-uniform 16-B
+// vector loads, scalar loads and a v_readlane broadcast were measured and dropped: DESIGN.md §5.1, §7.)
 #ifndef GSR_LDS_EARLY
 #define GSR_LDS_EARLY 1  // record LDS reads of the next slot issued before this slot's blend
 #endif
-#ifndef GSR_STORE_AUX
-#define GSR_STORE_AUX 0  // cache-policy bits of the strip epilogue's colour stores (2 = nt)
-#endif
 #ifndef GSR_BATCH_NSLOT
 #define GSR_BATCH_NSLOT 3  // pipeline slots of the batched (throughput) kernels
-#endif
-#ifndef GSR_TAKE_VCC
-#define GSR_TAKE_VCC 0  // 1: the blend step on per-lane values (take_vcc), no lane-mask state (measured +1.6%: off)
-#endif
-#ifndef GSR_HALF_REC_DIRECT
-#define GSR_HALF_REC_DIRECT 1  // half-strip (single-frame) waves: each lane loads its Gaussian's 32-B record
-                               // with two 16-B loads (no LDS broadcast on the k-step's dependency chain)
-#endif
-#ifndef GSR_FILL16
-#define GSR_FILL16 1  // empty tiles as 16-byte stores (0: per-strip dword stores, the round-2 form; PMC A/B)
 #endif
 
 typedef float floatx16 __attribute__((ext_vector_type(16)));
@@ -115,22 +90,6 @@ __device__ __forceinline__ float take_step(float alpha, float inv_depth, uint32_
     return w;
 }
 
-// take_step without lane-mask state (GSR_TAKE_VCC): `alpha` already 0 below 1/255 (alpha stage), and
-// Tc = T for a live pixel, 0 once it stopped, so every branch of take_step is a value select on one
-// compare: a stopped pixel's test_T = 0 < 1e-4 takes nothing again, a skipped Gaussian gives
-// test_T = T * 1 = T.  Same products and decisions as take_step (T the pixel's output transmittance).
-__device__ __forceinline__ float take_vcc(float alpha, float inv_depth, uint32_t pos, float& Tc, float& T, float& invd,
-                                          uint32_t& last) {
-    const float test_T = Tc * (1.0f - alpha);
-    const bool term = test_T < 0.0001f;
-    const float w = term ? 0.0f : alpha * Tc;
-    Tc = term ? 0.0f : test_T;
-    T = term ? T : test_T;
-    invd = fmaf(inv_depth, w, invd);
-    last = w > 0.0f ? pos : last;
-    return w;
-}
-
 // Split-bf16 accumulation (gsr_set_split_bf16): f = f_hi + f_lo with f_hi = bf16_rne(f),
 // f_lo = bf16_rne(f - f_hi); the four bf16 products f_hi.w_hi + f_lo.w_hi + f_hi.w_lo + f_lo.w_lo
 // are exact in f32, so the only loss is the split residual (|f - f_hi - f_lo| <= 2^-17 |f|, the same
@@ -160,17 +119,15 @@ __device__ __forceinline__ float4 rec_load(__amdgpu_buffer_rsrc_t rs, uint32_t o
 // channels [keep, keep + n_out) already hold the refiner head's 1x1 conv W.(C + T bg); they get the
 // bias and the leaky ReLU here and go to out_refine, channels [0, keep) to out_color, the rest
 // nowhere.  No extra registers: the blend loop is the same kernel.
-// skip: strip pixels (bit = pixel) whose outputs are NOT written here (the quad tail's live
-// pixels, written by quad_store later).
 template <bool EMPTY, bool REFINE>
 __device__ __forceinline__ void store_strip(const Dims& d, const ImageArena& im, const Outputs& o,
                                             const float* bg, int b, int sx0, int sy0, int lane,
                                             const floatx16& acc0, const floatx16& acc1, float T,
-                                            float invd, uint32_t last, uint64_t skip = 0) {
+                                            float invd, uint32_t last) {
     const int64_t HW = (int64_t)d.H * d.W;
     const int px = sx0 + lane % kStripW;
     const int py = sy0 + lane / kStripW;
-    if (px < d.W && py < d.H && !((skip >> lane) & 1u)) {
+    if (px < d.W && py < d.H) {
         const int64_t pix = b * HW + (int64_t)py * d.W + px;
         im.final_T[pix] = T;
         im.n_contrib[pix] = last;
@@ -192,9 +149,8 @@ __device__ __forceinline__ void store_strip(const Dims& d, const ImageArena& im,
     const int qy1 = qy0 + 32 / kStripW;  // the upper 32 pixels of the strip
     const int hi = lane >> 5;
     const int hoff = hi * 4 * (int)HW;  // channels +4 for the upper half-wave
-    const int v0 = (qx < d.W && qy0 < d.H && !((skip >> j) & 1u)) ? (hoff + qy0 * d.W + qx) * 4 : 0x7FFFFFF0;
-    const int v1 = (qx < d.W && qy1 < d.H && !((skip >> (j + 32)) & 1u)) ? (hoff + qy1 * d.W + qx) * 4
-                                                                          : 0x7FFFFFF0;
+    const int v0 = (qx < d.W && qy0 < d.H) ? (hoff + qy0 * d.W + qx) * 4 : 0x7FFFFFF0;
+    const int v1 = (qx < d.W && qy1 < d.H) ? (hoff + qy1 * d.W + qx) * 4 : 0x7FFFFFF0;
     __amdgpu_buffer_rsrc_t rr = rs;
     if (REFINE)
         rr = __builtin_amdgcn_make_buffer_rsrc(o.out_refine + (int64_t)b * o.n_out * HW, 0,
@@ -207,8 +163,8 @@ __device__ __forceinline__ void store_strip(const Dims& d, const ImageArena& im,
         float x0 = EMPTY ? bgc : fmaf(T0, bgc, acc0[r]);
         float x1 = EMPTY ? bgc : fmaf(T1, bgc, acc1[r]);
         if (!REFINE) {
-            __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(x0), rs, v0, so, GSR_STORE_AUX);
-            __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(x1), rs, v1, so, GSR_STORE_AUX);
+            __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(x0), rs, v0, so, 0);
+            __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(x1), rs, v1, so, 0);
         } else {
             // branch-free: every channel is offered to both outputs; the one it does not belong to
             // gets an offset past its buffer (dropped by the buffer range check)
@@ -341,15 +297,19 @@ __device__ __forceinline__ void overflow_fill(const Dims& d, const Outputs& o) {
 
 // Work items: the 4 strips of each non-empty tile in strip_list order, most survivors first (items
 // [0, 4*NE)), then each empty tile whole (items [4*NE, 3*NE + B*T)).  Eight queues, one per
-// XCD, take every eighth item (item = x + 8k); a wave dequeues from its own XCD's queue and, once
-// that is drained, from the others, so no counter sees more than a fraction of the traffic.
+// XCD (queue_item); a wave dequeues from its own XCD's queue and, once that is drained, from the
+// others, so no counter sees more than a fraction of the traffic.
 //
-// The survivor stream runs as a three-stage software pipeline over k-steps (two Gaussians each) held
-// in three rotating register slots: the records and feature operand of step s+3 are loaded while
-// step s+1's alphas (the exp-heavy, transmittance-independent part) are computed and step s's
-// serial blend and MFMA accumulation run.
+// The survivor stream runs as a software pipeline over k-steps (two Gaussians each) held in NSLOT
+// rotating register slots: the records and feature operand of step s+NSLOT-1 are loaded while step
+// s+1's alphas are computed and step s's serial blend and MFMA accumulation run.
+//
+// SPLIT: 0 = f32 MFMA (exact), 1 = split-bf16 products of per-frame features, 2 = of the batch's
+// pre-split feature table (k_split_features).  HALF: one frame, a wave per half strip.  STATS / TL:
+// the instrumented variants (gsr_render_counters / gsr_render_timeline).  ABL: timing ablations
+// (GSR_TUNING builds only).
 template <bool EXACT, bool STATS, bool TL, bool REFINE, int ABL = 0, int SPLIT = 0, int NSLOT = 3,
-          bool HALF = false, bool QUAD = false, bool QONLY = false, bool HTAIL = false>
+          bool HALF = false>
 __device__ __forceinline__ void render_fwd_body(const Dims& d, const Inputs& in, const GeomArena& g,
                                                 const ImageArena& im, const BinArena& bn,
                                                 const Outputs& o) {
@@ -358,13 +318,10 @@ __device__ __forceinline__ void render_fwd_body(const Dims& d, const Inputs& in,
         return;
     }
     static_assert(!HALF || (!STATS && !TL && !REFINE && ABL == 0), "half-strip waves: production kernel only");
-    static_assert(!QUAD || (!HALF && !REFINE && SPLIT == 0 && NSLOT == 3), "quad tail: full-strip f32 kernel only");
-    static_assert(!QONLY || (QUAD && !STATS && !TL && ABL == 0), "quad-only waves: production kernel only");
-    static_assert(!HTAIL || (QUAD && !QONLY), "half tail: before the quad tail of the strip kernel");
+    static_assert(NSLOT == 3 || NSLOT == 5, "three or five pipeline slots");
     const uint32_t ne = g.ctrl[kCtrlNonEmpty];
     // HALF: every strip is two work items (one wave per 32-pixel half, the strip's rows 0-3 / 4-7)
-    // QONLY: every strip is four work items (one wave per 4x4 quad of the strip)
-    const uint32_t nstrip = (HALF ? 2u : QONLY ? 4u : 1u) * (uint32_t)kStrips * ne;
+    const uint32_t nstrip = (HALF ? 2u : 1u) * (uint32_t)kStrips * ne;
     const uint32_t nitems = nstrip + (uint32_t)(d.B * d.T) - ne;
     const int lane = threadIdx.x & 63;
     const int hi = lane >> 5;
@@ -378,9 +335,8 @@ __device__ __forceinline__ void render_fwd_body(const Dims& d, const Inputs& in,
             uint32_t k = 0;
             if (lane == 0) k = atomicAdd(&g.ctrl[kCtrlXcdQueue + kCtrlXcdStride * q], 1u);
             k = __builtin_amdgcn_readfirstlane(k);
-            item = HALF    ? queue_item_n<2>(q, k, ne, nitems - nstrip, in.xcd_map, g.ctrl)
-                   : QONLY ? queue_item_n<4>(q, k, ne, nitems - nstrip, in.xcd_map, g.ctrl)
-                           : queue_item(q, k, ne, nitems - nstrip, in.xcd_map, g.ctrl);
+            item = HALF ? queue_item_n<2>(q, k, ne, nitems - nstrip, in.xcd_map, g.ctrl)
+                        : queue_item(q, k, ne, nitems - nstrip, in.xcd_map, g.ctrl);
             if (item != 0xFFFFFFFFu) break;
             q = (q + 1) & 7u;
             q_left--;
@@ -393,16 +349,18 @@ __device__ __forceinline__ void render_fwd_body(const Dims& d, const Inputs& in,
             const int t = tile_g - b * d.T;
             const floatx16 unused = {};
             if (ABL == 8) {  /* timing ablation: no empty-tile stores */
-            } else if (GSR_FILL16 && !REFINE && (d.W & 3) == 0 &&((reinterpret_cast<uintptr_t>(o.out_color) |
-                                                      reinterpret_cast<uintptr_t>(o.out_invdepth)) & 15u) == 0 &&
+            } else if (!REFINE && (d.W & 3) == 0 &&
+                       ((reinterpret_cast<uintptr_t>(o.out_color) | reinterpret_cast<uintptr_t>(o.out_invdepth)) &
+                        15u) == 0 &&
                        (t % d.gx + 1) * GSR_BX <= d.W && (t / d.gx + 1) * GSR_BY <= d.H) {
                 fill_tile(d, im, o, in.bg + in.s_bg * b, b, t % d.gx, t / d.gx, lane);
-            } else
-            for (int sp = 0; sp < kStrips; sp++) {
-                int ex0, ey0;
-                strip_origin(t % d.gx, t / d.gx, sp, ex0, ey0);
-                store_strip<true, REFINE>(d, im, o, in.bg + in.s_bg * b, b, ex0, ey0, lane, unused, unused,
-                                          1.0f, 0.f, 0u);
+            } else {
+                for (int sp = 0; sp < kStrips; sp++) {
+                    int ex0, ey0;
+                    strip_origin(t % d.gx, t / d.gx, sp, ex0, ey0);
+                    store_strip<true, REFINE>(d, im, o, in.bg + in.s_bg * b, b, ex0, ey0, lane, unused, unused,
+                                              1.0f, 0.f, 0u);
+                }
             }
             if (TL && lane == 0 && item < o.timeline_cap) {  // empty tiles: k-steps 0xFFFFFFFF
                 uint32_t* rec = o.timeline + 4 * (size_t)item;
@@ -414,9 +372,8 @@ __device__ __forceinline__ void render_fwd_body(const Dims& d, const Inputs& in,
             continue;
         }
         const uint64_t t_start = TL ? __builtin_amdgcn_s_memrealtime() : 0;
-        const uint32_t code = im.strip_list[HALF ? item >> 1 : QONLY ? item >> 2 : item];
+        const uint32_t code = im.strip_list[HALF ? item >> 1 : item];
         const int half = HALF ? (int)(item & 1u) : 0;
-        const int quad = QONLY ? (int)(item & 3u) : 0;  // 4x4 quad of the strip (x = quad & 1, y = quad >> 1)
         const int tile_g = (int)(code >> 2);
         const int strip = (int)(code & 3u);
         const int b = tile_g / d.T;
@@ -431,14 +388,10 @@ __device__ __forceinline__ void render_fwd_body(const Dims& d, const Inputs& in,
         const int py = sy0 + lpix / kStripW;
         const float pfx = (float)px, pfy = (float)py;
         bool done = !(px < d.W && py < d.H);
-        // GSR_TAKE_VCC: the throughput strip loop keeps Tc (T while live, 0 once stopped) in place of done
-        constexpr bool VCC = GSR_TAKE_VCC && !HALF && !STATS && !TL && !QUAD && !QONLY && ABL == 0;
-        float Tc = done ? 0.0f : 1.0f;
         float T = 1.0f, invd = 0.f;
         uint32_t last = 0, stop = 0;
         const uint32_t smask_bit = 1u << (28 + strip);
-        const bool strip_empty = im.strip_cnt[(int64_t)tile_g * kStrips + strip] == 0u;
-        if (!QONLY && !STATS && !TL && strip_empty) {
+        if (!STATS && !TL && im.strip_cnt[(int64_t)tile_g * kStrips + strip] == 0u) {
             // no list entry reaches the strip (k_strip_count): nothing is taken anywhere in it, so
             // its outputs are the background, T = 1, n_contrib = 0, inverse depth 0 -- the values
             // the list walk would give -- without walking the tile's list
@@ -450,15 +403,14 @@ __device__ __forceinline__ void render_fwd_body(const Dims& d, const Inputs& in,
             continue;
         }
         const uint2 range = im.ranges[tile_g];
-        // (QONLY: a strip no entry reaches walks an empty list -- the quad epilogue stores the background)
-        const int n = (QONLY && strip_empty) ? 0 : (int)(range.y - range.x);
+        const int n = (int)(range.y - range.x);
         const uint32_t* __restrict__ plist = bn.point_list + range.x;
         // render records through a buffer resource: the byte offset of a (wave-uniform) record is
         // one SGPR, no 64-bit address arithmetic per survivor
         const __amdgpu_buffer_rsrc_t rrs = __builtin_amdgcn_make_buffer_rsrc(
             (void*)(g.rrec + (int64_t)b * d.P * 2), 0, (int)min((int64_t)d.P * 32, (int64_t)0x7FFFFFFF), 0x00020000);
-        // this wave's record staging slot (GSR_REC_PATH 3)
-        // (words 0..15; lanes 8..63 write their out-of-range zeros to the spare words 24..87)
+        // this wave's record staging slot (words 0..15; lanes 8..63 write their out-of-range zeros to
+        // the spare words 24..87)
         __shared__ unsigned rec_lds_all[GSR_TILE_PIX / 64][88];
         unsigned* rec_lds = rec_lds_all[threadIdx.x >> 6];
         const int rec_widx = lane < 8 ? lane : 16 + lane;
@@ -475,13 +427,11 @@ __device__ __forceinline__ void render_fwd_body(const Dims& d, const Inputs& in,
             (int)min((int64_t)d.P * GSR_C * 4, (int64_t)0x7FFFFFFF), 0x00020000);
 
         floatx16 acc0, acc1;
-        uint4x sa_ = {0u, 0u, 0u, 0u}, sb0_ = {0u, 0u, 0u, 0u}, sb1_ = {0u, 0u, 0u, 0u};  // SPLIT operands, k 4..7 stay 0
 #pragma unroll
         for (int r = 0; r < 16; r++) { acc0[r] = 0.f; acc1[r] = 0.f; }
-        uint64_t n_surv = 0, n_steps = 0, n_contrib_pairs = 0, n_staged = 0, n_dead = 0, n_qsurv = 0, n_hsurv = 0;
+        uint64_t n_surv = 0, n_steps = 0, n_contrib_pairs = 0, n_staged = 0, n_dead = 0;
 
-        // Survivor stream: wave-uniform state walking the list 64 entries at a time; the next
-        // chunk's entries (index | strip mask << 28) are always in flight.
+        // Survivor stream: wave-uniform state walking the list 64 entries at a time.
         int base = -64;
         uint64_t mask = 0;
         uint32_t cidx = 0;
@@ -505,8 +455,8 @@ __device__ __forceinline__ void render_fwd_body(const Dims& d, const Inputs& in,
             }                                                                                       \
             ok_;                                                                                    \
         })
-        // stage 1: fetch the next k-step (two survivors) into slot S: render records (uniform
-        // vector loads, in-order completion) and this lane's feature operand
+        // stage 1: fetch the next k-step (two survivors) into slot S: render records and this
+        // lane's feature word (in-order completion)
 #define GSR_FETCH(S)                                                                                \
         {                                                                                           \
             uint32_t ga_ = 0, gb_ = 0;                                                              \
@@ -532,20 +482,17 @@ __device__ __forceinline__ void render_fwd_body(const Dims& d, const Inputs& in,
                 if (!S##hb) { gb_ = (uint32_t)d.P; pb_ = pa_; }                                     \
             }                                                                                       \
             S##pa = pa_; S##pb = pb_;                                                               \
-            if (HALF && GSR_HALF_REC_DIRECT) {  /* lane half h: survivor h's whole record */        \
+            if (HALF) {  /* lane half h: survivor h's whole record, two 16-B loads */               \
                 const uint32_t gl_ = hi ? gb_ : ga_;                                                \
                 S##a0 = rec_load(rrs, gl_ * 32);                                                    \
                 S##a1 = rec_load(rrs, gl_ * 32 + 16);                                               \
-            } else if (GSR_REC_PATH == 3) {  /* lanes 0..7: dword `lane` of both records, SGPR offsets */ \
+            } else {  /* lanes 0..7: dword `lane` of both records, SGPR offsets */                  \
                 S##r = __builtin_amdgcn_raw_buffer_load_b32(rrs, rec_voff, (int)(ga_ * 32), 0);     \
                 S##r2 = __builtin_amdgcn_raw_buffer_load_b32(rrs, rec_voff, (int)(gb_ * 32), 0);    \
-            } else {                                                                                \
-                S##a0 = rec_load(rrs, ga_ * 32); S##a1 = rec_load(rrs, ga_ * 32 + 16);              \
-                S##b0 = rec_load(rrs, gb_ * 32); S##b1 = rec_load(rrs, gb_ * 32 + 16);              \
             }                                                                                       \
             /* this lane's feature word: channel ch of survivor a (lanes 0..31) or b (32..63), */  \
-            /* the survivor's row offset in the SGPR offset (range-checked like voffset: past */    \
-            /* offset in SGPRs; the other half's lanes are out of range and read 0) */            \
+            /* the survivor's row offset in the SGPR offset (range-checked like voffset: the */     \
+            /* other half's lanes are out of range and read 0) */                                   \
             S##fa = ABL == 2 ? 0u : __builtin_amdgcn_raw_buffer_load_b32(frs, feat_voff_a,          \
                                                                         (int)(ga_ * (GSR_C * 4)), 0); \
             S##fb = ABL == 2 ? 0u : __builtin_amdgcn_raw_buffer_load_b32(frs, feat_voff_b,          \
@@ -554,37 +501,21 @@ __device__ __forceinline__ void render_fwd_body(const Dims& d, const Inputs& in,
         // stage 2: the pixel-local alphas of slot S (a missing survivor has alpha 0): the records
         // through the wave's LDS slot (GSR_ALPHA_LDS), then the alpha arithmetic (GSR_ALPHA_MATH)
 #define GSR_ALPHA_LDS(S)                                                                            \
-        {                                                                                           \
-            if (HALF && GSR_HALF_REC_DIRECT) {  /* (loaded straight into a0 / a1 by GSR_FETCH) */    \
-            } else if (HALF) {  /* each lane its own Gaussian's record: a in lanes 0-31, b in 32-63 */ \
-                rec_lds[rec_widx] = S##r; rec_lds[rec_widx + 8] = S##r2;                            \
-                __builtin_amdgcn_wave_barrier();                                                    \
-                S##a0 = __builtin_bit_cast(float4, *(const uint4x*)&rec_lds[8 * hi]);               \
-                S##a1 = __builtin_bit_cast(float4, *(const uint4x*)&rec_lds[8 * hi + 4]);           \
-                __builtin_amdgcn_wave_barrier();                                                    \
-            } else if (GSR_REC_PATH == 3) {  /* uniform-address b128 reads (lanes 8..63: spare) */  \
-                rec_lds[rec_widx] = S##r; rec_lds[rec_widx + 8] = S##r2;                            \
-                __builtin_amdgcn_wave_barrier();                                                    \
-                S##a0 = __builtin_bit_cast(float4, *(const uint4x*)&rec_lds[0]);                    \
-                S##a1 = __builtin_bit_cast(float4, *(const uint4x*)&rec_lds[4]);                    \
-                S##b0 = __builtin_bit_cast(float4, *(const uint4x*)&rec_lds[8]);                    \
-                S##b1 = __builtin_bit_cast(float4, *(const uint4x*)&rec_lds[12]);                   \
-                __builtin_amdgcn_wave_barrier();                                                    \
-            }                                                                                       \
+        if (!HALF) {  /* uniform-address b128 reads (lanes 8..63 wrote spare words) */              \
+            rec_lds[rec_widx] = S##r; rec_lds[rec_widx + 8] = S##r2;                                \
+            __builtin_amdgcn_wave_barrier();                                                        \
+            S##a0 = __builtin_bit_cast(float4, *(const uint4x*)&rec_lds[0]);                        \
+            S##a1 = __builtin_bit_cast(float4, *(const uint4x*)&rec_lds[4]);                        \
+            S##b0 = __builtin_bit_cast(float4, *(const uint4x*)&rec_lds[8]);                        \
+            S##b1 = __builtin_bit_cast(float4, *(const uint4x*)&rec_lds[12]);                       \
+            __builtin_amdgcn_wave_barrier();                                                        \
         }
 #define GSR_ALPHA_MATH(S)                                                                           \
         {                                                                                           \
-            if (HALF) {                                                                             \
-                S##al = alpha_of<EXACT>(S##a0, S##a1, pfx, pfy);                                    \
-                S##ai = S##a0.w;                                                                    \
-            } else {                                                                                \
-                S##al = alpha_of<EXACT>(S##a0, S##a1, pfx, pfy);                                    \
+            S##al = alpha_of<EXACT>(S##a0, S##a1, pfx, pfy);                                        \
+            S##ai = S##a0.w;                                                                        \
+            if (!HALF) {                                                                            \
                 S##bl = alpha_of<EXACT>(S##b0, S##b1, pfx, pfy);                                    \
-                if (VCC) {  /* below 1/255: never taken (forward.cu:362-363) */                     \
-                    S##al = S##al < 1.0f / 255.0f ? 0.0f : S##al;                                   \
-                    S##bl = S##bl < 1.0f / 255.0f ? 0.0f : S##bl;                                   \
-                }                                                                                   \
-                S##ai = S##a0.w;                                                                    \
                 S##bi = S##b0.w;                                                                    \
             }                                                                                       \
             S##f = __uint_as_float(S##fa | S##fb);                                                  \
@@ -619,16 +550,12 @@ __device__ __forceinline__ void render_fwd_body(const Dims& d, const Inputs& in,
             } else {                                                                                \
                 acc0 = __builtin_amdgcn_mfma_f32_32x32x2f32(S##f, w_, acc0, 0, 0, 0);               \
             }                                                                                       \
-        } else if (!GSR_SKIP_DEAD || STATS || TL ||  /* a k-step no live pixel takes: skipped (exact) */ \
-                   __builtin_amdgcn_ballot_w64(!done && (!(S##al < 1.0f / 255.0f) ||                \
-                                                         !(S##bl < 1.0f / 255.0f))) != 0ull) {       \
+        } else {                                                                                    \
             const float f_ = S##f;                                                                  \
             const bool was_done_ = done;                                                            \
-            const float wa_ = VCC ? take_vcc(S##al, S##ai, (uint32_t)S##pa, Tc, T, invd, last)      \
-                                  : take_step(S##al, S##ai, (uint32_t)S##pa, T, invd, last, done);  \
+            const float wa_ = take_step(S##al, S##ai, (uint32_t)S##pa, T, invd, last, done);        \
             const bool done_a_ = done;                                                              \
-            const float wb_ = VCC ? take_vcc(S##bl, S##bi, (uint32_t)S##pb, Tc, T, invd, last)      \
-                                  : take_step(S##bl, S##bi, (uint32_t)S##pb, T, invd, last, done);  \
+            const float wb_ = take_step(S##bl, S##bi, (uint32_t)S##pb, T, invd, last, done);        \
             if (STATS) {                                                                            \
                 if (!was_done_ && done_a_) stop = (uint32_t)S##pa;                                  \
                 else if (!done_a_ && done) stop = (uint32_t)S##pb;                                  \
@@ -637,50 +564,28 @@ __device__ __forceinline__ void render_fwd_body(const Dims& d, const Inputs& in,
                 n_surv += S##v ? (S##hb ? 2 : 1) : 0;                                               \
             }                                                                                       \
             if (STATS || TL) n_steps += S##v ? 1 : 0;                                               \
-            const auto sw_ = __builtin_amdgcn_permlane32_swap(__float_as_uint(wa_),                 \
-                                                              __float_as_uint(wb_), false, false);  \
-            if (ABL == 1) {  /* timing ablation: VALU stand-in for the MFMAs */                  \
+            if (ABL == 1) {  /* timing ablation: VALU stand-in for the MFMAs */                     \
+                const auto sw_ = __builtin_amdgcn_permlane32_swap(__float_as_uint(wa_),             \
+                                                                  __float_as_uint(wb_), false, false); \
                 acc0[0] = fmaf(f_, __uint_as_float(sw_[0]), acc0[0]);                               \
                 acc1[0] = fmaf(f_, __uint_as_float(sw_[1]), acc1[0]);                               \
-            } else if (ABL == 4) {  /* timing ablation: bf16 32x32x16 MFMAs in place of the f32 ones */ \
-                const unsigned fb_ = __float_as_uint(f_);                                           \
-                const bf16x8 a_ = __builtin_bit_cast(bf16x8, (uint4x)(fb_, fb_ >> 16, fb_, 0u));    \
-                const bf16x8 b0_ = __builtin_bit_cast(bf16x8, (uint4x)(sw_[0], sw_[0] >> 16, sw_[0], 0u)); \
-                const bf16x8 b1_ = __builtin_bit_cast(bf16x8, (uint4x)(sw_[1], sw_[1] >> 16, sw_[1], 0u)); \
-                acc0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a_, b0_, acc0, 0, 0, 0);               \
-                acc1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a_, b1_, acc1, 0, 0, 0);               \
             } else if (SPLIT) {  /* k 0..3 of each half: f_hi.w_hi + f_lo.w_hi + f_hi.w_lo + f_lo.w_lo */ \
+                /* split both weights, then swap the (hi, hi) and (lo, lo) words: the swaps */      \
+                /* consume the split words, the weights stay for the inverse depth */               \
                 const unsigned fp_ = S##fp;                                                         \
-                unsigned h0_, l0_, h1_, l1_;                                                        \
-                split_hh_ll(__uint_as_float(sw_[0]), h0_, l0_);                                     \
-                split_hh_ll(__uint_as_float(sw_[1]), h1_, l1_);                                     \
-                if (GSR_SPLIT_FIRST) {  /* split both weights, then swap the (hi, hi) and (lo, lo) words: */ \
-                    /* the swaps consume the split words, the weights stay for the inverse depth */ \
-                    unsigned ha_, la_, hb_, lb_;                                                    \
-                    split_hh_ll(wa_, ha_, la_);                                                     \
-                    split_hh_ll(wb_, hb_, lb_);                                                     \
-                    const auto sh_ = __builtin_amdgcn_permlane32_swap(ha_, hb_, false, false);      \
-                    const auto sl_ = __builtin_amdgcn_permlane32_swap(la_, lb_, false, false);      \
-                    const uint2x a2_ = {fp_, fp_}, b0_ = {sh_[0], sl_[0]}, b1_ = {sh_[1], sl_[1]};  \
-                    acc0 = __builtin_amdgcn_mfma_f32_32x32x8bf16_1k(__builtin_bit_cast(shortx4, a2_), \
-                                                                   __builtin_bit_cast(shortx4, b0_), acc0, 0, 0, 0); \
-                    acc1 = __builtin_amdgcn_mfma_f32_32x32x8bf16_1k(__builtin_bit_cast(shortx4, a2_), \
-                                                                   __builtin_bit_cast(shortx4, b1_), acc1, 0, 0, 0); \
-                } else if (GSR_MFMA_K8) {  /* k = 8: exactly the four products per lane half, no padding */ \
-                    const uint2x a2_ = {fp_, fp_}, b0_ = {h0_, l0_}, b1_ = {h1_, l1_};              \
-                    acc0 = __builtin_amdgcn_mfma_f32_32x32x8bf16_1k(__builtin_bit_cast(shortx4, a2_), \
-                                                                   __builtin_bit_cast(shortx4, b0_), acc0, 0, 0, 0); \
-                    acc1 = __builtin_amdgcn_mfma_f32_32x32x8bf16_1k(__builtin_bit_cast(shortx4, a2_), \
-                                                                   __builtin_bit_cast(shortx4, b1_), acc1, 0, 0, 0); \
-                } else {                                                                            \
-                    sa_.x = fp_; sa_.y = fp_;                                                       \
-                    sb0_.x = h0_; sb0_.y = l0_; sb1_.x = h1_; sb1_.y = l1_;                         \
-                    acc0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, sa_), \
-                                                                   __builtin_bit_cast(bf16x8, sb0_), acc0, 0, 0, 0); \
-                    acc1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, sa_), \
-                                                                   __builtin_bit_cast(bf16x8, sb1_), acc1, 0, 0, 0); \
-                }                                                                                   \
+                unsigned ha_, la_, hb_, lb_;                                                        \
+                split_hh_ll(wa_, ha_, la_);                                                         \
+                split_hh_ll(wb_, hb_, lb_);                                                         \
+                const auto sh_ = __builtin_amdgcn_permlane32_swap(ha_, hb_, false, false);          \
+                const auto sl_ = __builtin_amdgcn_permlane32_swap(la_, lb_, false, false);          \
+                const uint2x a2_ = {fp_, fp_}, b0_ = {sh_[0], sl_[0]}, b1_ = {sh_[1], sl_[1]};      \
+                acc0 = __builtin_amdgcn_mfma_f32_32x32x8bf16_1k(__builtin_bit_cast(shortx4, a2_),   \
+                                                               __builtin_bit_cast(shortx4, b0_), acc0, 0, 0, 0); \
+                acc1 = __builtin_amdgcn_mfma_f32_32x32x8bf16_1k(__builtin_bit_cast(shortx4, a2_),   \
+                                                               __builtin_bit_cast(shortx4, b1_), acc1, 0, 0, 0); \
             } else {                                                                                \
+                const auto sw_ = __builtin_amdgcn_permlane32_swap(__float_as_uint(wa_),             \
+                                                                  __float_as_uint(wb_), false, false); \
                 const float fa_ = ABL == 2 ? 1.0f : f_;  /* timing ablation: no feature operand */  \
                 acc0 = __builtin_amdgcn_mfma_f32_32x32x2f32(fa_, __uint_as_float(sw_[0]), acc0, 0, 0, 0); \
                 acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(fa_, __uint_as_float(sw_[1]), acc1, 0, 0, 0); \
@@ -693,9 +598,7 @@ __device__ __forceinline__ void render_fwd_body(const Dims& d, const Inputs& in,
         GSR_SLOT(C)
         // An invalid slot takes nothing (alpha 0, feature 0); the loop leaves only at its head and
         // its foot, which keeps the MFMA accumulators in one register chain.
-        bool to_quad = false, to_half = false;
-        if constexpr (QONLY) {
-        } else if constexpr (NSLOT == 3) {
+        if constexpr (NSLOT == 3) {
             GSR_FETCH(A)
             GSR_FETCH(B)
             GSR_FETCH(C)
@@ -707,22 +610,7 @@ __device__ __forceinline__ void render_fwd_body(const Dims& d, const Inputs& in,
                 GSR_FETCH(B)
                 GSR_STEP(A, C)
                 GSR_FETCH(C)
-                if constexpr (QUAD) {
-                    // at most 16 pixels still blending: the rest of the list runs in the quad tail
-                    const uint64_t live_ = __ballot(!done);
-                    if (live_ == 0ull) break;  // every pixel of the strip finished
-                    const int nl_ = __builtin_popcountll(live_);
-                    if (nl_ <= 16) { to_quad = true; break; }
-                    if (HTAIL && nl_ <= 32) { to_half = true; break; }
-                } else {
-                    if (!(VCC ? __any(Tc != 0.0f) : __any(!done))) break;  // every pixel of the strip finished
-                }
-            }
-            if (QUAD && (to_quad || to_half)) {
-                // drain the pipeline in strip layout: slot A's alphas are computed, B and C fetched
-                GSR_STEP(B, A)
-                GSR_STEP(C, B)
-                GSR_TAKE(C)
+                if (!__any(!done)) break;  // every pixel of the strip finished
             }
         } else {
             // latency mode (single-frame launches, where one wave's strip sets the kernel time): five
@@ -746,387 +634,9 @@ __device__ __forceinline__ void render_fwd_body(const Dims& d, const Inputs& in,
                 GSR_FETCH(D)
                 GSR_STEP(A, E)
                 GSR_FETCH(E)
-                if (!(VCC ? __any(Tc != 0.0f) : __any(!done))) break;
+                if (!__any(!done)) break;
             }
         }
-        // ---- half tail ----
-        // 17..32 pixels still blending: compacted into 32 slots, two survivors per step with ONE
-        // alpha per lane (lane = slot + 32 q, Gaussian q), the pair's blend run in both lane halves
-        // (one permlane32 swap per value), one v_mfma_f32_32x32x2_f32 per step on the slots' 32x32
-        // colour tile (the strip layout's acc0 with slots for pixels) -- half the matrix work and 60%
-        // of the vector work of a strip k-step for the same two survivors.  Reaching <= 16 live slots
-        // it hands over to the quad tail.  Bit-exact as the quad tail (each pixel's fma chain goes on).
-        uint64_t half_live = 0;     // strip pixels handed to the half tail
-        uint64_t half_quad = 0;     // half slots handed on to the quad tail (bit = slot)
-        uint64_t ev_half = 0;       // STATS: pairs visited of the half slots stored by it
-        const int hj = lane & 31, hq = lane >> 5;
-        int hp = 0;                 // the half slot's strip pixel
-        bool hslot_ok = false;
-        float Th = 1.0f, invdh = 0.f;
-        uint32_t lasth = 0, stoph = 0;
-        bool doneh = true;
-        floatx16 ha;
-        const __amdgpu_buffer_rsrc_t qfs = __builtin_amdgcn_make_buffer_rsrc(
-            (void*)(in.colors + in.s_colors * b), 0, (int)min((int64_t)d.P * GSR_C * 4, (int64_t)0x7FFFFFFF),
-            0x00020000);  // f32 features of the half / quad tails (exact mode only)
-        if constexpr (HTAIL) if (to_half) {
-            half_live = __ballot(!done);
-            const int nlive = __builtin_popcountll(half_live);
-            store_strip<false, false>(d, im, o, in.bg + in.s_bg * b, b, sx0, sy0, lane, acc0, acc1, T, invd, last,
-                                      half_live);
-            const uint32_t my_slot = __builtin_amdgcn_mbcnt_hi((uint32_t)(half_live >> 32),
-                                                               __builtin_amdgcn_mbcnt_lo((uint32_t)half_live, 0u));
-            if ((half_live >> lane) & 1u) rec_lds[my_slot] = (unsigned)lane;
-            __builtin_amdgcn_wave_barrier();
-            hslot_ok = hj < nlive;
-            hp = hslot_ok ? (int)rec_lds[hj] : 0;
-            __builtin_amdgcn_wave_barrier();
-            Th = __shfl(T, hp);
-            invdh = __shfl(invd, hp);
-            lasth = (uint32_t)__shfl((int)last, hp);
-            stoph = STATS ? (uint32_t)__shfl((int)stop, hp) : 0u;
-            doneh = !hslot_ok;
-            // ha[r] at lane l: channel (r & 3) + 8 (r >> 2) + 4 hq of slot hj = the strip layout's register r
-            // of pixel hp, at lane (hp & 31) + 32 hq of acc_{hp >= 32}
-            {
-                const int src = (hp & 31) + 32 * hq;
-                const bool up = hp >= 32;
-#pragma unroll
-                for (int r = 0; r < 16; r++) {
-                    const float x0 = __shfl(acc0[r], src), x1 = __shfl(acc1[r], src);
-                    ha[r] = up ? x1 : x0;
-                }
-            }
-            const float hfx = (float)(sx0 + hp % kStripW), hfy = (float)(sy0 + hp / kStripW);
-            const int hrec_w = lane < 16 ? lane : 24 + lane;  // lanes 16..63 -> spare words 40..87
-#define GSR_HFETCH(S)                                                                               \
-            {                                                                                       \
-                uint32_t ga_ = (uint32_t)d.P, gb_ = (uint32_t)d.P;                                  \
-                int pa_ = 0, pb_ = 0;                                                               \
-                if (__builtin_expect(__builtin_popcountll(mask) >= 2, 1)) {                         \
-                    const int i0_ = (int)__builtin_ctzll(mask); mask &= mask - 1;                   \
-                    const int i1_ = (int)__builtin_ctzll(mask); mask &= mask - 1;                   \
-                    ga_ = __builtin_amdgcn_readlane(cidx, i0_) & kIndexMask; pa_ = base + i0_ + 1;  \
-                    gb_ = __builtin_amdgcn_readlane(cidx, i1_) & kIndexMask; pb_ = base + i1_ + 1;  \
-                    S##v = true;                                                                    \
-                } else {                                                                            \
-                    S##v = GSR_NEXT(ga_, pa_);                                                      \
-                    if (S##v && !GSR_NEXT(gb_, pb_)) gb_ = (uint32_t)d.P;                           \
-                    if (!S##v) ga_ = (uint32_t)d.P;                                                 \
-                }                                                                                   \
-                S##pa = pa_; S##pb = pb_;                                                           \
-                const uint32_t gr_ = (lane & 8) ? gb_ : ga_;                                        \
-                S##r = __builtin_amdgcn_raw_buffer_load_b32(                                        \
-                    rrs, lane < 16 ? (int)(gr_ * 32u + (uint32_t)(lane & 7) * 4u) : (int)kOOB, 0, 0); \
-                const uint32_t gf_ = hq ? gb_ : ga_;                                                \
-                S##f = __builtin_amdgcn_raw_buffer_load_b32(qfs, (int)(gf_ * (uint32_t)(GSR_C * 4) + (uint32_t)hj * 4u), 0, 0); \
-            }
-#define GSR_HSTEP(S)                                                                                \
-            {                                                                                       \
-                rec_lds[hrec_w] = S##r;                                                             \
-                __builtin_amdgcn_wave_barrier();                                                    \
-                const float4 ra_ = __builtin_bit_cast(float4, *(const uint4x*)&rec_lds[8 * hq]);    \
-                const float4 rc_ = __builtin_bit_cast(float4, *(const uint4x*)&rec_lds[8 * hq + 4]); \
-                __builtin_amdgcn_wave_barrier();                                                    \
-                const float al_ = alpha_of<EXACT>(ra_, rc_, hfx, hfy);                              \
-                const auto a_ = __builtin_amdgcn_permlane32_swap(__float_as_uint(al_), __float_as_uint(al_), \
-                                                                  false, false);                    \
-                const auto i_ = __builtin_amdgcn_permlane32_swap(__float_as_uint(ra_.w), __float_as_uint(ra_.w), \
-                                                                  false, false);                    \
-                const bool was_ = doneh;                                                            \
-                const float w0_ = take_step(__uint_as_float(a_[0]), __uint_as_float(i_[0]), (uint32_t)S##pa, \
-                                            Th, invdh, lasth, doneh);                               \
-                if (STATS && !was_ && doneh) stoph = (uint32_t)S##pa;                               \
-                const bool was1_ = doneh;                                                           \
-                const float w1_ = take_step(__uint_as_float(a_[1]), __uint_as_float(i_[1]), (uint32_t)S##pb, \
-                                            Th, invdh, lasth, doneh);                               \
-                if (STATS && !was1_ && doneh) stoph = (uint32_t)S##pb;                              \
-                const float wq_ = hq ? w1_ : w0_;                                                   \
-                ha = __builtin_amdgcn_mfma_f32_32x32x2f32(__uint_as_float(S##f), wq_, ha, 0, 0, 0); \
-                if (STATS) {                                                                        \
-                    n_contrib_pairs += __popcll(__ballot(wq_ > 0.f));                               \
-                    n_hsurv += 1 + (S##pb > 0);                                                     \
-                }                                                                                   \
-                if (TL) n_steps += 1;                                                               \
-            }
-            bool Xv = false, Yv = false, to_q = false;
-            int Xpa, Xpb, Ypa, Ypb;
-            unsigned Xr, Xf, Yr, Yf;
-            // live half slots (lanes 0..31 carry every slot; the upper half duplicates them)
-#define GSR_HLIVE() ((uint32_t)__ballot(!doneh))
-            if (nlive > 0) {
-                GSR_HFETCH(X)
-                while (Xv) {
-                    GSR_HFETCH(Y)
-                    GSR_HSTEP(X)
-                    if (!Yv) break;
-                    {
-                        const int nl_ = __builtin_popcount(GSR_HLIVE());
-                        if (nl_ == 0) break;
-                        if (nl_ <= 16) {  /* Y's survivors are fetched: take them here first */
-                            GSR_HSTEP(Y)
-                            to_q = true;
-                            break;
-                        }
-                    }
-                    GSR_HFETCH(X)
-                    GSR_HSTEP(Y)
-                    {
-                        const int nl_ = __builtin_popcount(GSR_HLIVE());
-                        if (nl_ == 0) break;
-                        if (nl_ <= 16) {  /* X is fetched: take it, then the quad tail */
-                            if (Xv) GSR_HSTEP(X)
-                            to_q = true;
-                            break;
-                        }
-                    }
-                }
-            }
-#undef GSR_HFETCH
-#undef GSR_HSTEP
-            // slots still live go on to the quad tail (if it takes over), the rest are final now
-            const uint32_t hl = to_q ? GSR_HLIVE() : 0u;
-#undef GSR_HLIVE
-            half_quad = hl;
-            to_quad = to_q && hl != 0u;
-            {
-                const int64_t HW = (int64_t)d.H * d.W;
-                const int64_t pix = b * HW + (int64_t)(sy0 + hp / kStripW) * d.W + (sx0 + hp % kStripW);
-                const bool st = hslot_ok && !((hl >> hj) & 1u);
-                if (st && hq == 0) {
-                    im.final_T[pix] = Th;
-                    im.n_contrib[pix] = lasth;
-                    if (o.out_invdepth) o.out_invdepth[pix] = invdh;
-                }
-                const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
-                    o.out_color + (int64_t)b * GSR_C * HW, 0, (int)((int64_t)GSR_C * HW * 4), 0x00020000);
-                const float* bgp = in.bg + in.s_bg * b;
-                const float bgl = bgp[lane & 31];
-                const int vo = st ? (int)((pix - b * HW) * 4) : 0x7FFFFFF0;
-#pragma unroll
-                for (int r = 0; r < 16; r++) {
-                    const int c = (r & 3) + 8 * (r >> 2) + 4 * hq;
-                    const float bgc = __shfl(bgl, c);
-                    __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(fmaf(Th, bgc, ha[r])), rs, vo,
-                                                          c * (int)HW * 4, 0);
-                }
-                if (STATS && st && hq == 0) ev_half = doneh ? stoph : (uint32_t)n;
-            }
-        }
-
-        // ---- quad tail ----
-        // The strip's <= 16 still-blending pixels, compacted into 16 slots; each step takes the next
-        // FOUR survivors, lane = slot + 16 q computing Gaussian q's alpha at its slot's pixel (one
-        // alpha per lane instead of two alphas per lane for 64 mostly finished pixels).  Every lane
-        // of a slot runs the slot's serial blend over the four alphas (broadcast by one permlane16
-        // and two permlane32 swaps) in list order, and keeps its own Gaussian's weight as the
-        // K = 4 operand of two v_mfma_f32_16x16x4_f32 (channels 0-15, 16-31): an exact k-ordered fma
-        // chain continuing each pixel's colour chain, so the image is bit-identical to the strip
-        // layout's (and the oracle's).  The strip's finished pixels are stored first; the slots' state
-        // (T, inverse depth, last contributor, colour accumulators) moves over by ds_bpermute.
-        uint64_t quad_live = 0;  // strip pixels handed to the quad tail (stored by it)
-        uint64_t ev_quad = 0;    // STATS: the quad slots' pairs visited
-        if (QUAD && (QONLY || to_quad)) {
-            const int j = lane & 15, q = lane >> 4;
-            int nlive, p;
-            bool slot_ok;
-            float Ts, invds;
-            uint32_t lasts, stops;
-            floatx4 qa0, qa1;
-            if constexpr (QONLY) {
-                // a fresh 4x4 quad: slot j = quad pixel (j % 4, j / 4)
-                p = (4 * (quad >> 1) + (j >> 2)) * kStripW + 4 * (quad & 1) + (j & 3);
-                slot_ok = sx0 + p % kStripW < d.W && sy0 + p / kStripW < d.H;
-                nlive = 16;
-                Ts = 1.0f; invds = 0.f; lasts = 0u; stops = 0u;
-#pragma unroll
-                for (int r = 0; r < 4; r++) { qa0[r] = 0.f; qa1[r] = 0.f; }
-            } else if (HTAIL && to_half) {
-                // from the half tail: quad slot j <- the j-th live half slot
-                nlive = __builtin_popcount((uint32_t)half_quad);
-                const uint32_t my_slot = __builtin_amdgcn_mbcnt_lo((uint32_t)half_quad, 0u);
-                if (lane < 32 && ((half_quad >> lane) & 1u)) rec_lds[my_slot] = (unsigned)lane;
-                __builtin_amdgcn_wave_barrier();
-                slot_ok = j < nlive;
-                const int hs = slot_ok ? (int)rec_lds[j] : 0;
-                __builtin_amdgcn_wave_barrier();
-                p = __shfl(hp, hs);
-                Ts = __shfl(Th, hs);
-                invds = __shfl(invdh, hs);
-                lasts = (uint32_t)__shfl((int)lasth, hs);
-                stops = STATS ? (uint32_t)__shfl((int)stoph, hs) : 0u;
-                // channel c of half slot hs sits in ha[(c & 3) + 4 (c >> 3)] at lane hs + 32 ((c >> 2) & 1)
-                const int src = hs + 32 * (q & 1);
-                const bool h2 = (q >> 1) != 0;
-#pragma unroll
-                for (int r = 0; r < 4; r++) {
-                    const float a0 = __shfl(ha[r], src), a1 = __shfl(ha[r + 4], src);
-                    qa0[r] = h2 ? a1 : a0;
-                    const float b0 = __shfl(ha[r + 8], src), b1 = __shfl(ha[r + 12], src);
-                    qa1[r] = h2 ? b1 : b0;
-                }
-            } else {
-            quad_live = __ballot(!done);
-            nlive = __builtin_popcountll(quad_live);
-            // the strip's finished pixels: final now
-            store_strip<false, false>(d, im, o, in.bg + in.s_bg * b, b, sx0, sy0, lane, acc0, acc1, T, invd, last,
-                                      quad_live);
-            // slot j <- the j-th live pixel (in lane order), through the wave's LDS words
-            const uint32_t my_slot = __builtin_amdgcn_mbcnt_hi((uint32_t)(quad_live >> 32),
-                                                               __builtin_amdgcn_mbcnt_lo((uint32_t)quad_live, 0u));
-            if ((quad_live >> lane) & 1u) rec_lds[my_slot] = (unsigned)lane;
-            __builtin_amdgcn_wave_barrier();
-            slot_ok = j < nlive;
-            p = slot_ok ? (int)rec_lds[j] : 0;
-            __builtin_amdgcn_wave_barrier();
-            // the slot's pixel state (duplicated over the four lane groups)
-            Ts = __shfl(T, p);
-            invds = __shfl(invd, p);
-            lasts = (uint32_t)__shfl((int)last, p);
-            stops = STATS ? (uint32_t)__shfl((int)stop, p) : 0u;
-            // colour accumulators into the 16x16x4 layout: qa0[r] = channel 4q + r, qa1[r] = 16 + 4q + r
-            // of slot j; in the strip layout channel c of pixel p sits in acc_{p >= 32}[(c & 3) + 4 (c >> 3)]
-            // at lane (p & 31) + 32 ((c >> 2) & 1)
-            {
-                const int src = (p & 31) + 32 * (q & 1);
-                const bool up = p >= 32, h2 = (q >> 1) != 0;
-#pragma unroll
-                for (int r = 0; r < 4; r++) {
-                    const float a0l = __shfl(acc0[r], src), a0h = __shfl(acc0[r + 4], src);
-                    const float a1l = __shfl(acc1[r], src), a1h = __shfl(acc1[r + 4], src);
-                    qa0[r] = up ? (h2 ? a1h : a1l) : (h2 ? a0h : a0l);
-                    const float b0l = __shfl(acc0[r + 8], src), b0h = __shfl(acc0[r + 12], src);
-                    const float b1l = __shfl(acc1[r + 8], src), b1h = __shfl(acc1[r + 12], src);
-                    qa1[r] = up ? (h2 ? b1h : b1l) : (h2 ? b0h : b0l);
-                }
-            }
-            }
-            bool dones = !slot_ok;
-            const float qfx = (float)(sx0 + p % kStripW), qfy = (float)(sy0 + p / kStripW);
-            const int qrec_w = lane < 32 ? lane : 24 + lane;  // LDS word of this lane's record dword
-            const int rq = (lane >> 3) & 3;                   // record loads: lanes 8 rq .. 8 rq + 7
-            // next four survivors of the strip (index P past the list's end: zero record, zero feature)
-#define GSR_QFETCH(S)                                                                               \
-            {                                                                                       \
-                uint32_t g0_ = (uint32_t)d.P, g1_ = (uint32_t)d.P, g2_ = (uint32_t)d.P, g3_ = (uint32_t)d.P; \
-                int p0_ = 0, p1_ = 0, p2_ = 0, p3_ = 0;                                             \
-                if (__builtin_expect(__builtin_popcountll(mask) >= 4, 1)) {                         \
-                    /* common case: four survivors of the chunk in hand */                          \
-                    const int i0_ = (int)__builtin_ctzll(mask); mask &= mask - 1;                   \
-                    const int i1_ = (int)__builtin_ctzll(mask); mask &= mask - 1;                   \
-                    const int i2_ = (int)__builtin_ctzll(mask); mask &= mask - 1;                   \
-                    const int i3_ = (int)__builtin_ctzll(mask); mask &= mask - 1;                   \
-                    g0_ = __builtin_amdgcn_readlane(cidx, i0_) & kIndexMask; p0_ = base + i0_ + 1;  \
-                    g1_ = __builtin_amdgcn_readlane(cidx, i1_) & kIndexMask; p1_ = base + i1_ + 1;  \
-                    g2_ = __builtin_amdgcn_readlane(cidx, i2_) & kIndexMask; p2_ = base + i2_ + 1;  \
-                    g3_ = __builtin_amdgcn_readlane(cidx, i3_) & kIndexMask; p3_ = base + i3_ + 1;  \
-                    S##v = true;                                                                    \
-                } else {                                                                            \
-                    S##v = GSR_NEXT(g0_, p0_);                                                      \
-                    if (S##v && !GSR_NEXT(g1_, p1_)) g1_ = (uint32_t)d.P;                           \
-                    if (S##v && g1_ != (uint32_t)d.P && !GSR_NEXT(g2_, p2_)) g2_ = (uint32_t)d.P;   \
-                    if (S##v && g2_ != (uint32_t)d.P && !GSR_NEXT(g3_, p3_)) g3_ = (uint32_t)d.P;   \
-                    if (!S##v) g0_ = (uint32_t)d.P;                                                 \
-                }                                                                                   \
-                S##p0 = p0_; S##p1 = p1_; S##p2 = p2_; S##p3 = p3_;                                 \
-                const uint32_t gr_ = rq == 0 ? g0_ : rq == 1 ? g1_ : rq == 2 ? g2_ : g3_;           \
-                S##r = __builtin_amdgcn_raw_buffer_load_b32(                                        \
-                    rrs, lane < 32 ? (int)(gr_ * 32u + (uint32_t)(lane & 7) * 4u) : (int)kOOB, 0, 0); \
-                const uint32_t gf_ = q == 0 ? g0_ : q == 1 ? g1_ : q == 2 ? g2_ : g3_;              \
-                const int fo_ = (int)(gf_ * (uint32_t)(GSR_C * 4) + (uint32_t)j * 4u);              \
-                S##f0 = __builtin_amdgcn_raw_buffer_load_b32(qfs, fo_, 0, 0);                       \
-                S##f1 = __builtin_amdgcn_raw_buffer_load_b32(qfs, fo_ + 64, 0, 0);                  \
-            }
-#define GSR_QSTEP(S)                                                                                \
-            {                                                                                       \
-                rec_lds[qrec_w] = S##r;                                                             \
-                __builtin_amdgcn_wave_barrier();                                                    \
-                const float4 ra_ = __builtin_bit_cast(float4, *(const uint4x*)&rec_lds[8 * q]);     \
-                const float4 rc_ = __builtin_bit_cast(float4, *(const uint4x*)&rec_lds[8 * q + 4]); \
-                __builtin_amdgcn_wave_barrier();                                                    \
-                const float al_ = alpha_of<EXACT>(ra_, rc_, qfx, qfy);                              \
-                /* the four Gaussians' alphas and inverse depths at this slot, to every lane */     \
-                const auto a16_ = __builtin_amdgcn_permlane16_swap(__float_as_uint(al_), __float_as_uint(al_), \
-                                                                    false, false);                  \
-                const auto a02_ = __builtin_amdgcn_permlane32_swap(a16_[0], a16_[0], false, false); \
-                const auto a13_ = __builtin_amdgcn_permlane32_swap(a16_[1], a16_[1], false, false); \
-                const auto i16_ = __builtin_amdgcn_permlane16_swap(__float_as_uint(ra_.w),          \
-                                                                    __float_as_uint(ra_.w), false, false); \
-                const auto i02_ = __builtin_amdgcn_permlane32_swap(i16_[0], i16_[0], false, false); \
-                const auto i13_ = __builtin_amdgcn_permlane32_swap(i16_[1], i16_[1], false, false); \
-                const bool was_ = dones;                                                            \
-                const float w0_ = take_step(__uint_as_float(a02_[0]), __uint_as_float(i02_[0]),     \
-                                            (uint32_t)S##p0, Ts, invds, lasts, dones);              \
-                if (STATS && !was_ && dones) stops = (uint32_t)S##p0;                               \
-                const bool was1_ = dones;                                                           \
-                const float w1_ = take_step(__uint_as_float(a13_[0]), __uint_as_float(i13_[0]),     \
-                                            (uint32_t)S##p1, Ts, invds, lasts, dones);              \
-                if (STATS && !was1_ && dones) stops = (uint32_t)S##p1;                              \
-                const bool was2_ = dones;                                                           \
-                const float w2_ = take_step(__uint_as_float(a02_[1]), __uint_as_float(i02_[1]),     \
-                                            (uint32_t)S##p2, Ts, invds, lasts, dones);              \
-                if (STATS && !was2_ && dones) stops = (uint32_t)S##p2;                              \
-                const bool was3_ = dones;                                                           \
-                const float w3_ = take_step(__uint_as_float(a13_[1]), __uint_as_float(i13_[1]),     \
-                                            (uint32_t)S##p3, Ts, invds, lasts, dones);              \
-                if (STATS && !was3_ && dones) stops = (uint32_t)S##p3;                              \
-                const float wq_ = q == 0 ? w0_ : q == 1 ? w1_ : q == 2 ? w2_ : w3_;                 \
-                qa0 = __builtin_amdgcn_mfma_f32_16x16x4f32(__uint_as_float(S##f0), wq_, qa0, 0, 0, 0); \
-                qa1 = __builtin_amdgcn_mfma_f32_16x16x4f32(__uint_as_float(S##f1), wq_, qa1, 0, 0, 0); \
-                if (STATS) {                                                                        \
-                    n_contrib_pairs += __popcll(__ballot(wq_ > 0.f));                               \
-                    n_qsurv += 1 + (S##p1 > 0) + (S##p2 > 0) + (S##p3 > 0);                         \
-                }                                                                                   \
-                if (TL) n_steps += 1;  /* (STATS: quad steps in cn[8] as survivors, not k-steps) */ \
-            }
-            // three slots in rotation: a step's survivors are requested two steps before their blend
-            bool Xv = false, Yv = false, Zv = false;
-            int Xp0, Xp1, Xp2, Xp3, Yp0, Yp1, Yp2, Yp3, Zp0, Zp1, Zp2, Zp3;
-            unsigned Xr, Xf0, Xf1, Yr, Yf0, Yf1, Zr, Zf0, Zf1;
-            if (nlive > 0) {
-                GSR_QFETCH(X)
-                GSR_QFETCH(Y)
-                for (;;) {
-                    if (!Xv) break;
-                    GSR_QFETCH(Z)
-                    GSR_QSTEP(X)
-                    if (!Yv || !__any(!dones)) break;
-                    GSR_QFETCH(X)
-                    GSR_QSTEP(Y)
-                    if (!Zv || !__any(!dones)) break;
-                    GSR_QFETCH(Y)
-                    GSR_QSTEP(Z)
-                    if (!__any(!dones)) break;
-                }
-            }
-#undef GSR_QFETCH
-#undef GSR_QSTEP
-            // the slots' outputs: group 0 stores final_T / n_contrib / inverse depth, every lane its
-            // four channels of each half (pixels in the image by construction: they were live)
-            {
-                const int64_t HW = (int64_t)d.H * d.W;
-                const int64_t pix = b * HW + (int64_t)(sy0 + p / kStripW) * d.W + (sx0 + p % kStripW);
-                if (slot_ok && q == 0) {
-                    im.final_T[pix] = Ts;
-                    im.n_contrib[pix] = lasts;
-                    if (o.out_invdepth) o.out_invdepth[pix] = invds;
-                }
-                const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
-                    o.out_color + (int64_t)b * GSR_C * HW, 0, (int)((int64_t)GSR_C * HW * 4), 0x00020000);
-                const float* bgp = in.bg + in.s_bg * b;
-                const int vo = slot_ok ? (int)((pix - b * HW) * 4) : 0x7FFFFFF0;
-#pragma unroll
-                for (int r = 0; r < 4; r++) {
-                    const int c0 = 4 * q + r, c1 = 16 + 4 * q + r;
-                    __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(fmaf(Ts, bgp[c0], qa0[r])), rs, vo,
-                                                          c0 * (int)HW * 4, 0);
-                    __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(fmaf(Ts, bgp[c1], qa1[r])), rs, vo,
-                                                          c1 * (int)HW * 4, 0);
-                }
-                if (STATS && slot_ok && q == 0) ev_quad = dones ? stops : (uint32_t)n;
-            }
-        }
-
 #undef GSR_NEXT
 #undef GSR_FETCH
 #undef GSR_ALPHA
@@ -1139,10 +649,7 @@ __device__ __forceinline__ void render_fwd_body(const Dims& d, const Inputs& in,
         // ---- epilogue ----
         if (STATS) {
             unsigned long long* cn = (unsigned long long*)o.stats;
-            // pixels handed to the quad tail count there (ev_quad, one lane per slot)
-            uint64_t ev = (px < d.W && py < d.H && !(((quad_live | half_live) >> lane) & 1u))
-                              ? (done ? stop : (uint32_t)n) : 0;
-            ev += ev_quad + ev_half;
+            uint64_t ev = (px < d.W && py < d.H) ? (done ? stop : (uint32_t)n) : 0;
             for (int off = 32; off > 0; off >>= 1) ev += __shfl_xor(ev, off);
             if (lane == 0) {
                 atomicAdd(&cn[0], (unsigned long long)ev);
@@ -1151,8 +658,6 @@ __device__ __forceinline__ void render_fwd_body(const Dims& d, const Inputs& in,
                 atomicAdd(&cn[3], (unsigned long long)n_steps);
                 atomicAdd(&cn[4], (unsigned long long)n_staged);
                 atomicAdd(&cn[7], (unsigned long long)n_dead);
-                atomicAdd(&cn[8], (unsigned long long)n_qsurv);
-                atomicAdd(&cn[9], (unsigned long long)n_hsurv);
                 if (strip == 0) {
                     atomicAdd(&cn[5], (unsigned long long)n);
                     atomicAdd(&cn[6], 1ull);
@@ -1169,8 +674,7 @@ __device__ __forceinline__ void render_fwd_body(const Dims& d, const Inputs& in,
         }
         if constexpr (HALF) store_half(d, im, o, in.bg + in.s_bg * b, b, sx0, sy0 + half * (32 / kStripW), lane,
                                        acc0, T, invd, last);
-        else if (QUAD && (QONLY || to_quad || to_half)) {  /* stored by the half / quad tails */
-        } else if (ABL == 9) {  /* timing ablation: only final_T of the strip is stored */
+        else if (ABL == 9) {  /* timing ablation: only final_T of the strip is stored */
             if (px < d.W && py < d.H) im.final_T[b * (int64_t)d.H * d.W + (int64_t)py * d.W + px] = T + acc0[0] + acc1[0];
         }
         else store_strip<false, REFINE>(d, im, o, in.bg + in.s_bg * b, b, sx0, sy0, lane, acc0, acc1, T,
@@ -1179,34 +683,32 @@ __device__ __forceinline__ void render_fwd_body(const Dims& d, const Inputs& in,
 }
 
 // Register budget: 5 waves per SIMD (96 registers; the few values spilled live outside the blend
-// loop) for the 3-slot and half-strip kernels, launched 5 workgroups per CU: the blend loop is
-// VALU-issue-bound with latency that 4 waves did not cover.  The full-strip 5-slot latency kernel
-// keeps a 3-wave budget (it is launched 3 per CU).
+// loop) for the 3-slot kernel, launched 5 workgroups per CU at 16+ frames: the blend loop is
+// VALU-issue-bound with latency that 4 waves did not cover.  The half-strip (one frame) kernel
+// keeps a 3-wave budget (launched 3 per CU).
 #ifndef GSR_RENDER_WPE
 #define GSR_RENDER_WPE 5
 #endif
 #ifndef GSR_HALF_WPE
-#define GSR_HALF_WPE 3  // half-strip waves (one frame): launched GSR_RENDER_HALF_WG = 3 per CU
+#define GSR_HALF_WPE 3
 #endif
-#ifndef GSR_QONLY_WPE
-#define GSR_QONLY_WPE 6  // quad-only waves (one frame): no 32-register strip accumulators
-#endif
-template <bool EXACT, bool STATS, bool TL, int SPLIT = 0, int NSLOT = GSR_BATCH_NSLOT, bool HALF = false,
-          bool QUAD = false, bool QONLY = false, bool HTAIL = false>
+template <bool EXACT, bool STATS, bool TL, int SPLIT = 0, int NSLOT = GSR_BATCH_NSLOT, bool HALF = false>
 __global__ __launch_bounds__(GSR_TILE_PIX)
-__attribute__((amdgpu_waves_per_eu(QONLY ? GSR_QONLY_WPE : HALF ? GSR_HALF_WPE : (NSLOT == 5 && GSR_BATCH_NSLOT != 5) ? 3 : GSR_RENDER_WPE))) void k_render_fwd(
+__attribute__((amdgpu_waves_per_eu(HALF ? GSR_HALF_WPE : GSR_RENDER_WPE))) void k_render_fwd(
     Dims d, Inputs in, GeomArena g, ImageArena im, BinArena bn, Outputs o) {
-    render_fwd_body<EXACT, STATS, TL, false, 0, SPLIT, NSLOT, HALF, QUAD, QONLY, HTAIL>(d, in, g, im, bn, o);
+    render_fwd_body<EXACT, STATS, TL, false, 0, SPLIT, NSLOT, HALF>(d, in, g, im, bn, o);
 }
 
+#ifdef GSR_TUNING
 // Timing ablations of the production kernel (GSR_RENDER_ABLATE=1: VALU stand-in for the MFMAs,
-// 4: bf16 32x32x16 MFMAs on dummy operands in place of the f32 ones,
-// 2: no feature loads, 8: no empty-tile stores, 9: no strip colour stores).  Wrong images by construction; for attributing render_fwd time only.
+// 2: no feature loads, 8: no empty-tile stores, 9: no strip colour stores).  Wrong images by
+// construction; for attributing render_fwd time only, and only in tools/build_ab.py builds.
 template <int ABL>
-__global__ __launch_bounds__(GSR_TILE_PIX) void k_render_fwd_ablate(Dims d, Inputs in, GeomArena g,
-                                                                    ImageArena im, BinArena bn, Outputs o) {
+__global__ __launch_bounds__(GSR_TILE_PIX) __attribute__((amdgpu_waves_per_eu(GSR_RENDER_WPE)))
+void k_render_fwd_ablate(Dims d, Inputs in, GeomArena g, ImageArena im, BinArena bn, Outputs o) {
     render_fwd_body<true, false, false, false, ABL>(d, in, g, im, bn, o);
 }
+#endif
 
 // The refiner-head variant: the epilogue's extra stores would raise the register count past the
 // 4-waves-per-SIMD budget of the blend loop; pin the budget (the few extra live values of the
@@ -1221,68 +723,43 @@ void launch_render_fwd(const Dims& d, const Inputs& in_, const GeomArena& g, con
                        const BinArena& b, const Outputs& o, bool exact, bool split, hipStream_t s) {
     Inputs in = in_;  // one frame: strip_list is one longest-first list (launch_strip_order)
     if (d.B == 1 && in.xcd_map == 2u) in.xcd_map = 1u;
-    static const int ablate = [] { const char* e = getenv("GSR_RENDER_ABLATE"); return e ? atoi(e) : 0; }();
     const int nwaves = d.B * d.T * kStrips;  // upper bound of the work items
     if (nwaves == 0) return;
     // workgroups per CU: at most the resident capacity (GSR_RENDER_WPE waves/SIMD at the kernel's
     // register budget), so no render workgroup waits in the dispatcher ahead of another stream's
     // kernels.  Large batches take all 5 (-3% at 32 frames); small ones 4 (5 was +4% at the
     // 6-frame training batch, where fewer strips per wave leave a longer tail).
-    static const int wg_env = [] { const char* e = getenv("GSR_RENDER_WG_PER_CU"); return e ? atoi(e) : 0; }();
+    static const int wg_env = tune_env("GSR_RENDER_WG_PER_CU", 0);
     const int wg_per_cu = wg_env > 0 ? wg_env : (d.B >= 16 ? GSR_RENDER_WPE : 4);
-    // GSR_RENDER_LATENCY=0: single-frame launches use the throughput kernel (A/B)
-    static const bool latency_mode = [] { const char* e = getenv("GSR_RENDER_LATENCY"); return !(e && e[0] == '0'); }();
-    // GSR_RENDER_HALF=0: single-frame launches use full-strip waves (A/B); GSR_RENDER_HALF_WG: WGs per CU
-    static const bool half_mode = [] { const char* e = getenv("GSR_RENDER_HALF"); return !(e && e[0] == '0'); }();
-    static const int half_wg = [] { const char* e = getenv("GSR_RENDER_HALF_WG"); return e ? atoi(e) : GSR_HALF_WPE; }();
-    // GSR_RENDER_QONLY=1: single-frame launches use quad-only waves instead of the half-strip waves
-    // (measured the same, 0.271 ms per C2 frame either way: off by default); GSR_RENDER_QONLY_WG: WGs per CU
-    static const bool qonly_mode = [] { const char* e = getenv("GSR_RENDER_QONLY"); return e && e[0] == '1'; }();
-    static const int qonly_wg = [] { const char* e = getenv("GSR_RENDER_QONLY_WG"); return e ? atoi(e) : GSR_QONLY_WPE; }();
-    // GSR_QUAD_TAIL=1: the f32 (non-split) throughput kernel hands a strip's last <= 16 (and, with the
-    // half tail, <= 32) live pixels to the compacted tails.  Measured slower (C2 batch
-    // 1.343 -> 1.39 ms quad only, 1.90 ms with the half tail; the tails' register pressure spills per
-    // strip), so off by default
-    static const bool quad = [] { const char* e = getenv("GSR_QUAD_TAIL"); return e && e[0] == '1'; }();
-    // GSR_HALF_TAIL=0: no half tail before the quad tail (A/B)
-    static const bool htail = [] { const char* e = getenv("GSR_HALF_TAIL"); return !(e && e[0] == '0'); }();
-    const bool qt = quad && !split;
-    const bool ht = qt && htail;
+    // GSR_RENDER_HALF=0: single-frame launches on the throughput kernel (A/B); GSR_RENDER_HALF_WG: WGs per CU
+    static const bool half_mode = tune_env("GSR_RENDER_HALF", 1) != 0;
+    static const int half_wg = tune_env("GSR_RENDER_HALF_WG", GSR_HALF_WPE);
     const int grid = min((nwaves + 3) / 4, persistent_grid(wg_per_cu));
     const dim3 gr(grid), bl(GSR_TILE_PIX);
-#if GSR_BATCH_NSLOT == 3  /* (the tails follow the three-slot pipeline) */
-#define GSR_LAUNCH(E, S, L)                                                                                   \
-    {                                                                                                         \
-        if (ht) hipLaunchKernelGGL((k_render_fwd<E, S, L, 0, 3, false, true, false, true>), gr, bl, 0, s, d, in, g, im, b, o); \
-        else if (qt) hipLaunchKernelGGL((k_render_fwd<E, S, L, 0, 3, false, true>), gr, bl, 0, s, d, in, g, im, b, o); \
-        else hipLaunchKernelGGL((k_render_fwd<E, S, L>), gr, bl, 0, s, d, in, g, im, b, o);                  \
+#ifdef GSR_TUNING
+    static const int ablate = tune_env("GSR_RENDER_ABLATE", 0);
+    if (!o.stats && !o.timeline && !o.out_refine && ablate) {
+        if (ablate == 1) hipLaunchKernelGGL((k_render_fwd_ablate<1>), gr, bl, 0, s, d, in, g, im, b, o);
+        else if (ablate == 2) hipLaunchKernelGGL((k_render_fwd_ablate<2>), gr, bl, 0, s, d, in, g, im, b, o);
+        else if (ablate == 8) hipLaunchKernelGGL((k_render_fwd_ablate<8>), gr, bl, 0, s, d, in, g, im, b, o);
+        else if (ablate == 9) hipLaunchKernelGGL((k_render_fwd_ablate<9>), gr, bl, 0, s, d, in, g, im, b, o);
+        return;
     }
-#else
-#define GSR_LAUNCH(E, S, L) { (void)ht; (void)qt; hipLaunchKernelGGL((k_render_fwd<E, S, L>), gr, bl, 0, s, d, in, g, im, b, o); }
 #endif
-    if (o.stats) {
-        if (exact) GSR_LAUNCH(true, true, false) else GSR_LAUNCH(false, true, false)
+#define GSR_LAUNCH(SPL, ...)                                                                            \
+    {                                                                                                   \
+        if (exact) hipLaunchKernelGGL((k_render_fwd<true, __VA_ARGS__>), gr, bl, 0, s, d, in, g, im, b, o);   \
+        else hipLaunchKernelGGL((k_render_fwd<false, __VA_ARGS__>), gr, bl, 0, s, d, in, g, im, b, o);        \
     }
-    else if (o.timeline) { if (exact) GSR_LAUNCH(true, false, true) else GSR_LAUNCH(false, false, true) }
-    else if (o.out_refine) {  // (4-wave register budget: 4 workgroups per CU)
+    if (o.stats) {
+        GSR_LAUNCH(0, true, false)
+    } else if (o.timeline) {
+        GSR_LAUNCH(0, false, true)
+    } else if (o.out_refine) {  // (4-wave register budget: 4 workgroups per CU)
         const dim3 grf(min((nwaves + 3) / 4, persistent_grid(4)));
         if (exact) hipLaunchKernelGGL((k_render_fwd_refine<true>), grf, bl, 0, s, d, in, g, im, b, o);
         else hipLaunchKernelGGL((k_render_fwd_refine<false>), grf, bl, 0, s, d, in, g, im, b, o);
-    }
-    else if (ablate == 1) hipLaunchKernelGGL((k_render_fwd_ablate<1>), gr, bl, 0, s, d, in, g, im, b, o);
-    else if (ablate == 2) hipLaunchKernelGGL((k_render_fwd_ablate<2>), gr, bl, 0, s, d, in, g, im, b, o);
-    else if (ablate == 4) hipLaunchKernelGGL((k_render_fwd_ablate<4>), gr, bl, 0, s, d, in, g, im, b, o);
-    else if (ablate == 8) hipLaunchKernelGGL((k_render_fwd_ablate<8>), gr, bl, 0, s, d, in, g, im, b, o);
-    else if (ablate == 9) hipLaunchKernelGGL((k_render_fwd_ablate<9>), gr, bl, 0, s, d, in, g, im, b, o);
-    else if (d.B == 1 && latency_mode && qonly_mode && !split) {
-        // one frame, quad waves: every strip is four 4x4-pixel work items, each wave taking four
-        // survivors per step (lane = pixel + 16 Gaussian) -- a quarter of the longest strip's serial
-        // chain per work item
-        const dim3 gq(min((4 * nwaves + 3) / 4, persistent_grid(qonly_wg)));
-        if (exact) hipLaunchKernelGGL((k_render_fwd<true, false, false, 0, 3, false, true, true>), gq, bl, 0, s, d, in, g, im, b, o);
-        else hipLaunchKernelGGL((k_render_fwd<false, false, false, 0, 3, false, true, true>), gq, bl, 0, s, d, in, g, im, b, o);
-    }
-    else if (d.B == 1 && latency_mode && half_mode) {
+    } else if (d.B == 1 && half_mode) {
         // one frame, half-strip waves: a strip's two halves run in parallel, each lane one
         // (pixel, Gaussian) alpha per k-step -- the longest strip's time is what counts here
         const dim3 gl(min((2 * nwaves + 3) / 4, persistent_grid(half_wg)));
@@ -1293,29 +770,16 @@ void launch_render_fwd(const Dims& d, const Inputs& in_, const GeomArena& g, con
             if (exact) hipLaunchKernelGGL((k_render_fwd<true, false, false, 0, 5, true>), gl, bl, 0, s, d, in, g, im, b, o);
             else hipLaunchKernelGGL((k_render_fwd<false, false, false, 0, 5, true>), gl, bl, 0, s, d, in, g, im, b, o);
         }
-    }
-    else if (d.B == 1 && latency_mode) {  // one frame: the longest strip's wave sets the time
-        const dim3 gl(min((nwaves + 3) / 4, persistent_grid(3)));  // 3 waves per SIMD at 5 slots
-        if (split) {
-            if (exact) hipLaunchKernelGGL((k_render_fwd<true, false, false, 1, 5>), gl, bl, 0, s, d, in, g, im, b, o);
-            else hipLaunchKernelGGL((k_render_fwd<false, false, false, 1, 5>), gl, bl, 0, s, d, in, g, im, b, o);
-        } else {
-            if (exact) hipLaunchKernelGGL((k_render_fwd<true, false, false, 0, 5>), gl, bl, 0, s, d, in, g, im, b, o);
-            else hipLaunchKernelGGL((k_render_fwd<false, false, false, 0, 5>), gl, bl, 0, s, d, in, g, im, b, o);
-        }
-    }
-    else if (split && in.s_colors == 0) {  // one feature set for the batch: split it once
+    } else if (split && in.s_colors == 0) {  // one feature set for the batch: split it once
         hipLaunchKernelGGL(k_split_features, dim3((d.P * GSR_C / 4 + 255) / 256), dim3(256), 0, s,
                            d.P * GSR_C / 4, reinterpret_cast<const float4*>(in.colors),
                            reinterpret_cast<uint4*>(g.fsplit));
-        if (exact) hipLaunchKernelGGL((k_render_fwd<true, false, false, 2>), gr, bl, 0, s, d, in, g, im, b, o);
-        else hipLaunchKernelGGL((k_render_fwd<false, false, false, 2>), gr, bl, 0, s, d, in, g, im, b, o);
+        GSR_LAUNCH(0, false, false, 2)
+    } else if (split) {
+        GSR_LAUNCH(0, false, false, 1)
+    } else {
+        GSR_LAUNCH(0, false, false)
     }
-    else if (split) {
-        if (exact) hipLaunchKernelGGL((k_render_fwd<true, false, false, 1>), gr, bl, 0, s, d, in, g, im, b, o);
-        else hipLaunchKernelGGL((k_render_fwd<false, false, false, 1>), gr, bl, 0, s, d, in, g, im, b, o);
-    }
-    else { if (exact) GSR_LAUNCH(true, false, false) else GSR_LAUNCH(false, false, false) }
 #undef GSR_LAUNCH
 }
 

@@ -321,9 +321,13 @@ class EHMDeformer:
         for name, a in (("body", self.body), ("flame", self.flame)):
             if name in self.sparse:
                 sp, keep = self.sparse[name]
-                tl = [tile_base(x) if x.numel() else None for x in (a["shapedirs_t"], _f32(a["posedirs"]))]
+                bases = (a["shapedirs_t"], _f32(a["posedirs"]))
+                tl = [tile_base(x) if x.numel() else None for x in bases]
                 keep += tl
                 sp.shapedirs_tiled, sp.posedirs_tiled = (x.data_ptr() if x is not None else None for x in tl)
+                # the K x M each base was tiled for (the library refuses calls of another shape)
+                (sp.shapedirs_tiled_k, sp.shapedirs_tiled_m), (sp.posedirs_tiled_k, sp.posedirs_tiled_m) = (
+                    tuple(x.shape) if x.numel() else (0, 0) for x in bases)
         self.head_index = t(np.asarray(smplx2flame_ind, np.int32))
         self.l_eyelid, self.r_eyelid = t(np.asarray(l_eyelid, np.float32)), t(np.asarray(r_eyelid, np.float32))
         self.bad = torch.zeros(1, dtype=torch.int32, device=dev)

@@ -9,6 +9,7 @@ tensors resized through the C ABI's allocator callbacks, exactly as resizeFuncti
 Differences by design: scratch buffers live on means3D's device (the reference uses the current
 device); kernels run on the current HIP stream of that device.
 """
+import collections
 import ctypes
 import os
 import weakref
@@ -283,8 +284,17 @@ class _Scratch:
         return s
 
 
-_SCRATCH = {}
+_SCRATCH = collections.OrderedDict()  # (device, stream handle) -> _Scratch, least recently used first
+_SCRATCH_MAX = 8
 _SCRATCH_FNS = None
+
+
+def clear_scratch():
+    """Release the inference scratch arenas kept per (device, stream) (they are re-created on the
+    next call).  At most _SCRATCH_MAX streams keep arenas; the least recently used is dropped first.
+    A stream handle that the runtime reuses after its stream was destroyed inherits that stream's
+    arenas, which is safe: they are scratch, used in stream order."""
+    _SCRATCH.clear()
 
 
 def rasterize_inference(background, means3D, colors, opacity, scales, rotations, scale_modifier, cov3D_precomp,
@@ -301,6 +311,10 @@ def rasterize_inference(background, means3D, colors, opacity, scales, rotations,
     P, H, W = int(means3D.size(0)), int(image_height), int(image_width)
     dev = means3D.device
     if P == 0 or dev.type != "cuda" or colors is None or colors.numel() == 0:
+        return None
+    if means3D.get_device() != torch.cuda.current_device():
+        # the library sizes its persistent grids and raises LDS limits on the current device: the
+        # general path enters the inputs' device first (no device switch on this hot path)
         return None
     L = _lib.load()
     bound = L.gsr_forward_async_bound(P, W, H)
@@ -326,6 +340,10 @@ def rasterize_inference(background, means3D, colors, opacity, scales, rotations,
     sc = _SCRATCH.get(key)
     if sc is None:
         sc = _SCRATCH[key] = _Scratch(dev)
+        while len(_SCRATCH) > _SCRATCH_MAX:
+            _SCRATCH.popitem(last=False)
+    else:
+        _SCRATCH.move_to_end(key)
     s = sc.fit(L, P, W, H, bound)
     if _SCRATCH_FNS is None:
         addr = lambda f: ctypes.cast(f, ctypes.c_void_p).value  # noqa: E731

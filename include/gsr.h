@@ -72,8 +72,9 @@ const char* gsr_last_error(void);
  * render_motion.py).  Preprocess then writes only what binning and compositing read (depth, render
  * record, tile rect and count; plus the caller's radii) and skips the rows kept for the backward
  * (cov3D, means2D, conic, inverse depth, radii in the workspace): 56 of 108 bytes per visible
- * Gaussian.  Images are unchanged.  A gsr_backward_batch* on such a workspace computes nothing and
- * its gradients stay as the caller zeroed them (the Python mirror raises first). */
+ * Gaussian.  Images are unchanged.  A gsr_backward_batch* on a workspace whose last forward was
+ * forward-only fails with GSR_ERR_ARG (the library records it per workspace pointer on the host;
+ * the kernels also skip such a workspace, so nothing is computed either way). */
 #define GSR_FORWARD_ONLY 0x100u
 
 /* Scratch sizes used by gsr_forward (the three resizer requests).  Unlike the reference's
@@ -264,9 +265,7 @@ int gsr_profile_read(double* ms, int* counts, int n);
  * position, or the whole list), [1] pairs that contributed (alpha >= 1/255, before termination),
  * [2] (wave strip, Gaussian) pairs blended after the per-wave cull, [3] MFMA k-steps issued per
  * wave, [4] Gaussians staged (list entries loaded into LDS), [5] list entries of all tiles,
- * [6] tiles rendered, [7] k-steps in which no pixel of the wave took either Gaussian, [8] survivors
- * blended in the quad tail (16 pixel slots, 4 Gaussians per step; [2] counts the 64-pixel strip
- * layout's), [9] survivors blended in the half tail (32 slots, 2 Gaussians per step).  NULL
+ * [6] tiles rendered, [7] k-steps in which no pixel of the wave took either Gaussian.  NULL
  * restores the production kernel. */
 int gsr_render_counters(uint64_t* device_counters);
 /* Work-item timeline of the render kernel (a lightly instrumented variant runs while set):

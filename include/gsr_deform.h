@@ -73,11 +73,15 @@ int gsr_lbs(int B, int V, int J, int NB, const float* v_template, int64_t v_temp
  *   skin_k in [1, 16] (0: the dense lbs_weights_t), skin_joint / skin_weight [skin_k, V]: per vertex
  *   its nonzero (joint, weight) pairs in increasing joint order, padded with weight 0 -- the dense
  *   skinning's fmaf chains minus their zero terms, so the vertices and transforms are identical.
+ *   skin_joint values must be in [0, J) (the kernel clamps them to J-1, so a bad value gives a wrong
+ *   vertex, never an out-of-range read).
  *   shapedirs_tiled / posedirs_tiled (or NULL): the blend-shape bases shapedirs_t [NB][3V] and
  *   posedirs [9(J-1)][3V] re-laid as 1-KB tiles of 32 coordinates x 8 k for 16-byte loads:
  *   float4 (t * ceil(K/8) + g) * 64 + 32 h + c, component j = base[8g + 4h + j][32t + c], zero-padded
  *   to K multiple of 8 and 3V multiple of 32 (gsr_lbs_tile_bases).  Used for B = 1 and B > 16; the
- *   k sums are re-associated (fixed order, deterministic). */
+ *   k sums are re-associated (fixed order, deterministic).  *_tiled_k / *_tiled_m: the K and M the
+ *   base was tiled for; a call whose NB (shape) or 9(J-1) (pose) and 3V differ is refused
+ *   (GSR_ERR_ARG), since the tile indexing depends on both. */
 typedef struct {
     const int32_t* jreg_row;
     const int32_t* jreg_col;
@@ -88,6 +92,8 @@ typedef struct {
     const float* skin_weight;
     const float* shapedirs_tiled;
     const float* posedirs_tiled;
+    int32_t shapedirs_tiled_k, shapedirs_tiled_m;
+    int32_t posedirs_tiled_k, posedirs_tiled_m;
 } GsrLbsSparse;
 /* Floats of a tiled base (GsrLbsSparse.*_tiled) for K x M, and the re-layout of a k-major base
  * [K][M] (device pointers) into it. */

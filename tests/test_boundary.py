@@ -211,3 +211,17 @@ def test_ctypes_structs_match_the_c_layout(tmp_path):
         assert got[(cname, "size")] == ctypes.sizeof(py), cname
         for f, _ in py._fields_:
             assert got[(cname, f)] == getattr(py, f).offset, (cname, f)
+
+
+def test_product_library_has_no_tuning_switches():
+    """The timing ablations (wrong images by construction) and the tuning switches are compiled only
+    into tools/build_ab.py's A/B builds (-DGSR_TUNING): the product libgsr.so holds neither the
+    ablation kernels nor the environment-variable names, so a stray GSR_*_ABLATE or tuning variable in
+    a deployment cannot change a render."""
+    from guava_renderer_amd import build as gb
+    blob = open(gb.LIB, "rb").read()
+    assert b"k_render_fwd" in blob  # (the device code object is searchable: the check below means something)
+    for name in (b"k_render_fwd_ablate", b"GSR_RENDER_ABLATE", b"GSR_BWD_ABLATE", b"GSR_SCATTER_ABLATE",
+                 b"GSR_RENDER_WG_PER_CU", b"GSR_RENDER_HALF", b"GSR_BUCKET_DIV", b"GSR_CHUNK_PASSES",
+                 b"GSR_XCD_MAP", b"GSR_BLEND_TILED", b"GSR_BWD_SPLIT"):
+        assert name not in blob, name

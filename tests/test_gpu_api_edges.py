@@ -248,6 +248,13 @@ def test_forward_only_batch_same_images_and_backward_refused():
         assert torch.equal(a, b)
     with pytest.raises(GsrError):
         r.backward(*args, torch.zeros((B, 32, H, W), device=DEV))
+    # the C ABI refuses it too (a caller that drives the library directly, not through the mirror)
+    r._fwd_only = False
+    with pytest.raises(GsrError, match="FORWARD_ONLY"):
+        r.backward(*args, torch.zeros((B, 32, H, W), device=DEV))
+    r.forward(*args)  # a full forward makes the workspace differentiable again
+    r.backward(*args, torch.zeros((B, 32, H, W), device=DEV))
+    torch.cuda.synchronize()
 
 
 def test_inference_path_equals_general_forward():

@@ -1,7 +1,9 @@
 """Build an A/B variant of libgsr.so into guava_renderer_amd/lib/ab/libgsr_<tag>.so:
     python tools/build_ab.py <tag> [src.hip=path/to/replacement.hip ...] [-DFLAG ...]
-Every source not replaced is the tree's object (run `python -m guava_renderer_amd.build` first);
-replaced sources (or all sources given -D flags) are compiled with the tree's flags."""
+Every source is compiled with the tree's flags plus -DGSR_TUNING (the tuning switches and timing
+ablations read from the environment: gsr_internal.h tune_env) and the given -D flags; a replaced
+source comes from the given path.  The product library (guava_renderer_amd/build.py) never sets
+GSR_TUNING."""
 import os
 import subprocess
 import sys
@@ -11,7 +13,7 @@ from guava_renderer_amd import build as b  # noqa: E402
 
 tag = sys.argv[1]
 repl = dict(a.split("=", 1) for a in sys.argv[2:] if "=" in a and not a.startswith("-D"))
-defs = [a for a in sys.argv[2:] if a.startswith("-D")]
+defs = ["-DGSR_TUNING"] + [a for a in sys.argv[2:] if a.startswith("-D")]
 out_dir = os.path.join(os.path.dirname(b.LIB), "ab")
 os.makedirs(out_dir, exist_ok=True)
 want = b.source_hash()

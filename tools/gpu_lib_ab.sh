@@ -2,7 +2,8 @@
 # Same-box timing A/B of library builds (tools/build_ab.py <tag> ... -> guava_renderer_amd/lib/ab/
 # libgsr_<tag>.so) and environment switches on one bench pipeline, R rounds, interleaved:
 #   tools/gpu_lib_ab.sh base fill4 n5w4 'env:GSR_RENDER_ABLATE=8' ...
-# "base" is the tree's library; "env:VAR=VAL[,VAR=VAL]" runs the tree's library with those variables.
+# "base" is the tree's library; "env:VAR=VAL[,VAR=VAL]" runs the GSR_TUNING build tagged "tune"
+# (python tools/build_ab.py tune) with those variables: the product library ignores them.
 # PIPE (default avatar), BATCH (32), STEPS (100), R (2), TESTS (pytest files run first, optional).
 # Prints frames/s, ms/step and render_fwd's isolated-pass launch time per variant.
 set -u
@@ -20,7 +21,8 @@ for r in $(seq 1 ${R:-2}); do
     (
       case "$V" in
         base) ;;
-        env:*) for kv in $(echo "${V#env:}" | tr ',' ' '); do export "$kv"; done ;;
+        env:*) export GSR_LIB=guava_renderer_amd/lib/ab/libgsr_tune.so
+               for kv in $(echo "${V#env:}" | tr ',' ' '); do export "$kv"; done ;;
         *) export GSR_LIB=guava_renderer_amd/lib/ab/libgsr_$V.so ;;
       esac
       tag=$(echo "$V" | tr -c 'A-Za-z0-9_\n' '_')
