@@ -37,6 +37,12 @@ namespace gsr {
 #ifndef GSR_LDS_EARLY
 #define GSR_LDS_EARLY 1  // record LDS reads of the next slot issued before this slot's blend
 #endif
+#ifndef GSR_PAD_SALU
+#define GSR_PAD_SALU 0  // instrumentation: extra SALU per k-step (A/B builds)
+#endif
+#ifndef GSR_PAD_VALU
+#define GSR_PAD_VALU 0  // instrumentation: extra VALU per k-step (A/B builds)
+#endif
 #ifndef GSR_BATCH_NSLOT
 #define GSR_BATCH_NSLOT 3  // pipeline slots of the batched (throughput) kernels
 #endif
@@ -501,7 +507,7 @@ __device__ __forceinline__ void render_fwd_body(const Dims& d, const Inputs& in,
         // stage 2: the pixel-local alphas of slot S (a missing survivor has alpha 0): the records
         // through the wave's LDS slot (GSR_ALPHA_LDS), then the alpha arithmetic (GSR_ALPHA_MATH)
 #define GSR_ALPHA_LDS(S)                                                                            \
-        if (!HALF) {  /* uniform-address b128 reads (lanes 8..63 wrote spare words) */              \
+        if (!HALF) {  /* uniform-address b128 reads (lanes 8..63 wrote spare words) */       \
             rec_lds[rec_widx] = S##r; rec_lds[rec_widx + 8] = S##r2;                                \
             __builtin_amdgcn_wave_barrier();                                                        \
             S##a0 = __builtin_bit_cast(float4, *(const uint4x*)&rec_lds[0]);                        \
@@ -525,9 +531,23 @@ __device__ __forceinline__ void render_fwd_body(const Dims& d, const Inputs& in,
         // GSR_LDS_EARLY: slot S+1's record reads are issued before slot S's serial blend, so the LDS
         // latency runs under the blend (the alpha arithmetic of S+1 still follows it)
 #if GSR_LDS_EARLY
-#define GSR_STEP(N, S) GSR_ALPHA_LDS(N) __builtin_amdgcn_sched_barrier(0); GSR_TAKE(S) GSR_ALPHA_MATH(N)
+#define GSR_STEP(N, S) GSR_ALPHA_LDS(N) __builtin_amdgcn_sched_barrier(0); GSR_TAKE(S) GSR_ALPHA_MATH(N) GSR_PAD()
 #else
-#define GSR_STEP(N, S) GSR_ALPHA(N) GSR_TAKE(S)
+#define GSR_STEP(N, S) GSR_ALPHA(N) GSR_TAKE(S) GSR_PAD()
+#endif
+#if GSR_PAD_SALU || GSR_PAD_VALU
+        // issue-sensitivity instrumentation (A/B builds only): extra SALU / VALU per k-step
+        uint32_t pad_s = __builtin_amdgcn_readfirstlane((uint32_t)n);
+        float pad_v = pfx;
+#define GSR_PAD()                                                                                   \
+        {                                                                                           \
+            _Pragma("unroll") for (int i_ = 0; i_ < GSR_PAD_SALU; i_++)                             \
+                asm volatile("s_add_u32 %0, %0, 1" : "+s"(pad_s) :: "scc");                         \
+            _Pragma("unroll") for (int i_ = 0; i_ < GSR_PAD_VALU; i_++)                             \
+                asm volatile("v_add_f32 %0, 1.0, %0" : "+v"(pad_v));                                \
+        }
+#else
+#define GSR_PAD()
 #endif
         // stage 3: the serial blend of slot S and its accumulation on the matrix cores
 #define GSR_TAKE(S)                                                                                 \
@@ -645,6 +665,7 @@ __device__ __forceinline__ void render_fwd_body(const Dims& d, const Inputs& in,
 #undef GSR_STEP
 #undef GSR_TAKE
 #undef GSR_SLOT
+#undef GSR_PAD
 
         // ---- epilogue ----
         if (STATS) {

@@ -76,8 +76,17 @@ static inline void blend_parts(float x, float* q, int* k) {
     *q = fmaf(p, r * r, r);
     *k = (kf == kf) ? (int)kf : 0; /* v_cvt_i32_f32 gives 0 for NaN; |kf| <= 126 otherwise */
 }
+/* Blend arithmetic modes (the `exact_exp` argument of the render functions):
+ *   1 GSRO_RESTATED  -- the restatement the GPU reproduces bit for bit: fused power, blend_parts exp,
+ *                       C = fmaf(f, alpha T, C);
+ *   0 GSRO_LIBM_EXP  -- the same arithmetic with libm expf (the reference's exp, forward.cu:360);
+ *   2 GSRO_LITERAL   -- the reference's expressions as written, every product and sum rounded
+ *                       (C semantics; nvcc may contract some into fma, which this container cannot
+ *                       reproduce): power = -0.5f * (a dx dx + c dy dy) - b dx dy (forward.cu:352,
+ *                       backward.cu:564), alpha = min(0.99f, o expf(power)) (:360), C += f alpha T
+ *                       (:372), invdepth += (1 / depth) alpha T (:375), out = C + T bg (:391). */
 float gsro_blend_alpha(float o, float x, int exact) {
-    if (!exact) return fminf(0.99f, o * expf(x));
+    if (exact != 1) return fminf(0.99f, o * expf(x));
     if (x < -87.0f) return 0.0f;
     float q;
     int k;
@@ -87,7 +96,7 @@ float gsro_blend_alpha(float o, float x, int exact) {
 }
 /* exp(x) = 2^k (1 + q) for the backward's dL/dopacity and dL/dG terms */
 float gsro_blend_G(float x, int exact) {
-    if (!exact) return expf(x);
+    if (exact != 1) return expf(x);
     if (x < -87.0f) x = -87.0f; /* never used there (alpha is 0); keeps k in range */
     float q;
     int k;
@@ -374,6 +383,15 @@ int64_t gsro_bin(int P, int W, int H, const int* radii, const float* means2D, co
     return R;
 }
 
+/* The blend's Gaussian exponent at d = (dx, dy) = xy - pixel: mode 2 as written at forward.cu:352
+ * (left to right, each product rounded); else the fused form of gsr_math.h blend_power (an algebraic
+ * rewrite with A = -a/2, B = -b, C = -c/2, exact scalings). */
+static inline float blend_power_m(const float* co, float dx, float dy, int mode) {
+    if (mode == 2) return -0.5f * (co[0] * dx * dx + co[2] * dy * dy) - co[1] * dx * dy;
+    const float A = -0.5f * co[0], Bb = -co[1], Cq = -0.5f * co[2];
+    return fmaf(dy, fmaf(Cq, dy, Bb * dx), (A * dx) * dx);
+}
+
 void gsro_render(int W, int H, const uint32_t* ranges, const uint32_t* point_list,
                  const float* means2D, const float* colors, const float* conic_opacity,
                  const float* depths, const float* bg, int exact_exp,
@@ -402,23 +420,28 @@ void gsro_render(int W, int H, const uint32_t* ranges, const uint32_t* point_lis
                     const float* co = conic_opacity + 4 * (size_t)g;
                     const float dx = means2D[2 * (size_t)g] - pfx;
                     const float dy = means2D[2 * (size_t)g + 1] - pfy;
-                    const float A = -0.5f * co[0], Bb = -co[1], Cq = -0.5f * co[2];
-                    const float power = fmaf(dy, fmaf(Cq, dy, Bb * dx), (A * dx) * dx);
+                    const float power = blend_power_m(co, dx, dy, exact_exp);
                     if (power > 0.0f) continue;
                     const float alpha = gsro_blend_alpha(co[3], power, exact_exp);
                     if (alpha < 1.0f / 255.0f) continue;
                     const float test_T = Tr * (1.0f - alpha);
                     if (test_T < 0.0001f) break; /* done: the reference stops iterating */
-                    const float w = alpha * Tr;
                     const float* f = colors + (size_t)g * C;
-                    for (int ch = 0; ch < C; ch++) Cc[ch] = fmaf(f[ch], w, Cc[ch]);
-                    invd = fmaf(1.0f / depths[g], w, invd);
+                    if (exact_exp == 2) {
+                        for (int ch = 0; ch < C; ch++) Cc[ch] += f[ch] * alpha * Tr;
+                        invd += (1.0f / depths[g]) * alpha * Tr;
+                    } else {
+                        const float w = alpha * Tr;
+                        for (int ch = 0; ch < C; ch++) Cc[ch] = fmaf(f[ch], w, Cc[ch]);
+                        invd = fmaf(1.0f / depths[g], w, invd);
+                    }
                     Tr = test_T;
                     last = contributor;
                 }
                 final_T[pix] = Tr;
                 n_contrib[pix] = last;
-                for (int ch = 0; ch < C; ch++) out_color[(size_t)ch * HW + pix] = fmaf(Tr, bg[ch], Cc[ch]);
+                for (int ch = 0; ch < C; ch++)
+                    out_color[(size_t)ch * HW + pix] = exact_exp == 2 ? Cc[ch] + Tr * bg[ch] : fmaf(Tr, bg[ch], Cc[ch]);
                 if (out_invdepth) out_invdepth[pix] = invd;
             }
     }
@@ -446,8 +469,7 @@ void gsro_render_counts(int W, int H, const uint32_t* ranges, const uint32_t* po
                     const float* co = conic_opacity + 4 * (size_t)g;
                     const float dx = means2D[2 * (size_t)g] - (float)x;
                     const float dy = means2D[2 * (size_t)g + 1] - (float)y;
-                    const float A = -0.5f * co[0], Bb = -co[1], Cq = -0.5f * co[2];
-                    const float power = fmaf(dy, fmaf(Cq, dy, Bb * dx), (A * dx) * dx);
+                    const float power = blend_power_m(co, dx, dy, exact_exp);
                     if (power > 0.0f) continue;
                     const float alpha = gsro_blend_alpha(co[3], power, exact_exp);
                     if (alpha < 1.0f / 255.0f) continue;
@@ -471,6 +493,13 @@ void gsro_render_counts(int W, int H, const uint32_t* ranges, const uint32_t* po
  * Returns the number of flagged pixels. */
 uint64_t gsro_render_decision_flips(int W, int H, const uint32_t* ranges, const uint32_t* point_list,
                                     const float* means2D, const float* conic_opacity, uint8_t* flags) {
+    return gsro_render_decision_flips_modes(W, H, ranges, point_list, means2D, conic_opacity, 1, 0, flags);
+}
+
+/* The same between any two blend modes (mode_a, mode_b: 0 / 1 / 2 as gsro_render). */
+uint64_t gsro_render_decision_flips_modes(int W, int H, const uint32_t* ranges, const uint32_t* point_list,
+                                          const float* means2D, const float* conic_opacity, int mode_a,
+                                          int mode_b, uint8_t* flags) {
     const int gx = (W + BX - 1) / BX, gy = (H + BY - 1) / BY;
     uint64_t nflip = 0;
 #pragma omp parallel for schedule(dynamic, 1) num_threads(gsro_get_threads()) reduction(+ : nflip)
@@ -488,11 +517,9 @@ uint64_t gsro_render_decision_flips(int W, int H, const uint32_t* ranges, const 
                     const float* co = conic_opacity + 4 * (size_t)g;
                     const float dx = means2D[2 * (size_t)g] - (float)x;
                     const float dy = means2D[2 * (size_t)g + 1] - (float)y;
-                    const float A = -0.5f * co[0], Bb = -co[1], Cq = -0.5f * co[2];
-                    const float power = fmaf(dy, fmaf(Cq, dy, Bb * dx), (A * dx) * dx);
-                    if (power > 0.0f) continue;
-                    const float a0 = gsro_blend_alpha(co[3], power, 1);
-                    const float a1 = gsro_blend_alpha(co[3], power, 0);
+                    const float p0 = blend_power_m(co, dx, dy, mode_a), p1 = blend_power_m(co, dx, dy, mode_b);
+                    const float a0 = p0 > 0.0f ? 0.0f : gsro_blend_alpha(co[3], p0, mode_a);
+                    const float a1 = p1 > 0.0f ? 0.0f : gsro_blend_alpha(co[3], p1, mode_b);
                     const int take0 = !(a0 < 1.0f / 255.0f), take1 = !(a1 < 1.0f / 255.0f);
                     if (take0 != take1) { flip = 1; break; }
                     if (!take0) continue;
@@ -510,6 +537,14 @@ uint64_t gsro_render_decision_flips(int W, int H, const uint32_t* ranges, const 
     return nflip;
 }
 
+/* Accumulation order of gsro_render_backward's per-Gaussian sums (test infrastructure): 0 = tiles,
+ * then pixels, in increasing order; 1 = both reversed.  The reference accumulates with float atomics
+ * in whatever order its threads arrive (backward.cu:593-635), so the difference between the two orders
+ * is the f32 noise floor that any reassociating implementation (the GPU's included) is judged
+ * against per element (tests/helpers.py grad_check). */
+static int g_bwd_reverse = 0;
+void gsro_set_backward_order(int reverse) { g_bwd_reverse = reverse; }
+
 void gsro_render_backward(int W, int H, const uint32_t* ranges, const uint32_t* point_list,
                           const float* bg, const float* means2D, const float* conic_opacity,
                           const float* colors, const float* depths, const float* final_T,
@@ -523,11 +558,13 @@ void gsro_render_backward(int W, int H, const uint32_t* ranges, const uint32_t* 
     const float ddelx_dx = (float)(0.5 * W);
     const float ddely_dy = (float)(0.5 * H);
     const int use_invd = (dL_dinvdepth_pix != NULL && dL_dinvdepth_g != NULL);
-    for (int tile = 0; tile < T; tile++) {
+    for (int tile_i = 0; tile_i < T; tile_i++) {
+        const int tile = g_bwd_reverse ? T - 1 - tile_i : tile_i;
         const int tx = tile % gx, ty = tile / gx;
         const uint32_t start = ranges[2 * tile], end = ranges[2 * tile + 1];
-        for (int ly = 0; ly < BY; ly++)
-            for (int lx = 0; lx < BX; lx++) {
+        for (int pi = 0; pi < BX * BY; pi++) {
+                const int pp = g_bwd_reverse ? BX * BY - 1 - pi : pi;
+                const int lx = pp % BX, ly = pp / BX;
                 const int x = tx * BX + lx, y = ty * BY + ly;
                 if (x >= W || y >= H) continue;
                 const size_t pix = (size_t)W * (size_t)y + (size_t)x;
@@ -554,8 +591,7 @@ void gsro_render_backward(int W, int H, const uint32_t* ranges, const uint32_t* 
                     const float* co = conic_opacity + 4 * (size_t)g;
                     const float dx = means2D[2 * (size_t)g] - pfx;
                     const float dy = means2D[2 * (size_t)g + 1] - pfy;
-                    const float A = -0.5f * co[0], Bb = -co[1], Cq = -0.5f * co[2];
-                    const float power = fmaf(dy, fmaf(Cq, dy, Bb * dx), (A * dx) * dx);
+                    const float power = blend_power_m(co, dx, dy, exact_exp);
                     if (power > 0.0f) continue;
                     const float G = gsro_blend_G(power, exact_exp);
                     const float alpha = gsro_blend_alpha(co[3], power, exact_exp);

@@ -70,7 +70,9 @@ int64_t gsro_bin(int P, int W, int H, const int* radii, const float* means2D, co
                  const uint32_t* tiles_touched, uint32_t* point_offsets,
                  uint32_t* point_list, uint64_t* point_keys, uint32_t* ranges, int64_t R_cap);
 
-/* renderCUDA fwd (forward.cu:274-397).  exact_exp selects the bit-reproducible blend exp (1, gsro_blend_alpha) or libm expf (0).
+/* renderCUDA fwd (forward.cu:274-397).  exact_exp selects the blend arithmetic: 1 the bit-reproducible
+ * restatement (gsro_blend_alpha), 0 the same with libm expf, 2 the reference's expressions as written
+ * with libm expf (gsr_oracle.c, "Blend arithmetic modes").
  * out_color[C*H*W], out_invdepth[H*W] (may be NULL), final_T[H*W], n_contrib[H*W]. */
 void gsro_render(int W, int H, const uint32_t* ranges, const uint32_t* point_list,
                  const float* means2D, const float* colors, const float* conic_opacity,
@@ -83,9 +85,15 @@ void gsro_render(int W, int H, const uint32_t* ranges, const uint32_t* point_lis
 void gsro_render_counts(int W, int H, const uint32_t* ranges, const uint32_t* point_list,
                         const float* means2D, const float* conic_opacity, int exact_exp,
                         uint64_t* out);
-/* Pixels whose take/stop decisions differ between exact_exp = 1 and libm expf (test only). */
+/* Pixels whose take/stop decisions differ between two blend modes (test only): exact_exp = 1 and
+ * libm expf, or any two of the modes 0 / 1 / 2 (gsr_oracle.c: GSRO_RESTATED, _LIBM_EXP, _LITERAL). */
+uint64_t gsro_render_decision_flips_modes(int W, int H, const uint32_t* ranges, const uint32_t* point_list,
+                                          const float* means2D, const float* conic_opacity, int mode_a,
+                                          int mode_b, uint8_t* flags);
 uint64_t gsro_render_decision_flips(int W, int H, const uint32_t* ranges, const uint32_t* point_list,
                                     const float* means2D, const float* conic_opacity, uint8_t* flags);
+/* Accumulation order of gsro_render_backward (test only): 0 forward, 1 tiles and pixels reversed. */
+void gsro_set_backward_order(int reverse);
 void gsro_render_backward(int W, int H, const uint32_t* ranges, const uint32_t* point_list,
                           const float* bg, const float* means2D, const float* conic_opacity,
                           const float* colors, const float* depths, const float* final_T,

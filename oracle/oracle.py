@@ -58,6 +58,10 @@ def lib():
                                          _u64]
         L.gsro_render_decision_flips.restype = ctypes.c_uint64
         L.gsro_render_decision_flips.argtypes = [ctypes.c_int, ctypes.c_int, _u32, _u32, _f, _f, _u8]
+        L.gsro_set_backward_order.argtypes = [ctypes.c_int]
+        L.gsro_render_decision_flips_modes.restype = ctypes.c_uint64
+        L.gsro_render_decision_flips_modes.argtypes = [ctypes.c_int, ctypes.c_int, _u32, _u32, _f, _f,
+                                                       ctypes.c_int, ctypes.c_int, _u8]
         L.gsro_render_backward.argtypes = [ctypes.c_int, ctypes.c_int, _u32, _u32, _f, _f, _f, _f,
                                            _f, _f, _u32, _f, _f, ctypes.c_int, _f, _f, _f, _f, _f]
         L.gsro_preprocess_backward.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, _f, _i, _f,
@@ -158,6 +162,18 @@ def bin_and_sort(st, W, H):
     return st
 
 
+LITERAL = "literal"
+
+
+def _mode(exact_exp):
+    """Blend arithmetic mode of the C oracle (gsr_oracle.c, "Blend arithmetic modes"): True -> 1 (the
+    restatement the GPU reproduces bit for bit), False -> 0 (the same with libm expf), "literal" -> 2
+    (the reference's expressions as written, forward.cu:352-391 / backward.cu:564-568, libm expf)."""
+    if exact_exp == LITERAL:
+        return 2
+    return int(bool(exact_exp))
+
+
 def render(st, colors, bg, W, H, exact_exp=True):
     colors = _f32(colors)
     HW = W * H
@@ -168,7 +184,7 @@ def render(st, colors, bg, W, H, exact_exp=True):
     pl = st["point_list"] if st["R"] > 0 else np.zeros(1, np.uint32)
     lib().gsro_render(int(W), int(H), _p(st["ranges"], _u32), _p(pl, _u32),
                       _p(st["means2D"], _f), _p(colors, _f), _p(st["conic_opacity"], _f),
-                      _p(st["depths"], _f), _p(_f32(bg), _f), int(bool(exact_exp)),
+                      _p(st["depths"], _f), _p(_f32(bg), _f), _mode(exact_exp),
                       _p(out, _f), _p(invd, _f), _p(fT, _f), _p(nc, _u32))
     st.update(final_T=fT, n_contrib=nc)
     return out, invd
@@ -179,18 +195,20 @@ def render_counts(st, W, H, exact_exp=True):
     out = np.zeros(2, np.uint64)
     pl = st["point_list"] if st["R"] > 0 else np.zeros(1, np.uint32)
     lib().gsro_render_counts(int(W), int(H), _p(st["ranges"], _u32), _p(pl, _u32),
-                             _p(st["means2D"], _f), _p(st["conic_opacity"], _f), int(bool(exact_exp)),
+                             _p(st["means2D"], _f), _p(st["conic_opacity"], _f), _mode(exact_exp),
                              _p(out, _u64))
     return int(out[0]), int(out[1])
 
 
-def decision_flips(st, W, H):
-    """Pixels whose blend takes or stops differently with the restatement's exp and with libm expf
-    (gsro_render_decision_flips): bool [H, W]."""
+def decision_flips(st, W, H, against=False):
+    """Pixels whose blend takes or stops differently with the restatement's arithmetic (the GPU's)
+    and with `against` (False: the same arithmetic with libm expf; "literal": the reference's
+    expressions as written, gsro_render_decision_flips_modes): bool [H, W]."""
     flags = np.zeros(W * H, np.uint8)
     pl = st["point_list"] if st["R"] > 0 else np.zeros(1, np.uint32)
-    lib().gsro_render_decision_flips(int(W), int(H), _p(st["ranges"], _u32), _p(pl, _u32),
-                                     _p(st["means2D"], _f), _p(st["conic_opacity"], _f), _p(flags, _u8))
+    lib().gsro_render_decision_flips_modes(int(W), int(H), _p(st["ranges"], _u32), _p(pl, _u32),
+                                           _p(st["means2D"], _f), _p(st["conic_opacity"], _f), 1,
+                                           _mode(against), _p(flags, _u8))
     return flags.reshape(H, W).astype(bool)
 
 
@@ -206,8 +224,10 @@ def forward(means3D, colors, opacities, scales, rotations, cov3D_precomp, view, 
 
 def backward(st, means3D, colors, opacities, scales, rotations, cov3D_precomp, view, proj, W, H,
              tanx, tany, bg, dL_dcolor, dL_dinvdepth=None, scale_modifier=1.0, antialiasing=False,
-             exact_exp=True):
-    """Full backward (rasterizer_impl.cu:345-450). Returns the 8 grads in _C order:
+             exact_exp=True, reverse_order=False):
+    """Full backward (rasterizer_impl.cu:345-450).  reverse_order: the per-Gaussian sums accumulated
+    over tiles and pixels in reverse (gsro_set_backward_order; the f32 reassociation noise floor).
+    Returns the 8 grads in _C order:
     (dL_dmeans2D[P,3], dL_dcolors[P,C], dL_dopacity[P,1], dL_dmeans3D[P,3], dL_dcov3D[P,6],
      dL_dsh[P,0,3], dL_dscales[P,3], dL_drotations[P,4])."""
     means3D = _f32(means3D)
@@ -218,12 +238,14 @@ def backward(st, means3D, colors, opacities, scales, rotations, cov3D_precomp, v
     g_col = np.zeros((P, C), np.float32)
     g_invd = np.zeros(P, np.float32) if dL_dinvdepth is not None else None
     pl = st["point_list"] if st["R"] > 0 else np.zeros(1, np.uint32)
+    lib().gsro_set_backward_order(int(bool(reverse_order)))
     lib().gsro_render_backward(
         int(W), int(H), _p(st["ranges"], _u32), _p(pl, _u32), _p(_f32(bg), _f),
         _p(st["means2D"], _f), _p(st["conic_opacity"], _f), _p(_f32(colors), _f),
         _p(st["depths"], _f), _p(st["final_T"], _f), _p(st["n_contrib"], _u32),
-        _p(_f32(dL_dcolor), _f), _p(_f32(dL_dinvdepth), _f), int(bool(exact_exp)),
+        _p(_f32(dL_dcolor), _f), _p(_f32(dL_dinvdepth), _f), _mode(exact_exp),
         _p(g_m2, _f), _p(g_con, _f), _p(g_op, _f), _p(g_col, _f), _p(g_invd, _f))
+    lib().gsro_set_backward_order(0)
     g_m3 = np.zeros((P, 3), np.float32)
     g_cov = np.zeros((P, 6), np.float32)
     g_sc = np.zeros((P, 3), np.float32)

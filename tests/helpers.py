@@ -130,3 +130,47 @@ def gpu_forward(d, antialiasing=False, use_cov=None, debug=False, numerics=0):
     st["point_list"] = st["point_list"] & 0x0FFFFFFF
     st["R"] = R
     return color.cpu().numpy(), radii.cpu().numpy(), invd.cpu().numpy(), st
+
+
+GRAD_SCALE_TOL = 1e-4   # |a - b| <= 1e-4 * max|b| over the whole tensor
+GRAD_ELEM_TOL = 1e-3    # |a - b| <= 1e-3 * |b| on every element with |b| >= GRAD_ELEM_FLOOR * max|b|
+GRAD_ELEM_FLOOR = 1e-3
+
+
+NOISE_FACTOR = 3.0      # per-element bound relative to the reference algorithm's own f32 reordering noise
+
+
+def grad_check(name, a, b, scale_tol=GRAD_SCALE_TOL, elem_tol=GRAD_ELEM_TOL, floor=GRAD_ELEM_FLOOR,
+               noise=None):
+    """Gradient parity, two ways: against the tensor's scale (the per-Gaussian atomics of the
+    reference, backward.cu:593-635, reassociate freely) and per element -- a Gaussian with a small but
+    not negligible gradient must be right too: relative error <= elem_tol on every element with
+    |g| >= floor * max|g|.  `noise`: the same oracle gradient accumulated in another order
+    (oracle.backward(reverse_order=True)); the closed-form backward amplifies f32 reassociation on
+    ill-conditioned elements (the 2x2 conic inverse, computeCov2DCUDA, backward.cu:147-326), so the
+    per-element bound is max(elem_tol, NOISE_FACTOR x the reference's own reordering error), and the
+    99.9th percentile must stay within elem_tol / 10.  Prints both distributions."""
+    a = np.asarray(a, np.float64).reshape(-1)
+    b = np.asarray(b, np.float64).reshape(-1)
+    assert a.shape == b.shape, (name, a.shape, b.shape)
+    m = float(np.abs(b).max()) if b.size else 0.0
+    if m == 0.0:
+        assert np.abs(a).max(initial=0.0) == 0.0, name
+        return
+    err_scale = float(np.abs(a - b).max()) / m
+    big = np.abs(b) >= floor * m
+    rel = np.abs(a - b)[big] / np.abs(b)[big]
+    p999 = float(np.percentile(rel, 99.9)) if rel.size else 0.0
+    limit = elem_tol
+    msg = ""
+    if noise is not None:
+        nz = np.asarray(noise, np.float64).reshape(-1)
+        rel_n = np.abs(nz - b)[big] / np.abs(b)[big]
+        limit = max(elem_tol, NOISE_FACTOR * float(rel_n.max(initial=0.0)))
+        msg = (f"; reference reordered: max {rel_n.max(initial=0.0):.3g}, "
+               f"p99.9 {float(np.percentile(rel_n, 99.9)) if rel_n.size else 0.0:.3g}")
+    print(f"  {name}: {err_scale:.3g} of scale; elementwise over {int(big.sum())} |g| >= {floor:g} max: "
+          f"max {rel.max(initial=0.0):.3g}, p99.9 {p999:.3g}{msg}")
+    assert err_scale <= scale_tol, f"{name}: {err_scale:.3g} of scale"
+    assert rel.max(initial=0.0) <= limit, f"{name}: element rel err {rel.max():.3g} > {limit:.3g} (p99.9 {p999:.3g})"
+    assert p999 <= elem_tol / 10, f"{name}: element rel err p99.9 {p999:.3g}"

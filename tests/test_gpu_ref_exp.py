@@ -22,7 +22,7 @@ import numpy as np
 import pytest
 import torch
 
-from helpers import gpu_forward, oracle_forward
+from helpers import gpu_forward, grad_check, oracle_forward
 
 pytestmark = pytest.mark.gpu
 DEV = torch.device("cuda:0")
@@ -31,7 +31,11 @@ TOL = 1e-4        # north_star: 1e-4 L_inf; DESIGN.md §3: gradients within 1e-4
 
 
 @pytest.mark.parametrize("P,W,gpt", [(100000, 512, 1), (300000, 1024, 3)])
-def test_forward_default_vs_libm_expf(P, W, gpt):
+@pytest.mark.parametrize("against", [False, "literal"])
+def test_forward_default_vs_reference_arithmetic(P, W, gpt, against):
+    """against=False: the oracle with libm expf in place of the restatement's exp (every other
+    expression the restatement's); "literal": the reference's expressions as written
+    (forward.cu:352 power, libm expf, C += f alpha T, (1/depth) alpha T, C + T bg)."""
     import oracle
     from guava_renderer_amd import scenes
     oracle.set_threads(16)
@@ -39,17 +43,17 @@ def test_forward_default_vs_libm_expf(P, W, gpt):
     cam = scenes.frame_cameras(2, W, W, seed=1000)[1]
     d = dict(sc, **cam, bg=np.zeros(32, np.float32))
     g_col, g_radii, g_inv, gs = gpu_forward(d)  # library default numerics: exact poly exp, f32 MFMA
-    o_col, o_radii, o_inv, os_ = oracle_forward(d, exact=False)
+    o_col, o_radii, o_inv, os_ = oracle_forward(d, exact=against)
     np.testing.assert_array_equal(g_radii, o_radii)
     T = os_["ranges"].shape[0]
     np.testing.assert_array_equal(gs["ranges"].reshape(T, 2), os_["ranges"])
     np.testing.assert_array_equal(gs["point_list"][:gs["R"]], os_["point_list"])
     nc_mism = float((gs["n_contrib"] != os_["n_contrib"]).mean())
-    flips = oracle.decision_flips(os_, W, W)
+    flips = oracle.decision_flips(os_, W, W, against=against)
     keep = ~flips
     err = np.abs(g_col - o_col)
     worst_flip = float(err[:, flips].max()) if flips.any() else 0.0
-    print(f"P={P} {W}x{W}: n_contrib mismatch {nc_mism:.2e}, decision-flip pixels {int(flips.sum())} "
+    print(f"P={P} {W}x{W} vs {'literal reference arithmetic' if against else 'libm expf'}: n_contrib mismatch {nc_mism:.2e}, decision-flip pixels {int(flips.sum())} "
           f"({flips.mean():.2e}), L_inf on the other pixels {err[:, keep].max():.3g} "
           f"(RGB {err[:3][:, keep].max():.3g}), worst flipped pixel {worst_flip:.3g}")
     assert nc_mism <= FLIP_RATE, nc_mism
@@ -61,7 +65,8 @@ def test_forward_default_vs_libm_expf(P, W, gpt):
     assert dinv[keep].max() <= 1e-6 * max(1.0, float(np.abs(o_inv).max())), dinv[keep].max()
 
 
-def test_backward_batch6_vs_libm_expf():
+@pytest.mark.parametrize("against", [False, "literal"])
+def test_backward_batch6_vs_reference_arithmetic(against):
     from guava_renderer_amd import scenes
     import oracle
     from guava_renderer_amd.batch import BatchRasterizer
@@ -92,14 +97,14 @@ def test_backward_batch6_vs_libm_expf():
         cam = cams[f]
         _, _, _, st = oracle.forward(sc["means3D"], sc["colors"], sc["opacities"], sc["scales"], sc["rotations"],
                                      None, cam["viewmatrix"], cam["projmatrix"], W, W, cam["tanfovx"],
-                                     cam["tanfovy"], bg, exact_exp=False)
-        o = oracle.backward(st, sc["means3D"], sc["colors"], sc["opacities"], sc["scales"], sc["rotations"],
-                            None, cam["viewmatrix"], cam["projmatrix"], W, W, cam["tanfovx"], cam["tanfovy"],
-                            bg, dL[f], dLinv[f][None], exact_exp=False)
-        print(f"frame {f}: decision-flip pixels {int(oracle.decision_flips(st, W, W).sum())}")
-        for name, b in zip(names, o):
+                                     cam["tanfovy"], bg, exact_exp=against)
+        bargs = (st, sc["means3D"], sc["colors"], sc["opacities"], sc["scales"], sc["rotations"], None,
+                 cam["viewmatrix"], cam["projmatrix"], W, W, cam["tanfovx"], cam["tanfovy"], bg, dL[f],
+                 dLinv[f][None])
+        o = oracle.backward(*bargs, exact_exp=against)
+        o_rev = oracle.backward(*bargs, exact_exp=against, reverse_order=True)
+        print(f"frame {f} vs {'literal' if against else 'libm expf'}: decision-flip pixels "
+              f"{int(oracle.decision_flips(st, W, W, against=against).sum())}")
+        for name, b, bn in zip(names, o, o_rev):
             if name in mine_keys and b.size:
-                a = gpu[mine_keys[name]][f].reshape(b.shape)
-                err = float(np.abs(a - b).max() / max(np.abs(b).max(), 1e-20))
-                print(f"  {name}: {err:.3g}")
-                assert err <= TOL, f"frame {f} {name}: {err:.3g}"
+                grad_check(f"frame {f} {name}", gpu[mine_keys[name]][f].reshape(b.shape), b, noise=bn)

@@ -294,3 +294,59 @@ def test_exact_exp_vs_libm_expf_decisions():
     assert err.max() <= 1e-4, err.max()
     # a pixel where the exps agree on every decision differs only by the alphas' rounding
     assert err.max() <= 1e-5, err.max()
+
+
+@pytest.mark.parametrize("kind,P,W", [("random", 10000, 256), ("avatar", 20000, 256)])
+def test_restated_vs_literal_reference_arithmetic(kind, P, W):
+    """The restatement's arithmetic (fused power, polynomial exp, fmaf colour update -- bit-exact with
+    the GPU) against the reference's expressions as written (oracle mode "literal": forward.cu:352
+    power, libm expf for CUDA's expf, C += f alpha T, invdepth += (1/depth) alpha T, C + T bg) at
+    config-1 size: decision flips <= 0.1% of the pixels, every other pixel within 1e-5 on all 32
+    channels (north_star: 1e-4), final_T within 1e-6; radii and lists do not involve the blend."""
+    from helpers import make_scene, oracle_forward
+    d = make_scene(kind, P, W, W, seed=2)
+    c1, r1, i1, s1 = oracle_forward(d, exact=True)
+    c2, r2, i2, s2 = oracle_forward(d, exact=oracle.LITERAL)
+    np.testing.assert_array_equal(r1, r2)
+    np.testing.assert_array_equal(s1["point_list"], s2["point_list"])
+    flips = oracle.decision_flips(s1, W, W, against=oracle.LITERAL)
+    assert flips.mean() <= 1e-3, flips.mean()
+    assert (s1["n_contrib"] != s2["n_contrib"]).mean() <= 1e-3
+    keep = ~flips.reshape(-1)
+    err = np.abs(c1 - c2).reshape(32, -1)[:, keep]
+    assert err.max() <= 1e-5, err.max()
+    assert np.abs(s1["final_T"] - s2["final_T"])[keep].max() <= 1e-6
+    assert np.abs(i1 - i2).reshape(-1)[keep].max() <= 1e-5 * max(1.0, float(np.abs(i2).max()))
+
+
+def test_literal_mode_is_the_reference_expression():
+    """Mode "literal" evaluates forward.cu:352-391 as written: one Gaussian, one pixel, checked
+    against the same expressions evaluated step by step in numpy float32 (every op rounded)."""
+    from helpers import make_scene, oracle_forward
+    d = make_scene("random", 1, 16, 16, seed=3)
+    col, radii, invd, st = oracle_forward(d, exact=oracle.LITERAL)
+    if radii[0] == 0:
+        pytest.skip("the random Gaussian was culled")
+    f32 = np.float32
+    xy = st["means2D"].reshape(-1, 2)[0].astype(f32)
+    co = st["conic_opacity"].reshape(-1, 4)[0].astype(f32)
+    depth = f32(st["depths"][0])
+    checked = 0
+    for y in range(16):
+        for x in range(16):
+            dx, dy = f32(xy[0] - f32(x)), f32(xy[1] - f32(y))
+            s = f32(f32(f32(co[0] * dx) * dx) + f32(f32(co[2] * dy) * dy))
+            power = f32(f32(f32(-0.5) * s) - f32(f32(co[1] * dx) * dy))
+            if power > 0:
+                continue
+            alpha = min(f32(0.99), f32(co[3] * f32(np.exp(np.float64(power)))))  # (libm-rounded expf stand-in)
+            if alpha < f32(1.0) / f32(255.0):
+                continue
+            c0 = f32(f32(d["colors"][0, 0] * alpha) * f32(1.0))
+            want = f32(c0 + f32(f32(1.0 - alpha) * f32(d["bg"][0])))
+            got = col[0, y, x]
+            assert abs(float(got) - float(want)) <= 2e-7 * max(1.0, abs(float(want))), (x, y, got, want)
+            wi = f32(f32(f32(f32(1.0) / depth) * alpha) * f32(1.0))
+            assert abs(float(invd[0, y, x]) - float(wi)) <= 2e-7 * max(1.0, abs(float(wi)))
+            checked += 1
+    assert checked > 0
