@@ -21,6 +21,7 @@
 //                          stable rank = tile base + chunk base + earlier slots covering the tile
 //                          (popcount of row/column ballots), plus the exact 4-bit strip mask
 // Traffic per instance: 4 B point_list + 1 B strip mask written once; per Gaussian a few words.
+#include "gsr_cull.h"
 #include "gsr_internal.h"
 
 namespace gsr {
@@ -785,42 +786,7 @@ void launch_tile_scan(const Dims& d, const GeomArena& g, const ImageArena& im, h
 }
 
 // ---------------------------------------------------------------- strip masks
-// Minimum over the pixel-centre rectangle dx in [dxl, dxh], dy in [dyl, dyh] (dx = mean - pixel)
-// of the conic's quadratic form Q = a dx^2 + 2b dx dy + c dy^2 (power = -Q/2 in the blend).  Q is
-// convex (a, c > 0, ac > b^2), so the minimum is 0 if the mean lies inside, else it lies on an edge:
-// each edge is a 1-D quadratic minimised by clamping its vertex.
-// Only the edges FACING the mean can hold that minimum: from a point of any other edge the segment
-// towards the mean enters the rectangle and Q falls along it (convexity).  So at most one vertical
-// edge (the column nearest the mean, when the mean is left or right of the rectangle) and one
-// horizontal edge are evaluated -- half of the four-edge form's work, the same minimum.
-__host__ __device__ __forceinline__ float rect_qmin(float a, float b, float c, float ia, float ic, float dxl, float dxh,
-                                           float dyl, float dyh) {
-    const bool xin = dxl <= 0.f && dxh >= 0.f, yin = dyl <= 0.f && dyh >= 0.f;
-    if (xin && yin) return 0.f;
-    float q = 3.0e38f;
-    if (!xin) {  // the facing column: dx = dxl (mean right of it) or dxh (mean left of it)
-        const float X = dxl > 0.f ? dxl : dxh;
-        const float y = fminf(fmaxf(-b * X * ic, dyl), dyh);
-        q = a * X * X + 2.f * b * X * y + c * y * y;
-    }
-    if (!yin) {  // the facing row
-        const float Y = dyl > 0.f ? dyl : dyh;
-        const float x = fminf(fmaxf(-b * Y * ia, dxl), dxh);
-        q = fminf(q, a * x * x + 2.f * b * x * Y + c * Y * Y);
-    }
-    return q;
-}
-
-// Per-Gaussian part of the strip test, computed once per Gaussian (not once per instance):
-// (K = 2 ln(255 o), 1/a, 1/c, mode) with mode 0 = test the strips, 1 = no strip (o < 1/255:
-// alpha <= o < 1/255 at every pixel), 2 = every strip (non-finite or non-positive-definite conic).
-__host__ __device__ __forceinline__ float4 strip_pre(float4 co) {
-    const float a = co.x, b = co.y, c = co.z, o = co.w;
-    if (o < 1.0f / 255.0f) return make_float4(0.f, 0.f, 0.f, __builtin_bit_cast(float, 1u));
-    if (!(a > 0.f) || !(c > 0.f) || !(a * c - b * b > 0.f) || !(o <= 3.0e38f))
-        return make_float4(0.f, 0.f, 0.f, __builtin_bit_cast(float, 2u));
-    return make_float4(2.0f * logf(255.0f * o), 1.0f / a, 1.0f / c, __builtin_bit_cast(float, 0u));
-}
+// (rect_qmin, strip_pre and box_reach: gsr_cull.h, shared with render_fwd's quad waves)
 
 // Strip mask of one (Gaussian, tile) instance: bit s is set unless no pixel centre of the tile's
 // s-th strip (strip_origin, kStripW x kStripH) can give alpha = min(0.99, o*exp(-Q/2)) >= 1/255, i.e. unless Q > 2 ln(255 o)
@@ -841,14 +807,8 @@ __host__ __device__ __forceinline__ uint32_t strip_mask(float4 co, float4 pre, f
     for (int s = 0; s < kStrips; s++) {
         int sx0, sy0;
         strip_origin(tx, ty, s, sx0, sy0);
-        const float x0 = (float)sx0, y0 = (float)sy0;
-        const float dxl = m.x - (x0 + (float)(kStripW - 1)), dxh = m.x - x0;
-        const float mx = fmaxf(fabsf(dxl), fabsf(dxh));
-        const float dyl = m.y - (y0 + (float)(kStripH - 1)), dyh = m.y - y0;
-        const float my = fmaxf(fabsf(dyl), fabsf(dyh));
-        const float slack = 1e-4f * (a * mx * mx + 2.f * fabsf(b) * mx * my + c * my * my) + 1e-3f * K + 1e-3f;
-        const float q = rect_qmin(a, b, c, pre.y, pre.z, dxl, dxh, dyl, dyh);
-        if (!(q > K + slack)) bits |= 1u << s;
+        if (box_reach(a, b, c, K, pre.y, pre.z, m, (float)sx0, (float)sy0, (float)kStripW, (float)kStripH))
+            bits |= 1u << s;
     }
     return bits;
 }

@@ -1,0 +1,65 @@
+// gsr_cull.h -- the exact, conservative "can this Gaussian reach alpha >= 1/255 anywhere in this
+// pixel rectangle" test: binning's per-strip masks (binning.hip strip_mask) and render_fwd's
+// per-quad cull of the single-frame quad waves.  A rejected (rectangle, Gaussian) pair only ever
+// removes pairs the blend skips anyway (alpha < 1/255, forward.cu:362-363), so culling with it is
+// decision-preserving.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <math.h>
+#include <stdint.h>
+
+namespace gsr {
+
+// Minimum over the pixel-centre rectangle dx in [dxl, dxh], dy in [dyl, dyh] (dx = mean - pixel)
+// of the conic's quadratic form Q = a dx^2 + 2b dx dy + c dy^2 (power = -Q/2 in the blend).  Q is
+// convex (a, c > 0, ac > b^2), so the minimum is 0 if the mean lies inside, else it lies on an edge:
+// each edge is a 1-D quadratic minimised by clamping its vertex.
+// Only the edges FACING the mean can hold that minimum: from a point of any other edge the segment
+// towards the mean enters the rectangle and Q falls along it (convexity).  So at most one vertical
+// edge (the column nearest the mean, when the mean is left or right of the rectangle) and one
+// horizontal edge are evaluated -- half of the four-edge form's work, the same minimum.
+__host__ __device__ __forceinline__ float rect_qmin(float a, float b, float c, float ia, float ic, float dxl, float dxh,
+                                           float dyl, float dyh) {
+    const bool xin = dxl <= 0.f && dxh >= 0.f, yin = dyl <= 0.f && dyh >= 0.f;
+    if (xin && yin) return 0.f;
+    float q = 3.0e38f;
+    if (!xin) {  // the facing column: dx = dxl (mean right of it) or dxh (mean left of it)
+        const float X = dxl > 0.f ? dxl : dxh;
+        const float y = fminf(fmaxf(-b * X * ic, dyl), dyh);
+        q = a * X * X + 2.f * b * X * y + c * y * y;
+    }
+    if (!yin) {  // the facing row
+        const float Y = dyl > 0.f ? dyl : dyh;
+        const float x = fminf(fmaxf(-b * Y * ia, dxl), dxh);
+        q = fminf(q, a * x * x + 2.f * b * x * Y + c * Y * Y);
+    }
+    return q;
+}
+
+// Per-Gaussian part of the strip test, computed once per Gaussian (not once per instance):
+// (K = 2 ln(255 o), 1/a, 1/c, mode) with mode 0 = test the strips, 1 = no strip (o < 1/255:
+// alpha <= o < 1/255 at every pixel), 2 = every strip (non-finite or non-positive-definite conic).
+__host__ __device__ __forceinline__ float4 strip_pre(float4 co) {
+    const float a = co.x, b = co.y, c = co.z, o = co.w;
+    if (o < 1.0f / 255.0f) return make_float4(0.f, 0.f, 0.f, __builtin_bit_cast(float, 1u));
+    if (!(a > 0.f) || !(c > 0.f) || !(a * c - b * b > 0.f) || !(o <= 3.0e38f))
+        return make_float4(0.f, 0.f, 0.f, __builtin_bit_cast(float, 2u));
+    return make_float4(2.0f * logf(255.0f * o), 1.0f / a, 1.0f / c, __builtin_bit_cast(float, 0u));
+}
+
+// Whether the Gaussian (conic a, b, c; pre = strip_pre's K, 1/a, 1/c) can give alpha >= 1/255 at
+// some pixel centre of the w x h rectangle at (x0, y0): not (Q > K) on the whole rectangle, with a
+// slack of 1e-4 of the form's term magnitudes + 1e-3 relative that covers float rounding of both
+// this test and the blend's power (tools/strip_mask_check.cpp brute-forces it).
+__host__ __device__ __forceinline__ bool box_reach(float a, float b, float c, float K, float ia, float ic, float2 m,
+                                                   float x0, float y0, float w, float h) {
+    const float dxl = m.x - (x0 + (w - 1.0f)), dxh = m.x - x0;
+    const float mx = fmaxf(fabsf(dxl), fabsf(dxh));
+    const float dyl = m.y - (y0 + (h - 1.0f)), dyh = m.y - y0;
+    const float my = fmaxf(fabsf(dyl), fabsf(dyh));
+    const float slack = 1e-4f * (a * mx * mx + 2.f * fabsf(b) * mx * my + c * my * my) + 1e-3f * K + 1e-3f;
+    const float q = rect_qmin(a, b, c, ia, ic, dxl, dxh, dyl, dyh);
+    return !(q > K + slack);
+}
+
+}  // namespace gsr

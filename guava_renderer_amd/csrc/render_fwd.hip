@@ -26,6 +26,7 @@
 //
 // Roofline: per frame the kernel must read 156 B per visible Gaussian (features + 2D attributes)
 // and write 140 B per pixel (32 channels, inverse depth, final_T, n_contrib).
+#include "gsr_cull.h"
 #include "gsr_internal.h"
 
 namespace gsr {
@@ -740,6 +741,228 @@ __global__ __launch_bounds__(GSR_TILE_PIX) __attribute__((amdgpu_waves_per_eu(4)
     render_fwd_body<EXACT, false, false, true>(d, in, g, im, bn, o);
 }
 
+// ---------------------------------------------------------------- one frame: quad waves
+// The per-frame drop-in path renders ONE frame per launch; its 4,096 strips leave most of the chip
+// idle and the longest strips' serial chains set the time.  Here every strip is four work items,
+// one wave per 4x4 quad, and each quad wave walks only the Gaussians that can reach alpha >= 1/255
+// in ITS 16 pixels: per 64-entry list chunk, each lane loads the render record of one strip
+// survivor and tests it against the quad's pixel-centre box (box_reach, binning's strip test on a
+// 4x4 rectangle), and the quad survivors' records (word 7 := Gaussian index) and list positions
+// are appended to a per-wave LDS ring.  Offline, one C2 frame's longest quad chain is 0.63 of the
+// longest half-strip chain and 0.31 of it in 4-Gaussian steps (tools/analysis/quad_tail.py).
+//
+// A step takes the next FOUR ring entries: lane = pixel j (0..15) + 16 q, and each lane computes
+// Gaussian q's alpha at pixel j (one alpha per lane).  The four alphas and inverse depths reach
+// every lane by one permlane16 and two permlane32 swaps; each lane runs its pixel's serial blend
+// over the four in list order (the same decisions and products as forward.cu:349-381) and keeps
+// Gaussian q's weight, which is exactly the B operand of v_mfma_f32_16x16x4_f32 (B[k = q][n = j]),
+// with A[m][k = q] = channel m of Gaussian q: two MFMAs (channels 0-15, 16-31) accumulate the
+// quad's 32 x 16 colour tile as an exact k-ordered fma chain, bit-identical to fmaf(f, w, C)
+// Gaussian by Gaussian (the oracle).  Ring entries past the list's end are the null Gaussian
+// (zero record: opacity 0, nothing taken).  The next step's records (LDS) and feature words
+// (global) load while this step blends; the chunk after next's list entries and the next chunk's
+// records are loaded one refill ahead.
+#ifndef GSR_QUAD_WPE
+#define GSR_QUAD_WPE 4
+#endif
+constexpr int kQRing = 128;  // ring entries per wave (a refill adds <= 64 and runs below 8)
+
+template <bool EXACT>
+__global__ __launch_bounds__(GSR_TILE_PIX) __attribute__((amdgpu_waves_per_eu(GSR_QUAD_WPE))) void k_render_quad(
+    Dims d, Inputs in, GeomArena g, ImageArena im, BinArena bn, Outputs o) {
+    if (g.ctrl[kCtrlOverflow]) {
+        overflow_fill(d, o);
+        return;
+    }
+    __shared__ uint4 qrec_all[GSR_TILE_PIX / 64][kQRing * 2];  // ring records: (x, y, o, 1/depth), (A, B, C, index)
+    __shared__ uint32_t qpos_all[GSR_TILE_PIX / 64][kQRing];   // ring list positions (1-based)
+    uint4* qrec = qrec_all[threadIdx.x >> 6];
+    uint32_t* qpos = qpos_all[threadIdx.x >> 6];
+    const uint32_t ne = g.ctrl[kCtrlNonEmpty];
+    const uint32_t nquad = 16u * ne;  // 4 strips x 4 quads per non-empty tile
+    const uint32_t nempty = (uint32_t)(d.B * d.T) - ne;
+    const int lane = threadIdx.x & 63;
+    const int j = lane & 15, qq = lane >> 4;
+    const int64_t HW = (int64_t)d.H * d.W;
+    uint32_t q = __builtin_amdgcn_s_getreg((3 << 11) | 20) & 7u;  // HW_REG_XCC_ID
+    uint32_t q_left = 8;
+    for (;;) {
+        uint32_t item = 0xFFFFFFFFu;
+        while (q_left) {
+            uint32_t k = 0;
+            if (lane == 0) k = atomicAdd(&g.ctrl[kCtrlXcdQueue + kCtrlXcdStride * q], 1u);
+            k = __builtin_amdgcn_readfirstlane(k);
+            item = queue_item_n<4>(q, k, ne, nempty, in.xcd_map, g.ctrl);
+            if (item != 0xFFFFFFFFu) break;
+            q = (q + 1) & 7u;
+            q_left--;
+        }
+        if (!q_left) break;
+        if (item >= nquad) {  // empty tile: background everywhere, T = 1
+            const int tile_g = (int)im.work_list[ne + (item - nquad)];
+            const int b = tile_g / d.T;
+            const int t = tile_g - b * d.T;
+            if ((d.W & 3) == 0 &&
+                ((reinterpret_cast<uintptr_t>(o.out_color) | reinterpret_cast<uintptr_t>(o.out_invdepth)) & 15u) ==
+                    0 &&
+                (t % d.gx + 1) * GSR_BX <= d.W && (t / d.gx + 1) * GSR_BY <= d.H) {
+                fill_tile(d, im, o, in.bg + in.s_bg * b, b, t % d.gx, t / d.gx, lane);
+            } else {
+                const floatx16 unused = {};
+                for (int sp = 0; sp < kStrips; sp++) {
+                    int ex0, ey0;
+                    strip_origin(t % d.gx, t / d.gx, sp, ex0, ey0);
+                    store_strip<true, false>(d, im, o, in.bg + in.s_bg * b, b, ex0, ey0, lane, unused, unused, 1.0f,
+                                             0.f, 0u);
+                }
+            }
+            continue;
+        }
+        const uint32_t code = im.strip_list[item >> 2];
+        const int quad = (int)(item & 3u);
+        const int tile_g = (int)(code >> 2);
+        const int strip = (int)(code & 3u);
+        const int b = tile_g / d.T;
+        const int t = tile_g - b * d.T;
+        int sx0, sy0;
+        strip_origin(t % d.gx, t / d.gx, strip, sx0, sy0);
+        const int qx0 = sx0 + 4 * (quad & 1), qy0 = sy0 + 4 * (quad >> 1);
+        const int px = qx0 + (j & 3), py = qy0 + (j >> 2);
+        const bool inside = px < d.W && py < d.H;
+        const float pfx = (float)px, pfy = (float)py;
+        bool done = !inside;
+        float T = 1.0f, invd = 0.f;
+        uint32_t last = 0;
+        floatx4 qa0 = {0.f, 0.f, 0.f, 0.f}, qa1 = {0.f, 0.f, 0.f, 0.f};
+        const uint32_t smask_bit = 1u << (28 + strip);
+        if (im.strip_cnt[(int64_t)tile_g * kStrips + strip] != 0u) {
+            const uint2 range = im.ranges[tile_g];
+            const int n = (int)(range.y - range.x);
+            const uint32_t* __restrict__ plist = bn.point_list + range.x;
+            const __amdgpu_buffer_rsrc_t rrs = __builtin_amdgcn_make_buffer_rsrc(
+                (void*)(g.rrec + (int64_t)b * d.P * 2), 0, (int)min((int64_t)d.P * 32, (int64_t)0x7FFFFFFF),
+                0x00020000);
+            const __amdgpu_buffer_rsrc_t frs = __builtin_amdgcn_make_buffer_rsrc(
+                (void*)(in.colors + in.s_colors * b), 0, (int)min((int64_t)d.P * GSR_C * 4, (int64_t)0x7FFFFFFF),
+                0x00020000);
+            const float qbx = (float)qx0, qby = (float)qy0;
+            // list walk: chunk c's records (lane i: entry c*64 + i, when a strip survivor) and chunk
+            // c+1's entries are in flight one refill ahead
+            int base = 0;                  // first list position of the next chunk to test
+            uint32_t head = 0, tail = 0;   // ring counters (head advances by 4: entries never wrap in a step)
+            uint32_t e_cur = lane < n ? plist[lane] : 0u;
+            uint32_t e_nxt = 64 + lane < n ? plist[64 + lane] : 0u;
+            auto load_rec = [&](uint32_t e, int pos0, float4& r0, float4& r1) {
+                const bool sb = pos0 + lane < n && (e & smask_bit) != 0u;
+                const uint32_t off = sb ? (e & kIndexMask) * 32u : 0x80000000u;  // out of range: zeros
+                r0 = rec_load(rrs, off);
+                r1 = rec_load(rrs, off + 16u);
+            };
+            float4 c0, c1;
+            load_rec(e_cur, 0, c0, c1);
+            auto refill = [&]() {
+                // chunk at `base`: records c0 / c1 (zeros where not a strip survivor), entries e_cur
+                const bool sb = base + lane < n && (e_cur & smask_bit) != 0u;
+                bool keep = false;
+                if (sb) {
+                    const float a = -2.0f * c1.x, bb = -c1.y, c = -2.0f * c1.z;  // the conic (exact scalings)
+                    const float4 pre = strip_pre(make_float4(a, bb, c, c0.z));
+                    const uint32_t mode = __builtin_bit_cast(uint32_t, pre.w);
+                    keep = mode == 2u || (mode == 0u && box_reach(a, bb, c, pre.x, pre.y, pre.z,
+                                                                  make_float2(c0.x, c0.y), qbx, qby, 4.0f, 4.0f));
+                }
+                const uint64_t km = __ballot(keep);
+                if (keep) {
+                    const uint32_t slot = (tail + __builtin_amdgcn_mbcnt_hi((uint32_t)(km >> 32),
+                                                                            __builtin_amdgcn_mbcnt_lo((uint32_t)km, 0u))) &
+                                          (kQRing - 1);
+                    qrec[2 * slot] = __builtin_bit_cast(uint4, c0);
+                    qrec[2 * slot + 1] = make_uint4(__float_as_uint(c1.x), __float_as_uint(c1.y), __float_as_uint(c1.z),
+                                                    e_cur & kIndexMask);
+                    qpos[slot] = (uint32_t)(base + lane + 1);
+                }
+                tail += (uint32_t)__builtin_popcountll(km);
+                base += 64;
+                // next chunk: its records from the entries in hand, the entries after it
+                e_cur = e_nxt;
+                load_rec(e_cur, base, c0, c1);
+                e_nxt = base + 64 + lane < n ? plist[base + 64 + lane] : 0u;
+                __builtin_amdgcn_wave_barrier();
+            };
+            // fill so that entries [head, head + 8) exist, or the list is exhausted
+            auto ensure = [&]() {
+                while (tail - head < 8u && base < n) refill();
+            };
+            // one step's operands, lane group qq: ring entry head + qq (the null Gaussian past tail)
+            auto operands = [&](uint32_t h, float4& r0, float4& r1, uint4& pos4, float& f0, float& f1) {
+                const uint32_t slot = (h + (uint32_t)qq) & (kQRing - 1);
+                const bool valid = h + (uint32_t)qq < tail;
+                const uint4 u0 = qrec[2 * slot], u1 = qrec[2 * slot + 1];
+                r0 = valid ? __builtin_bit_cast(float4, u0) : make_float4(0.f, 0.f, 0.f, 0.f);
+                r1 = valid ? __builtin_bit_cast(float4, u1) : make_float4(0.f, 0.f, 0.f, 0.f);
+                pos4 = *reinterpret_cast<const uint4*>(&qpos[h & (kQRing - 1)]);
+                const uint32_t fo = valid ? u1.w * (uint32_t)(GSR_C * 4) + (uint32_t)j * 4u : 0x80000000u;
+                f0 = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(frs, (int)fo, 0, 0));
+                f1 = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(frs, (int)(fo + 64u), 0, 0));
+            };
+            ensure();
+            __builtin_amdgcn_wave_barrier();
+            float4 r0, r1;
+            uint4 p4;
+            float f0, f1;
+            operands(head, r0, r1, p4, f0, f1);
+            while (head < tail) {
+                // the next step's operands first (their loads run under this step's blend)
+                ensure();
+                __builtin_amdgcn_wave_barrier();
+                float4 nr0, nr1;
+                uint4 np4;
+                float nf0, nf1;
+                operands(head + 4u, nr0, nr1, np4, nf0, nf1);
+                // this step
+                const float al = alpha_of<EXACT>(r0, r1, pfx, pfy);
+                const auto a16 = __builtin_amdgcn_permlane16_swap(__float_as_uint(al), __float_as_uint(al), false, false);
+                const auto a02 = __builtin_amdgcn_permlane32_swap(a16[0], a16[0], false, false);
+                const auto a13 = __builtin_amdgcn_permlane32_swap(a16[1], a16[1], false, false);
+                const auto i16 = __builtin_amdgcn_permlane16_swap(__float_as_uint(r0.w), __float_as_uint(r0.w), false,
+                                                                  false);
+                const auto i02 = __builtin_amdgcn_permlane32_swap(i16[0], i16[0], false, false);
+                const auto i13 = __builtin_amdgcn_permlane32_swap(i16[1], i16[1], false, false);
+                const float w0 = take_step(__uint_as_float(a02[0]), __uint_as_float(i02[0]), p4.x, T, invd, last, done);
+                const float w1 = take_step(__uint_as_float(a13[0]), __uint_as_float(i13[0]), p4.y, T, invd, last, done);
+                const float w2 = take_step(__uint_as_float(a02[1]), __uint_as_float(i02[1]), p4.z, T, invd, last, done);
+                const float w3 = take_step(__uint_as_float(a13[1]), __uint_as_float(i13[1]), p4.w, T, invd, last, done);
+                const float wq = qq == 0 ? w0 : qq == 1 ? w1 : qq == 2 ? w2 : w3;
+                qa0 = __builtin_amdgcn_mfma_f32_16x16x4f32(f0, wq, qa0, 0, 0, 0);
+                qa1 = __builtin_amdgcn_mfma_f32_16x16x4f32(f1, wq, qa1, 0, 0, 0);
+                head += 4u;
+                r0 = nr0; r1 = nr1; p4 = np4; f0 = nf0; f1 = nf1;
+                if (!__any(!done)) break;  // every pixel of the quad finished
+            }
+        }
+        // epilogue: group 0 stores final_T / n_contrib / inverse depth, every lane its channels
+        // 4 qq + r and 16 + 4 qq + r of pixel j
+        const float* bgp = in.bg + in.s_bg * b;
+        const int64_t pix = (int64_t)py * d.W + px;
+        if (inside && qq == 0) {
+            im.final_T[b * HW + pix] = T;
+            im.n_contrib[b * HW + pix] = last;
+            if (o.out_invdepth) o.out_invdepth[b * HW + pix] = invd;
+        }
+        const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+            o.out_color + (int64_t)b * GSR_C * HW, 0, (int)((int64_t)GSR_C * HW * 4), 0x00020000);
+        const int vo = inside ? (int)(pix * 4) : 0x7FFFFFF0;
+#pragma unroll
+        for (int r = 0; r < 4; r++) {
+            const int c0_ = 4 * qq + r, c1_ = 16 + 4 * qq + r;
+            __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(fmaf(T, bgp[c0_], qa0[r])), rs, vo,
+                                                  c0_ * (int)HW * 4, 0);
+            __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(fmaf(T, bgp[c1_], qa1[r])), rs, vo,
+                                                  c1_ * (int)HW * 4, 0);
+        }
+    }
+}
+
 void launch_render_fwd(const Dims& d, const Inputs& in_, const GeomArena& g, const ImageArena& im,
                        const BinArena& b, const Outputs& o, bool exact, bool split, hipStream_t s) {
     Inputs in = in_;  // one frame: strip_list is one longest-first list (launch_strip_order)
@@ -754,6 +977,9 @@ void launch_render_fwd(const Dims& d, const Inputs& in_, const GeomArena& g, con
     const int wg_per_cu = wg_env > 0 ? wg_env : (d.B >= 16 ? GSR_RENDER_WPE : 4);
     // GSR_RENDER_HALF=0: single-frame launches on the throughput kernel (A/B); GSR_RENDER_HALF_WG: WGs per CU
     static const bool half_mode = tune_env("GSR_RENDER_HALF", 1) != 0;
+    // GSR_RENDER_QUAD=0: single-frame launches on the half-strip kernel (A/B); GSR_RENDER_QUAD_WG: WGs per CU
+    static const bool quad_mode = tune_env("GSR_RENDER_QUAD", 1) != 0;
+    static const int quad_wg = tune_env("GSR_RENDER_QUAD_WG", GSR_QUAD_WPE);
     static const int half_wg = tune_env("GSR_RENDER_HALF_WG", GSR_HALF_WPE);
     const int grid = min((nwaves + 3) / 4, persistent_grid(wg_per_cu));
     const dim3 gr(grid), bl(GSR_TILE_PIX);
@@ -780,6 +1006,11 @@ void launch_render_fwd(const Dims& d, const Inputs& in_, const GeomArena& g, con
         const dim3 grf(min((nwaves + 3) / 4, persistent_grid(4)));
         if (exact) hipLaunchKernelGGL((k_render_fwd_refine<true>), grf, bl, 0, s, d, in, g, im, b, o);
         else hipLaunchKernelGGL((k_render_fwd_refine<false>), grf, bl, 0, s, d, in, g, im, b, o);
+    } else if (d.B == 1 && quad_mode && !split) {
+        // one frame, quad waves with their own cull: the longest quads' chains are what count here
+        const dim3 gq(min((4 * nwaves + 3) / 4, persistent_grid(quad_wg)));
+        if (exact) hipLaunchKernelGGL((k_render_quad<true>), gq, bl, 0, s, d, in, g, im, b, o);
+        else hipLaunchKernelGGL((k_render_quad<false>), gq, bl, 0, s, d, in, g, im, b, o);
     } else if (d.B == 1 && half_mode) {
         // one frame, half-strip waves: a strip's two halves run in parallel, each lane one
         // (pixel, Gaussian) alpha per k-step -- the longest strip's time is what counts here

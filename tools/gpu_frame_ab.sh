@@ -10,7 +10,8 @@ for r in $(seq 1 ${R:-2}); do
     (
       case "$V" in
         base) ;;
-        env:*) for kv in $(echo "${V#env:}" | tr ',' ' '); do export "$kv"; done ;;
+        env:*) export GSR_LIB=guava_renderer_amd/lib/ab/libgsr_tune.so  # (the product library ignores them)
+               for kv in $(echo "${V#env:}" | tr ',' ' '); do export "$kv"; done ;;
         *) export GSR_LIB=guava_renderer_amd/lib/ab/libgsr_$V.so ;;
       esac
       tag=$(echo "$V" | tr -c 'A-Za-z0-9_\n' '_')
