@@ -53,12 +53,8 @@ struct Parents {
 
 // batch_rodrigues (lbs.py:379-410): angle = |r + 1e-8|, dir = r / angle,
 // R = I + sin K + (1 - cos) K.K with K the cross-product matrix of dir.
-__global__ void k_lbs_rodrigues(int B, int J, const float* __restrict__ pose, int pose2rot,
-                                float* __restrict__ rot, float* __restrict__ feat) {
-    const int t = blockIdx.x * blockDim.x + threadIdx.x;
-    if (t >= B * J) return;
-    const int b = t / J, j = t - b * J;
-    float R[9];
+// batch_rodrigues (lbs.py:379-410) of pose entry t (axis-angle, or a rotation matrix when !pose2rot)
+__device__ __forceinline__ void rodrigues_one(const float* __restrict__ pose, int t, int pose2rot, float (&R)[9]) {
     if (pose2rot) {
         const float rx = pose[3 * t], ry = pose[3 * t + 1], rz = pose[3 * t + 2];
         const float ex = rx + 1e-8f, ey = ry + 1e-8f, ez = rz + 1e-8f;
@@ -78,6 +74,15 @@ __global__ void k_lbs_rodrigues(int B, int J, const float* __restrict__ pose, in
 #pragma unroll
         for (int e = 0; e < 9; e++) R[e] = pose[9 * t + e];
     }
+}
+
+__global__ void k_lbs_rodrigues(int B, int J, const float* __restrict__ pose, int pose2rot,
+                                float* __restrict__ rot, float* __restrict__ feat) {
+    const int t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= B * J) return;
+    const int b = t / J, j = t - b * J;
+    float R[9];
+    rodrigues_one(pose, t, pose2rot, R);
 #pragma unroll
     for (int e = 0; e < 9; e++) rot[9 * t + e] = R[e];
     if (j > 0) {  // pose_feature = (rot_mats[:, 1:] - I).view(B, -1)   (lbs.py:303)
@@ -419,16 +424,31 @@ __device__ __forceinline__ float blend_tiled_one(const float* __restrict__ coef,
     return acc;
 }
 
+// pose (single-frame LBS, gsr_lbs_sp): the pose features are formed here from the frame's pose
+// (rodrigues_one, the same expressions as k_lbs_rodrigues) instead of read from a launch before
 __global__ __launch_bounds__(256) void k_lbs_blend_tiled1(int M, int NB, int NP, const float* __restrict__ vt,
                                                           const float* __restrict__ betas,
                                                           const float4* __restrict__ sd_tiled,
                                                           const float* __restrict__ feat,
                                                           const float4* __restrict__ pd_tiled,
                                                           float* __restrict__ v_shaped,
-                                                          float* __restrict__ v_posed) {
+                                                          float* __restrict__ v_posed,
+                                                          const float* __restrict__ pose, int pose2rot) {
     __shared__ float red[2][4][64];
+    __shared__ float sfeat[9 * (GSR_LBS_MAX_JOINTS - 1)];
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, hi = lane >> 5, l32 = lane & 31;
     const int t = blockIdx.x, m = t * 32 + l32;
+    if (pose && NP > 0 && v_posed) {
+        const int jn = NP / 9;  // J - 1 posed joints (pose_feature skips the root)
+        if ((int)threadIdx.x < jn) {
+            float R[9];
+            rodrigues_one(pose, (int)threadIdx.x + 1, pose2rot, R);
+#pragma unroll
+            for (int e = 0; e < 9; e++) sfeat[9 * threadIdx.x + e] = R[e] - ((e % 4) == 0 ? 1.0f : 0.0f);
+        }
+        __syncthreads();
+        feat = sfeat;
+    }
     red[0][w][lane] = NB > 0 ? blend_tiled_one(betas, sd_tiled, NB, t, w, hi, lane) : 0.f;
     red[1][w][lane] = (NP > 0 && v_posed) ? blend_tiled_one(feat, pd_tiled, NP, t, w, hi, lane) : 0.f;
     __syncthreads();
@@ -449,7 +469,15 @@ __global__ __launch_bounds__(256) void k_lbs_blend_tiled1(int M, int NB, int NP,
 // (tiled bases, when the caller prepared them: B > kLbsFrames and B = 1)
 static void launch_blend(int B, int M, int NB, int NP, const float* vt, int64_t vt_stride, const float* betas,
                          const float* sd_t, const float* feat, const float* pd, float* vs, float* vp,
-                         hipStream_t s, const GsrLbsSparse* sp = nullptr);
+                         hipStream_t s, const GsrLbsSparse* sp = nullptr, const float* pose = nullptr,
+                         int pose2rot = 1);
+
+// the single-frame tiled blend forms the pose features itself (k_lbs_blend_tiled1's pose argument)
+static bool blend_takes_pose(int B, int NB, int NP, const float* vp, const GsrLbsSparse* sp) {
+    static const bool tiled_on = tune_env("GSR_BLEND_TILED", 1) != 0;
+    return B == 1 && tiled_on && sp && (NB == 0 || sp->shapedirs_tiled) && (NP == 0 || !vp || sp->posedirs_tiled) &&
+           (NB > 0 || (NP > 0 && vp)) && NP <= 9 * (GSR_LBS_MAX_JOINTS - 1);
+}
 
 static size_t lbs_blend_lds(int NB, int NP, int nf, int split) {
     const size_t coef = sizeof(float) * (size_t)(NB + NP) * nf;
@@ -470,7 +498,7 @@ static void lbs_blend_attr(size_t lds) {
 
 static void launch_blend(int B, int M, int NB, int NP, const float* vt, int64_t vt_stride, const float* betas,
                          const float* sd_t, const float* feat, const float* pd, float* vs, float* vp,
-                         hipStream_t s, const GsrLbsSparse* sp) {
+                         hipStream_t s, const GsrLbsSparse* sp, const float* pose, int pose2rot) {
     static const bool valu_only = tune_env("GSR_BLEND_VALU", 0) == 1;  // timing A/B only
     // GSR_BLEND_TILED=0: the k-major kernels even with tiled bases (A/B)
     static const bool tiled_on = tune_env("GSR_BLEND_TILED", 1) != 0;
@@ -493,7 +521,7 @@ static void launch_blend(int B, int M, int NB, int NP, const float* vt, int64_t 
     if (tiled && B == 1) {
         hipLaunchKernelGGL(k_lbs_blend_tiled1, dim3((M + 31) / 32), dim3(256), 0, s, M, NB, vp ? NP : 0, vt, betas,
                            reinterpret_cast<const float4*>(sp->shapedirs_tiled), feat,
-                           reinterpret_cast<const float4*>(sp->posedirs_tiled), vs, vp);
+                           reinterpret_cast<const float4*>(sp->posedirs_tiled), vs, vp, pose, pose2rot);
         return;
     }
     if (B > kLbsFrames && !valu_only) {
@@ -622,11 +650,13 @@ __global__ __launch_bounds__(256) void k_lbs_joints_csr(int B, int V, int J, con
 // tree (16 threads per joint, one matrix element each): every joint of a level in one step, so
 // SMPL-X's 54 sequential products become its tree depth (~10) barrier steps -- each product is
 // the same expression as the sequential chain's, so the results are identical.
+// rot == null: each joint's rotation from the pose (rodrigues_one), as the single-frame path does
 __global__ __launch_bounds__(16 * GSR_LBS_MAX_JOINTS) void k_lbs_chain(int J, Parents par,
                                                                      const float* __restrict__ rot,
                                                                      const float* __restrict__ joints,
                                                                      float* __restrict__ jtrans,
-                                                                     float* __restrict__ A) {
+                                                                     float* __restrict__ A,
+                                                                     const float* __restrict__ pose, int pose2rot) {
     __shared__ float tm[GSR_LBS_MAX_JOINTS][16];
     __shared__ float ch[GSR_LBS_MAX_JOINTS][16];
     __shared__ int depth[GSR_LBS_MAX_JOINTS];
@@ -635,7 +665,13 @@ __global__ __launch_bounds__(16 * GSR_LBS_MAX_JOINTS) void k_lbs_chain(int J, Pa
     const float* Jb = joints + (int64_t)b * J * 3;
     if (t == 0) maxd = 0;
     if (t < J) {
-        const float* R = rot + ((int64_t)b * J + t) * 9;
+        float R[9];
+        if (rot) {
+#pragma unroll
+            for (int e = 0; e < 9; e++) R[e] = rot[((int64_t)b * J + t) * 9 + e];
+        } else {
+            rodrigues_one(pose, b * J + t, pose2rot, R);
+        }
         float rel[3];
         for (int c = 0; c < 3; c++) rel[c] = t == 0 ? Jb[c] : Jb[3 * t + c] - Jb[3 * par.p[t] + c];
         for (int r = 0; r < 3; r++) {
@@ -1249,15 +1285,22 @@ int gsr_lbs_sp(int B, int V, int J, int NB, const float* v_template, int64_t v_t
     const int NP = (J - 1) * 9;
     const int M = V * 3;
 
-    hipLaunchKernelGGL(k_lbs_rodrigues, dim3((B * J + 255) / 256), dim3(256), 0, s, B, J, pose,
-                       pose2rot, a.rot, a.feat);
-    if (int rc = hip_check("lbs_rodrigues")) return rc;
     if (lbs_blend_lds(NB, NP, kLbsFrames, kLbsSplit) > 160 * 1024) return api_fail(GSR_ERR_ARG, "gsr_lbs: NB + 9(J-1) too large for LDS");
-    launch_blend(B, M, NB, NP, v_template, v_template_stride, betas, shapedirs_t, a.feat, posedirs, vs, a.vp, s, sp);
+    // single frame on tiled bases: Rodrigues runs inside the blend (pose features) and the chain
+    // (rotations), one launch fewer on the per-frame path; otherwise its own launch feeds both
+    const bool fused = blend_takes_pose(B, NB, NP, a.vp, sp);
+    if (!fused) {
+        hipLaunchKernelGGL(k_lbs_rodrigues, dim3((B * J + 255) / 256), dim3(256), 0, s, B, J, pose,
+                           pose2rot, a.rot, a.feat);
+        if (int rc = hip_check("lbs_rodrigues")) return rc;
+    }
+    launch_blend(B, M, NB, NP, v_template, v_template_stride, betas, shapedirs_t, a.feat, posedirs, vs, a.vp, s, sp,
+                 fused ? pose : nullptr, pose2rot);
     if (int rc = hip_check("lbs_blend")) return rc;
     launch_joints(B, V, J, J_regressor, sp, vs, joints_offset, jr, s);
     if (int rc = hip_check("lbs_joints")) return rc;
-    hipLaunchKernelGGL(k_lbs_chain, dim3(B), dim3(16 * GSR_LBS_MAX_JOINTS), 0, s, J, par, a.rot, jr, joints_transformed, A);
+    hipLaunchKernelGGL(k_lbs_chain, dim3(B), dim3(16 * GSR_LBS_MAX_JOINTS), 0, s, J, par, fused ? nullptr : a.rot,
+                       jr, joints_transformed, A, pose, pose2rot);
     if (int rc = hip_check("lbs_chain")) return rc;
     if (sp && sp->skin_k > 0) {
         const dim3 g((V + 255) / 256, B);

@@ -141,7 +141,7 @@ NOISE_FACTOR = 3.0      # per-element bound relative to the reference algorithm'
 
 
 def grad_check(name, a, b, scale_tol=GRAD_SCALE_TOL, elem_tol=GRAD_ELEM_TOL, floor=GRAD_ELEM_FLOOR,
-               noise=None):
+               noise=None, p999_tol=None):
     """Gradient parity, two ways: against the tensor's scale (the per-Gaussian atomics of the
     reference, backward.cu:593-635, reassociate freely) and per element -- a Gaussian with a small but
     not negligible gradient must be right too: relative error <= elem_tol on every element with
@@ -149,7 +149,7 @@ def grad_check(name, a, b, scale_tol=GRAD_SCALE_TOL, elem_tol=GRAD_ELEM_TOL, flo
     (oracle.backward(reverse_order=True)); the closed-form backward amplifies f32 reassociation on
     ill-conditioned elements (the 2x2 conic inverse, computeCov2DCUDA, backward.cu:147-326), so the
     per-element bound is max(elem_tol, NOISE_FACTOR x the reference's own reordering error), and the
-    99.9th percentile must stay within elem_tol / 10.  Prints both distributions."""
+    99.9th percentile must stay within p999_tol (default elem_tol / 10).  Prints both distributions."""
     a = np.asarray(a, np.float64).reshape(-1)
     b = np.asarray(b, np.float64).reshape(-1)
     assert a.shape == b.shape, (name, a.shape, b.shape)
@@ -173,4 +173,5 @@ def grad_check(name, a, b, scale_tol=GRAD_SCALE_TOL, elem_tol=GRAD_ELEM_TOL, flo
           f"max {rel.max(initial=0.0):.3g}, p99.9 {p999:.3g}{msg}")
     assert err_scale <= scale_tol, f"{name}: {err_scale:.3g} of scale"
     assert rel.max(initial=0.0) <= limit, f"{name}: element rel err {rel.max():.3g} > {limit:.3g} (p99.9 {p999:.3g})"
-    assert p999 <= elem_tol / 10, f"{name}: element rel err p99.9 {p999:.3g}"
+    p999_tol = elem_tol / 10 if p999_tol is None else p999_tol
+    assert p999 <= p999_tol, f"{name}: element rel err p99.9 {p999:.3g} > {p999_tol:.3g}"

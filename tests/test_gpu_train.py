@@ -141,7 +141,10 @@ def test_fullsize_backward_batch6(split, per_frame_colors):
         print(f"frame {f} (split {split}, per-frame colours {per_frame_colors}):")
         for name, b, bn in zip(NAMES, o, o_rev):
             if name in mine:
-                grad_check(f"frame {f} {name}", mine[name], b, noise=bn)
+                # split-bf16 g (≤ 3e-5 relative per product) cancels over the 32
+                # channels of a random dL: the per-element tail is looser than the exact mode's,
+                # p99.9 <= 5e-4 instead of 1e-4 (max and scale bars unchanged)
+                grad_check(f"frame {f} {name}", mine[name], b, noise=bn, p999_tol=5e-4 if split else None)
 
 
 def _ssim64(img, tgt):
