@@ -295,18 +295,21 @@ constexpr int kCountThreads = 1024, kCountPer = 8;
 // kernel above that size, and make_dims' nb_cap keeps NB there for every P it serves
 constexpr int kLdsBuckets = 16384;
 static_assert(kLdsBuckets % kCountThreads == 0, "bucket claims: whole rows of the workgroup");
+// PER Gaussians per thread: kCountPer, or fewer for the single-frame launch (more workgroups for a
+// latency-bound grid)
+template <int PER>
 __global__ __launch_bounds__(kCountThreads) void k_bucket_count_lds(Dims d, GeomArena g) {
     extern __shared__ uint32_t hist[];  // NB
     if (g.ctrl[kCtrlOverflow]) return;
     const int b = blockIdx.y;
-    const int i0 = blockIdx.x * kCountThreads * kCountPer;
+    const int i0 = blockIdx.x * kCountThreads * PER;
     for (int k = threadIdx.x; k < d.NB; k += kCountThreads) hist[k] = 0u;
     __syncthreads();
     const uint32_t kmin = ~g.fstat[kFsWords * b + kFsNotKeyMax], kmax = g.fstat[kFsWords * b + kFsKeyMax];
     const float scale = bucket_scale(kmin, kmax, d.NB);
-    uint32_t bk[kCountPer], ls[kCountPer];
+    uint32_t bk[PER], ls[PER];
 #pragma unroll
-    for (int p = 0; p < kCountPer; p++) {
+    for (int p = 0; p < PER; p++) {
         const int i = i0 + p * kCountThreads + threadIdx.x;
         bk[p] = 0xFFFFFFFFu;
         ls[p] = 0u;
@@ -340,7 +343,7 @@ __global__ __launch_bounds__(kCountThreads) void k_bucket_count_lds(Dims d, Geom
     }
     __syncthreads();
 #pragma unroll
-    for (int p = 0; p < kCountPer; p++) {
+    for (int p = 0; p < PER; p++) {
         const int i = i0 + p * kCountThreads + threadIdx.x;
         if (bk[p] != 0xFFFFFFFFu) g.bslot[(int64_t)b * d.P + i] = hist[bk[p]] + ls[p];
     }
@@ -433,7 +436,9 @@ constexpr size_t sort_lds_bytes(int NT, int CAP) { return (size_t)14 * CAP + 4 *
 
 // Large buckets (worklist from k_bucket_scan): LDS sort, 256 threads up to kSortSmallCap keys,
 // 1024 threads up to kSortLargeCap, a bitonic network in global memory beyond.
-template <int NT, int CAP>
+// ALL: one launch takes every listed bucket (the single-frame path, whose few long buckets do not
+// pay for a second launch)
+template <int NT, int CAP, bool ALL = false>
 __global__ __launch_bounds__(NT) void k_bucket_sort(Dims d, GeomArena g) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     if (g.ctrl[kCtrlOverflow]) return;
@@ -444,7 +449,7 @@ __global__ __launch_bounds__(NT) void k_bucket_sort(Dims d, GeomArena g) {
         const uint32_t* bs = g.bstart + (int64_t)b * (d.NB + 1);
         const uint32_t s0 = bs[bk];
         const int n = (int)(bs[bk + 1] - s0);
-        const bool mine = (CAP == kSortSmallCap) ? n <= kSortSmallCap : n > kSortSmallCap;
+        const bool mine = ALL || ((CAP == kSortSmallCap) ? n <= kSortSmallCap : n > kSortSmallCap);
         if (!mine) continue;
         uint64_t* keys = g.skey + (int64_t)b * d.P + s0;
         uint32_t* out = g.order + (int64_t)b * d.P + s0;
@@ -461,9 +466,17 @@ __global__ __launch_bounds__(NT) void k_bucket_sort(Dims d, GeomArena g) {
 void launch_depth_sort(const Dims& d, const GeomArena& g, hipStream_t s) {
     if (d.P == 0 || d.B == 0) return;
     if (d.NB <= kLdsBuckets) {  // every bucket has a claim slot (kClaims per thread)
-        const int per_wg = kCountThreads * kCountPer;
-        hipLaunchKernelGGL(k_bucket_count_lds, dim3((d.P + per_wg - 1) / per_wg, d.B), dim3(kCountThreads),
-                           (size_t)d.NB * 4, s, d, g);
+        // GSR_B1_COUNT_PER: Gaussians per thread of the single-frame count (2 or kCountPer)
+        static const int b1_per = tune_env("GSR_B1_COUNT_PER", kCountPer);
+        if (d.B == 1 && b1_per == 2) {
+            const int per_wg = kCountThreads * 2;
+            hipLaunchKernelGGL(k_bucket_count_lds<2>, dim3((d.P + per_wg - 1) / per_wg, d.B), dim3(kCountThreads),
+                               (size_t)d.NB * 4, s, d, g);
+        } else {
+            const int per_wg = kCountThreads * kCountPer;
+            hipLaunchKernelGGL(k_bucket_count_lds<kCountPer>, dim3((d.P + per_wg - 1) / per_wg, d.B),
+                               dim3(kCountThreads), (size_t)d.NB * 4, s, d, g);
+        }
     } else {
         hipLaunchKernelGGL(k_bucket_count, dim3(d.nblk, d.B), dim3(kScanBlock), 0, s, d, g);
     }
@@ -475,6 +488,15 @@ void launch_depth_sort(const Dims& d, const GeomArena& g, hipStream_t s) {
         attr = true;
         hipFuncSetAttribute((const void*)k_bucket_sort<1024, kSortLargeCap>,
                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)sort_lds_bytes(1024, kSortLargeCap));
+        hipFuncSetAttribute((const void*)k_bucket_sort<1024, kSortLargeCap, true>,
+                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)sort_lds_bytes(1024, kSortLargeCap));
+    }
+    // GSR_SORT1=0: the two launches at B = 1 too (A/B)
+    static const bool one_launch = tune_env("GSR_SORT1", 1) != 0;
+    if (d.B == 1 && one_launch) {
+        hipLaunchKernelGGL((k_bucket_sort<1024, kSortLargeCap, true>), dim3(persistent_grid(1) / 4), dim3(1024),
+                           sort_lds_bytes(1024, kSortLargeCap), s, d, g);
+        return;
     }
     hipLaunchKernelGGL((k_bucket_sort<256, kSortSmallCap>), dim3(persistent_grid(2)), dim3(256),
                        sort_lds_bytes(256, kSortSmallCap), s, d, g);

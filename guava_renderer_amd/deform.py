@@ -332,6 +332,17 @@ class EHMDeformer:
         self.l_eyelid, self.r_eyelid = t(np.asarray(l_eyelid, np.float32)), t(np.asarray(r_eyelid, np.float32))
         self.bad = torch.zeros(1, dtype=torch.int32, device=dev)
         self._ws = {}
+        # the FLAME head chain and the body blend shapes are independent until the splice: the head
+        # runs on a side stream beside the body (GSR_EHM_OVERLAP=0: one stream, A/B)
+        self.overlap = os.environ.get("GSR_EHM_OVERLAP", "1") != "0"
+        self._side = {}
+
+    def _side_stream(self, main):
+        """(side stream, fork event, join event) for a main stream, made once."""
+        key = main.cuda_stream
+        if key not in self._side:
+            self._side[key] = (torch.cuda.Stream(self.dev), torch.cuda.Event(), torch.cuda.Event())
+        return self._side[key]
 
     def _workspace(self, B, V, J, NB):
         # one per stream: batches in flight on different streams must not share scratch
@@ -380,16 +391,25 @@ class EHMDeformer:
             _seg(segs, hsb, 0, hs, B)
         table = _fill_zeros(segs, views, B)
         _lib.check(L.gsr_pack_rows(B, len(table), (_lib.RowSegment * len(table))(*table), st), "gsr_pack_rows")
-        # FLAME head (EHM.py:41-75)
+        # FLAME head (EHM.py:41-75), on the side stream when overlapping: every buffer it touches is
+        # allocated on the main stream and the main stream joins it before the splice reads them
         hv = torch.empty((B, Vh, 3), **o)
         hj = torch.empty((B, Jh, 3), **o)
         sph = ctypes.byref(self.sparse["flame"][0]) if "flame" in self.sparse else None
         spb = ctypes.byref(self.sparse["body"][0]) if "body" in self.sparse else None
+        ws_h = self._workspace(B, Vh, Jh, NBh)
+        hst = st
+        if self.overlap:
+            main = torch.cuda.current_stream(self.dev)
+            side, fork, join = self._side_stream(main)
+            fork.record(main)
+            side.wait_event(fork)
+            hst = ctypes.c_void_p(side.cuda_stream)
         rc = L.gsr_lbs_sp(B, Vh, Jh, NBh, _ptr(fa["v_template"]), 0, _ptr(betas_h),
                           _ptr(fa["shapedirs_t"]), _ptr(pose_h), 1, _ptr(fa["posedirs"]),
                           _ptr(fa["J_regressor"]), fa["parents"].ctypes.data_as(ctypes.c_void_p),
                           _ptr(fa["lbs_weights_t"]), None, _ptr(hv), _ptr(hj), None, None, None, None,
-                          _ptr(self._workspace(B, Vh, Jh, NBh)), sph, st)
+                          _ptr(ws_h), sph, hst)
         _lib.check(rc, "gsr_lbs (FLAME head)")
         # body template (EHM.py:101-118): blend shapes of shape ++ exp, regressed joints + offset
         joff = _f32(bp["joints_offset"]) if bp.get("joints_offset") is not None else None
@@ -398,6 +418,9 @@ class EHMDeformer:
         _lib.check(L.gsr_blend_joints_sp(B, Vb, Jb, NBb, _ptr(ba["v_template"]), 0, _ptr(sc),
                                          _ptr(ba["shapedirs_t"]), _ptr(ba["J_regressor"]), _ptr(joff),
                                          _ptr(vt), _ptr(tj), spb, st), "gsr_blend_joints")
+        if self.overlap:
+            join.record(side)
+            main.wait_event(join)
         # head splice (EHM.py:72-75, 121-124)
         eyelid = _f32(fp["eyelid_params"]) if fp.get("eyelid_params") is not None else None
         _lib.check(L.gsr_splice_head(B, Vb, Vh, _ptr(self.head_index), _ptr(hv), _ptr(self.r_eyelid),
