@@ -21,7 +21,7 @@ EXPORTS = ("gsr_version", "gsr_last_error", "gsr_geometry_bytes",
            "gsr_lbs_tiled_floats", "gsr_lbs_tile_bases",
            "gsr_scratch_geometry", "gsr_scratch_binning", "gsr_scratch_image", "gsr_forward_batch_deformed",
            "gsr_splice_head",
-           "gsr_pack_rows", "gsr_deform_gaussians",
+           "gsr_pack_rows", "gsr_deform_gaussians", "gsr_ehm_workspace_bytes", "gsr_ehm_forward",
            # include/gsr_ssim.h
            "gsr_fused_ssim", "gsr_fused_ssim_backward", "gsr_image_loss_partials", "gsr_image_loss")
 
@@ -84,6 +84,37 @@ class LbsSparse(ctypes.Structure):
                 ("shapedirs_tiled", _vp), ("posedirs_tiled", _vp), ("shapedirs_tiled_k", ctypes.c_int32),
                 ("shapedirs_tiled_m", ctypes.c_int32), ("posedirs_tiled_k", ctypes.c_int32),
                 ("posedirs_tiled_m", ctypes.c_int32)]
+
+
+class EhmModel(ctypes.Structure):
+    """GsrEhmModel (include/gsr_deform.h)."""
+    _fields_ = [("V", ctypes.c_int32), ("J", ctypes.c_int32), ("NB", ctypes.c_int32), ("pad_", ctypes.c_int32),
+                ("v_template", _vp), ("shapedirs_t", _vp), ("posedirs", _vp), ("J_regressor", _vp),
+                ("lbs_weights_t", _vp), ("parents_host", _vp), ("sparse", ctypes.POINTER(LbsSparse))]
+
+
+class Ehm(ctypes.Structure):
+    """GsrEhm (include/gsr_deform.h)."""
+    _fields_ = [("flame", EhmModel), ("body", EhmModel), ("head_index", _vp), ("l_eyelid", _vp),
+                ("r_eyelid", _vp), ("N_head", ctypes.c_int32), ("hj0", ctypes.c_int32), ("hj1", ctypes.c_int32),
+                ("bj0", ctypes.c_int32), ("bj1", ctypes.c_int32), ("pad_", ctypes.c_int32), ("bad_index_flag", _vp)]
+
+
+class EhmParam(ctypes.Structure):
+    """GsrEhmParam (include/gsr_deform.h)."""
+    _fields_ = [("p", _vp), ("row_stride", _i64), ("width", ctypes.c_int32), ("pad_", ctypes.c_int32)]
+
+
+class EhmOutputs(ctypes.Structure):
+    """GsrEhmOutputs (include/gsr_deform.h)."""
+    _fields_ = [("vertices", _vp), ("joints", _vp), ("joints_transform", _vp), ("ver_transform_mat", _vp),
+                ("joint_transform_mat", _vp)]
+
+
+# GsrEhmParam slots (include/gsr_deform.h GSR_EHM_*)
+EHM_SLOTS = ("flame.shape_params", "flame.expression_params", "flame.jaw_params", "flame.eye_pose_params",
+             "flame.eyelid_params", "body.shape", "body.exp", "body.global_pose", "body.body_pose",
+             "body.left_hand_pose", "body.right_hand_pose", "body.head_scale", "body.joints_offset")
 
 
 class GsrError(RuntimeError):
@@ -205,6 +236,11 @@ def load(path=None):
     L.gsr_deform_gaussians.argtypes = [_i, _i, _i, _i, _vp, _vp, _vp, _vp, _i64, _vp, _i64, _vp, _vp,
                                        _vp, _i64, _vp, _i64, _vp, _i64, _vp, _vp, _vp, _vp, _vp]
     L.gsr_deform_gaussians.restype = _i
+    L.gsr_ehm_workspace_bytes.argtypes = [ctypes.POINTER(Ehm), _i]
+    L.gsr_ehm_workspace_bytes.restype = _sz
+    L.gsr_ehm_forward.argtypes = [ctypes.POINTER(Ehm), _i, ctypes.POINTER(EhmParam), ctypes.POINTER(EhmOutputs),
+                                  _vp, _vp]
+    L.gsr_ehm_forward.restype = _i
     L.gsr_fused_ssim.argtypes = [_i, _i, _i, _i, _f, _f, _vp, _vp, _vp, _vp, _vp, _vp, _vp]
     L.gsr_fused_ssim.restype = _i
     L.gsr_fused_ssim_backward.argtypes = [_i, _i, _i, _i, _f, _f, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp]

@@ -17,7 +17,7 @@ LIB_DIR = os.path.join(HERE, "lib")
 OBJ_DIR = os.path.join(HERE, "lib", "obj")
 LIB = os.path.join(LIB_DIR, "libgsr.so")
 SOURCES = ["preprocess.hip", "binning.hip", "render_fwd.hip", "render_bwd.hip",
-           "preprocess_bwd.hip", "deform.hip", "ssim.hip", "frames.hip", "capi.hip"]
+           "preprocess_bwd.hip", "deform.hip", "ehm.hip", "ssim.hip", "frames.hip", "capi.hip"]
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = os.environ.get("GSR_OFFLOAD_ARCH", "gfx950")
 FLAGS = ["-O3", "-std=c++17", "-fPIC", "-ffp-contract=off", f"--offload-arch={ARCH}",

@@ -466,8 +466,9 @@ __global__ __launch_bounds__(NT) void k_bucket_sort(Dims d, GeomArena g) {
 void launch_depth_sort(const Dims& d, const GeomArena& g, hipStream_t s) {
     if (d.P == 0 || d.B == 0) return;
     if (d.NB <= kLdsBuckets) {  // every bucket has a claim slot (kClaims per thread)
-        // GSR_B1_COUNT_PER: Gaussians per thread of the single-frame count (2 or kCountPer)
-        static const int b1_per = tune_env("GSR_B1_COUNT_PER", kCountPer);
+        // GSR_B1_COUNT_PER: Gaussians per thread of the single-frame count, 2 (49 workgroups at 100k
+        // Gaussians: -5 us per frame against 8) or kCountPer (A/B)
+        static const int b1_per = tune_env("GSR_B1_COUNT_PER", 2);
         if (d.B == 1 && b1_per == 2) {
             const int per_wg = kCountThreads * 2;
             hipLaunchKernelGGL(k_bucket_count_lds<2>, dim3((d.P + per_wg - 1) / per_wg, d.B), dim3(kCountThreads),

@@ -222,12 +222,16 @@ class GaussianDeformer:
             raise RuntimeError(f"expected {self.V} vertices, got {V}")
         P = self.V + self.N
         dev = verts.device
-        o = dict(dtype=torch.float32, device=dev)
-        xyz = torch.empty((B, P, 3), **o)
-        rot = torch.empty((B, P, 4), **o)
-        scl = torch.empty((B, P, 3), **o)
-        verts = _f32(verts)
-        vt = _f32(vert_transforms)
+        # one allocation, three views; the rotations first (the kernel stores them as float4)
+        buf = torch.empty((B * P * 10,), dtype=torch.float32, device=dev)
+        rot = buf[:B * P * 4].view(B, P, 4)
+        xyz = buf[B * P * 4:B * P * 7].view(B, P, 3)
+        scl = buf[B * P * 7:].view(B, P, 3)
+        if verts.dtype is not torch.float32 or not verts.is_contiguous():
+            verts = _f32(verts)
+        vt = vert_transforms
+        if vt.dtype is not torch.float32 or not vt.is_contiguous():
+            vt = _f32(vt)
         rc = _lib.load().gsr_deform_gaussians(
             B, V, self.faces.shape[0], self.N, _ptr(verts), _ptr(vt), _ptr(self.faces),
             _ptr(self.v_rot), 0, _ptr(self.v_scale), 0, _ptr(self.bind), _ptr(self.bary),
@@ -332,17 +336,38 @@ class EHMDeformer:
         self.l_eyelid, self.r_eyelid = t(np.asarray(l_eyelid, np.float32)), t(np.asarray(r_eyelid, np.float32))
         self.bad = torch.zeros(1, dtype=torch.int32, device=dev)
         self._ws = {}
-        # the FLAME head chain and the body blend shapes are independent until the splice: the head
-        # runs on a side stream beside the body (GSR_EHM_OVERLAP=0: one stream, A/B)
-        self.overlap = os.environ.get("GSR_EHM_OVERLAP", "1") != "0"
-        self._side = {}
+        self._ehm = self._ehm_struct()
+        self._ehm_ref = ctypes.byref(self._ehm)
+        # GSR_EHM_ONECALL=0: the per-step C calls from Python (forward_calls), A/B
+        self.one_call = os.environ.get("GSR_EHM_ONECALL", "1") != "0"
 
-    def _side_stream(self, main):
-        """(side stream, fork event, join event) for a main stream, made once."""
-        key = main.cuda_stream
-        if key not in self._side:
-            self._side[key] = (torch.cuda.Stream(self.dev), torch.cuda.Event(), torch.cuda.Event())
-        return self._side[key]
+    def _ehm_struct(self):
+        """GsrEhm (include/gsr_deform.h) of this avatar, made once; the objects it points to are
+        attributes of self."""
+        def model(a, name):
+            m = _lib.EhmModel()
+            m.J, m.V = a["J_regressor"].shape
+            m.NB = a["shapedirs"].shape[2]
+            m.v_template, m.shapedirs_t = a["v_template"].data_ptr(), a["shapedirs_t"].data_ptr()
+            a["posedirs"] = _f32(a["posedirs"])
+            m.posedirs, m.J_regressor = a["posedirs"].data_ptr(), a["J_regressor"].data_ptr()
+            m.lbs_weights_t = a["lbs_weights_t"].data_ptr()
+            a["parents"] = np.ascontiguousarray(a["parents"], np.int32)
+            m.parents_host = a["parents"].ctypes.data
+            if name in self.sparse:
+                m.sparse = ctypes.pointer(self.sparse[name][0])
+            return m
+        for a in (self.body, self.flame):
+            for k in ("v_template", "J_regressor"):
+                a[k] = _f32(a[k])
+        e = _lib.Ehm()
+        e.flame, e.body = model(self.flame, "flame"), model(self.body, "body")
+        e.head_index, e.l_eyelid, e.r_eyelid = (x.data_ptr() for x in (self.head_index, self.l_eyelid, self.r_eyelid))
+        e.N_head = self.head_index.shape[0]
+        e.hj0, e.hj1 = self.HEAD_REF
+        e.bj0, e.bj1 = self.BODY_REF
+        e.bad_index_flag = self.bad.data_ptr()
+        return e
 
     def _workspace(self, B, V, J, NB):
         # one per stream: batches in flight on different streams must not share scratch
@@ -353,6 +378,56 @@ class EHMDeformer:
         return self._ws[key]
 
     def forward(self, body_param_dict, flame_param_dict):
+        """EHM.forward through gsr_ehm_forward: the parameter descriptors and one C call."""
+        if not self.one_call:
+            return self.forward_calls(body_param_dict, flame_param_dict)
+        bp, fp = body_param_dict, flame_param_dict
+        if bp.get("hand_scale") is not None:
+            raise NotImplementedError("hand_scale (EHM.py:126-132) needs the MANO vertex map, not bundled")
+        B = fp["shape_params"].shape[0]
+        prm = (_lib.EhmParam * 13)()
+        keep = []
+        for i, t in enumerate((fp["shape_params"], fp["expression_params"], fp.get("jaw_params"),
+                               fp.get("eye_pose_params"), fp.get("eyelid_params"), bp["shape"], bp["exp"],
+                               bp.get("global_pose"), bp.get("body_pose"), bp["left_hand_pose"],
+                               bp["right_hand_pose"], bp.get("head_scale"), bp.get("joints_offset"))):
+            if t is None:
+                continue
+            if t.dtype is not torch.float32 or not t.is_contiguous():
+                t = _f32(t)
+                keep.append(t)
+            if not t.is_cuda:
+                raise RuntimeError("guava_renderer_amd.deform runs on the GPU only (got a CPU tensor)")
+            rows = t.shape[0] if t.dim() > 1 else 1  # 1-D: one row for every frame
+            if rows != 1 and rows != B:
+                raise RuntimeError(f"parameter batch {rows} does not match the frame batch {B}")
+            q = prm[i]
+            q.p = t.data_ptr()
+            q.width = t.numel() // rows if rows else 0
+            q.row_stride = q.width if rows > 1 else 0
+        Vb, Jb = self._ehm.body.V, self._ehm.body.J
+        n3, n16 = B * Vb * 3, B * Vb * 16
+        j3, j16 = B * Jb * 3, B * Jb * 16
+        # one allocation for the five outputs; the 4x4 transforms first (stored as float4)
+        buf = torch.empty((n16 + j16 + n3 + 2 * j3,), dtype=torch.float32, device=self.dev)
+        T = buf[:n16].view(B, Vb, 4, 4)
+        A = buf[n16:n16 + j16].view(B, Jb, 4, 4)
+        o = n16 + j16
+        verts, J, jt2 = buf[o:o + n3].view(B, Vb, 3), buf[o + n3:o + n3 + j3].view(B, Jb, 3), buf[o + n3 + j3:].view(B, Jb, 3)
+        out = _lib.EhmOutputs(verts.data_ptr(), J.data_ptr(), jt2.data_ptr(), T.data_ptr(), A.data_ptr())
+        st = torch.cuda.current_stream(self.dev).cuda_stream
+        ws = self._ws.get((B, st))
+        if ws is None:
+            n = _lib.load().gsr_ehm_workspace_bytes(self._ehm_ref, B)
+            ws = self._ws[(B, st)] = torch.empty((n,), dtype=torch.uint8, device=self.dev)
+        _lib.check(_lib.load().gsr_ehm_forward(self._ehm_ref, B, prm, ctypes.byref(out), ws.data_ptr(), st),
+                   "gsr_ehm_forward")
+        return {"vertices": verts, "joints": J, "joints_transform": jt2, "ver_transform_mat": T,
+                "joint_transform_mat": A}
+
+    def forward_calls(self, body_param_dict, flame_param_dict):
+        """EHM.forward as Python-issued C calls per step (gsr_pack_rows, gsr_lbs_sp, gsr_blend_joints_sp,
+        gsr_splice_head, gsr_lbs_sp): the same kernels and results as forward()."""
         L = _lib.load()
         st = _stream(self.dev)
         bp, fp = body_param_dict, flame_param_dict
@@ -391,25 +466,16 @@ class EHMDeformer:
             _seg(segs, hsb, 0, hs, B)
         table = _fill_zeros(segs, views, B)
         _lib.check(L.gsr_pack_rows(B, len(table), (_lib.RowSegment * len(table))(*table), st), "gsr_pack_rows")
-        # FLAME head (EHM.py:41-75), on the side stream when overlapping: every buffer it touches is
-        # allocated on the main stream and the main stream joins it before the splice reads them
+        # FLAME head (EHM.py:41-75)
         hv = torch.empty((B, Vh, 3), **o)
         hj = torch.empty((B, Jh, 3), **o)
         sph = ctypes.byref(self.sparse["flame"][0]) if "flame" in self.sparse else None
         spb = ctypes.byref(self.sparse["body"][0]) if "body" in self.sparse else None
-        ws_h = self._workspace(B, Vh, Jh, NBh)
-        hst = st
-        if self.overlap:
-            main = torch.cuda.current_stream(self.dev)
-            side, fork, join = self._side_stream(main)
-            fork.record(main)
-            side.wait_event(fork)
-            hst = ctypes.c_void_p(side.cuda_stream)
         rc = L.gsr_lbs_sp(B, Vh, Jh, NBh, _ptr(fa["v_template"]), 0, _ptr(betas_h),
                           _ptr(fa["shapedirs_t"]), _ptr(pose_h), 1, _ptr(fa["posedirs"]),
                           _ptr(fa["J_regressor"]), fa["parents"].ctypes.data_as(ctypes.c_void_p),
                           _ptr(fa["lbs_weights_t"]), None, _ptr(hv), _ptr(hj), None, None, None, None,
-                          _ptr(ws_h), sph, hst)
+                          _ptr(self._workspace(B, Vh, Jh, NBh)), sph, st)
         _lib.check(rc, "gsr_lbs (FLAME head)")
         # body template (EHM.py:101-118): blend shapes of shape ++ exp, regressed joints + offset
         joff = _f32(bp["joints_offset"]) if bp.get("joints_offset") is not None else None
@@ -418,9 +484,6 @@ class EHMDeformer:
         _lib.check(L.gsr_blend_joints_sp(B, Vb, Jb, NBb, _ptr(ba["v_template"]), 0, _ptr(sc),
                                          _ptr(ba["shapedirs_t"]), _ptr(ba["J_regressor"]), _ptr(joff),
                                          _ptr(vt), _ptr(tj), spb, st), "gsr_blend_joints")
-        if self.overlap:
-            join.record(side)
-            main.wait_event(join)
         # head splice (EHM.py:72-75, 121-124)
         eyelid = _f32(fp["eyelid_params"]) if fp.get("eyelid_params") is not None else None
         _lib.check(L.gsr_splice_head(B, Vb, Vh, _ptr(self.head_index), _ptr(hv), _ptr(self.r_eyelid),

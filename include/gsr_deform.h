@@ -181,6 +181,72 @@ typedef struct {
  * width <= 4096; segments must not overlap. */
 int gsr_pack_rows(int B, int nseg, const GsrRowSegment* segs, void* stream);
 
+/* EHM.forward (modules/ehm/EHM.py:36-156) for B frames in ONE host call: the coefficient-row glue
+ * (:41-48, :94-112, one pack launch), the FLAME head lbs (:67-70), the body template's blend shapes
+ * and joints (:114-118), the head splice with eyelids and head scale (:72-75, :121-124) and the body
+ * lbs_wobeta (:134-137) -- the same kernels as gsr_pack_rows + gsr_lbs_sp + gsr_blend_joints_sp +
+ * gsr_splice_head + gsr_lbs_sp, issued from C so a single-frame call pays one FFI crossing instead of
+ * five plus the host-side table building (the per-frame drop-in loop is host-bound there).
+ *
+ * One LBS model (GsrEhmModel): the assets of gsr_lbs_sp in its layouts; NB = the blend's shape
+ * coefficients (FLAME: shape + expression (+ zero padding); SMPL-X: shape + expression). */
+typedef struct {
+    int32_t V, J, NB, pad_;
+    const float* v_template;      /* [V,3] */
+    const float* shapedirs_t;     /* [NB, 3V] */
+    const float* posedirs;        /* [9(J-1), 3V] */
+    const float* J_regressor;     /* [J, V] */
+    const float* lbs_weights_t;   /* [J, V] */
+    const int32_t* parents_host;  /* HOST [J] */
+    const GsrLbsSparse* sparse;   /* or NULL */
+} GsrEhmModel;
+typedef struct {
+    GsrEhmModel flame, body;
+    const int32_t* head_index;    /* [N_head] smplx2flame_ind: body vertex of each FLAME vertex */
+    const float* l_eyelid;        /* [N_head,3] */
+    const float* r_eyelid;        /* [N_head,3] */
+    int32_t N_head;               /* = flame.V */
+    int32_t hj0, hj1, bj0, bj1;   /* splice reference joints (EHM: head [3,5), body [23,25)) */
+    int32_t pad_;
+    uint32_t* bad_index_flag;     /* device, ORed with 2 on an out-of-range head_index (or NULL) */
+} GsrEhm;
+/* One per-frame parameter: rows of `width` floats, row b at p + b * row_stride (row_stride 0: one
+ * row for every frame); p == NULL: absent (its columns stay zero, as the reference's zeros). */
+typedef struct {
+    const float* p;
+    int64_t row_stride;
+    int32_t width, pad_;
+} GsrEhmParam;
+/* The parameters' slots in the `params` array (the reference's dict keys):
+ * flame_param_dict shape_params, expression_params, jaw_params, eye_pose_params, eyelid_params;
+ * body_param_dict shape, exp, global_pose, body_pose, left_hand_pose, right_hand_pose, head_scale,
+ * joints_offset. */
+enum {
+    GSR_EHM_FLAME_SHAPE = 0, GSR_EHM_FLAME_EXPR, GSR_EHM_FLAME_JAW, GSR_EHM_FLAME_EYES, GSR_EHM_FLAME_EYELID,
+    GSR_EHM_BODY_SHAPE, GSR_EHM_BODY_EXP, GSR_EHM_BODY_GLOBAL, GSR_EHM_BODY_POSE, GSR_EHM_BODY_LHAND,
+    GSR_EHM_BODY_RHAND, GSR_EHM_BODY_HEAD_SCALE, GSR_EHM_BODY_JOINTS_OFFSET, GSR_EHM_NPARAM
+};
+/* EHM.forward's output dict; every pointer but vertices may be NULL. */
+typedef struct {
+    float* vertices;              /* [B,Vb,3] */
+    float* joints;                /* [B,Jb,3] rest joints incl. offset */
+    float* joints_transform;      /* [B,Jb,3] posed joints */
+    float* ver_transform_mat;     /* [B,Vb,16] */
+    float* joint_transform_mat;   /* [B,Jb,16] */
+} GsrEhmOutputs;
+/* Scratch bytes of gsr_ehm_forward for B frames (coefficient rows, the head's vertices and joints,
+ * the body template and joints, and both lbs workspaces). */
+size_t gsr_ehm_workspace_bytes(const GsrEhm* ehm, int B);
+/* Column layout (EHM.py): FLAME betas = shape ++ expression ++ zeros (flame.NB wide); FLAME pose =
+ * 0 global, 0 neck, jaw at column 6, eyes at 9 (3 * flame.J wide); body betas = shape (cut to
+ * body.NB - exp width, as the reference slices it) ++ zeros ++ exp at body.NB - exp width; body pose
+ * = global_pose (its first 3 columns) at 0, body_pose (first 63) at 3, zero jaw and eyes, left hand
+ * at 75, right hand at 120 (3 * body.J wide).  eyelid_params must be 2 wide, head_scale 3,
+ * joints_offset 3 * body.J.  A parameter that does not fit its columns is refused (GSR_ERR_ARG)
+ * before any launch. */
+int gsr_ehm_forward(const GsrEhm* ehm, int B, const GsrEhmParam* params, const GsrEhmOutputs* out,
+                    char* workspace, void* stream);
+
 /* Ubody_Gaussian.forward's Gaussian assembly for B frames; P = V + N Gaussians per frame, the V
  * vertex Gaussians first.
  *   verts [B,V,3], vert_transforms [B,V,16] (from gsr_lbs), faces [F,3] int32.

@@ -183,9 +183,61 @@ def test_deform_abi_validates_before_touching_memory():
                           torch.zeros(3, 4), torch.tensor([-1, 0, 1]), torch.zeros(4, 3))
 
 
+def _ehm_struct(Vh=5023, Jh=5, NBh=400, Vb=10595, Jb=55, NBb=310):
+    import ctypes
+    from guava_renderer_amd import _lib
+    bogus = 256
+    par_h = (ctypes.c_int32 * Jh)(*([-1] + [0] * (Jh - 1)))
+    par_b = (ctypes.c_int32 * Jb)(*([-1] + list(range(Jb - 1))))
+    e = _lib.Ehm()
+    for m, (V, J, NB, par) in ((e.flame, (Vh, Jh, NBh, par_h)), (e.body, (Vb, Jb, NBb, par_b))):
+        m.V, m.J, m.NB = V, J, NB
+        m.v_template = m.shapedirs_t = m.posedirs = m.J_regressor = m.lbs_weights_t = bogus
+        m.parents_host = ctypes.cast(par, ctypes.c_void_p).value
+    e.head_index = e.l_eyelid = e.r_eyelid = bogus
+    e.N_head, e.hj0, e.hj1, e.bj0, e.bj1 = Vh, 3, 5, 23, 25
+    return e, (par_h, par_b)
+
+
+def test_ehm_abi_sizes_and_validation():
+    """gsr_ehm_forward (include/gsr_deform.h): the workspace holds both lbs workspaces plus the
+    coefficient rows and intermediates, and the parameter checks fail on the host before any launch
+    (the pointers here are never dereferenced)."""
+    import ctypes
+    from guava_renderer_amd import _lib
+    L = _lib.load()
+    e, keep = _ehm_struct()
+    B = 3
+    ws = L.gsr_ehm_workspace_bytes(ctypes.byref(e), B)
+    assert ws >= L.gsr_lbs_workspace_bytes(B, 5023, 5, 400) + L.gsr_lbs_workspace_bytes(B, 10595, 55, 0) + \
+        4 * B * (10595 * 3 + 5023 * 3 + 400 + 310 + 3 * 5 + 3 * 55)
+    assert L.gsr_ehm_workspace_bytes(ctypes.byref(e), 2 * B) > ws
+    prm = (_lib.EhmParam * 13)()
+    out = _lib.EhmOutputs(256, None, None, None, None)
+
+    def call():
+        return L.gsr_ehm_forward(ctypes.byref(e), B, prm, ctypes.byref(out), 256, None)
+    assert call() == -1 and b"required" in L.gsr_last_error()
+    for i, w in ((0, 300), (1, 100), (5, 300), (6, 10), (9, 45), (10, 45)):
+        prm[i].p, prm[i].width, prm[i].row_stride = 256, w, w
+    prm[11].p, prm[11].width, prm[11].row_stride = 256, 4, 4  # head_scale must be 3 wide
+    assert call() == -1 and b"head_scale 3" in L.gsr_last_error()
+    prm[11].width = prm[11].row_stride = 3
+    prm[1].width = prm[1].row_stride = 101  # shape 300 + expression 101 > FLAME NB 400
+    assert call() == -1 and b"FLAME betas" in L.gsr_last_error()
+    prm[1].width = prm[1].row_stride = 100
+    prm[2].p, prm[2].width, prm[2].row_stride = 256, 3, 2  # row stride below the width
+    assert call() == -1 and b"row stride" in L.gsr_last_error()
+    prm[2].row_stride = 3
+    prm[8].p, prm[8].width, prm[8].row_stride = 256, 60, 60  # body_pose needs 63 columns
+    assert call() == -1 and b"body_pose 63" in L.gsr_last_error()
+    e.N_head = 7
+    assert call() == -1 and b"N_head" in L.gsr_last_error()
+
+
 def test_ctypes_structs_match_the_c_layout(tmp_path):
     """The ctypes mirrors of the C ABI's structs (_lib.DeformInputs / Scratch / LbsSparse /
-    RowSegment) have the C compiler's size and field offsets (include/gsr*.h, x86-64)."""
+    RowSegment / the GsrEhm* set) have the C compiler's size and field offsets (include/gsr*.h, x86-64)."""
     import shutil
     import subprocess
     from guava_renderer_amd import _lib
@@ -193,7 +245,9 @@ def test_ctypes_structs_match_the_c_layout(tmp_path):
         pytest.skip("no gcc")
     inc = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "include")
     structs = {"GsrDeformInputs": _lib.DeformInputs, "gsr_scratch": _lib.Scratch, "GsrLbsSparse": _lib.LbsSparse,
-               "GsrRowSegment": _lib.RowSegment, "gsr_refine_epilogue": _lib.RefineEpilogue}
+               "GsrRowSegment": _lib.RowSegment, "gsr_refine_epilogue": _lib.RefineEpilogue,
+               "GsrEhmModel": _lib.EhmModel, "GsrEhm": _lib.Ehm, "GsrEhmParam": _lib.EhmParam,
+               "GsrEhmOutputs": _lib.EhmOutputs}
     lines = ['#include <stddef.h>', '#include <stdio.h>', '#include "gsr.h"', '#include "gsr_deform.h"',
              "int main(void) {"]
     for cname, py in structs.items():

@@ -239,6 +239,30 @@ def test_ehm_sparse_assets_match_dense(monkeypatch):
             np.testing.assert_allclose(outs["1"][k], ref[k], atol=ATOL, rtol=0, err_msg=k)
 
 
+def test_ehm_one_call_equals_per_step_calls():
+    """gsr_ehm_forward (one C call, table built in C) against the same steps issued from Python
+    (EHMDeformer.forward_calls): the same kernels, so bit-identical outputs -- at B = 1 (the per-frame
+    drop-in) and B = 5 with a broadcast head_scale and joints_offset (expanded in the workspace)."""
+    from guava_renderer_amd import avatar, deform
+    body, flame, extra = avatar.ehm_assets(seed=0)
+    ehm = deform.EHMDeformer(body, flame, extra["smplx2flame_ind"], extra["l_eyelid"], extra["r_eyelid"],
+                             device=DEV)
+    assert ehm.one_call
+    for B in (1, 5):
+        bp, fp = avatar.ehm_params(B, seed=7000 + B)
+        gbp = {k: _t(v) for k, v in bp.items()}
+        gfp = {k: _t(v) for k, v in fp.items()}
+        if B > 1:
+            gbp["head_scale"] = _t(bp["head_scale"][:1])
+            gbp["joints_offset"] = _t(np.random.default_rng(B).normal(0, 0.01, (1, 55, 3)).astype(np.float32))
+        one = {k: v.cpu().numpy() for k, v in ehm.forward(gbp, gfp).items()}
+        if B > 1:  # the per-step path wants joints_offset per frame
+            gbp["joints_offset"] = gbp["joints_offset"].expand(B, -1, -1).contiguous()
+        steps = {k: v.cpu().numpy() for k, v in ehm.forward_calls(gbp, gfp).items()}
+        for k in ("vertices", "joints", "joints_transform", "ver_transform_mat", "joint_transform_mat"):
+            np.testing.assert_array_equal(one[k], steps[k], err_msg=f"B={B} {k}")
+
+
 def test_ehm_forward_large_batch_matrix_core_blend():
     """B=40 frames: the blend shapes run on the matrix-core kernel (k_lbs_blend_mfma, more than 16
     frames), one full 32-frame tile and one partial tile; V*3 = 31,425 is not a multiple of the
