@@ -292,7 +292,10 @@ static int forward_single(gsr_alloc_fn geometryBuffer, gsr_alloc_fn binningBuffe
     in.prefiltered = prefiltered; in.antialiasing = antialiasing;
     Outputs o{out_color, depth, radii, g_render_counters, g_timeline, g_timeline_cap};
 
-    HIP_TRY(hipMemsetAsync(g.ctrl, 0, ctrl_words(d) * 4, s));
+    // the control words are zeroed by the first kernel (zero_ctrl_words), except for a prefiltered
+    // forward (its culling-error word is set during that kernel) or an empty one (no kernel)
+    in.zero_ctrl = !in.prefiltered && d.P > 0 && d.B > 0;
+    if (!in.zero_ctrl) HIP_TRY(hipMemsetAsync(g.ctrl, 0, ctrl_words(d) * 4, s));
     { StageTimer st_(0, s); launch_preprocess(d, in, g, o, s); }
     STAGE(debug, s, "preprocess");
     if (status_host) {
@@ -570,7 +573,10 @@ static int forward_batch_impl(int B, int P, int width, int height, const float* 
         o.keep = refine->keep_channels;
         o.slope = refine->negative_slope;
     }
-    HIP_TRY(hipMemsetAsync(g.ctrl, 0, ctrl_words(d) * 4, s));
+    // the control words are zeroed by the first kernel (zero_ctrl_words), except for a prefiltered
+    // forward (its culling-error word is set during that kernel) or an empty one (no kernel)
+    in.zero_ctrl = !in.prefiltered && d.P > 0 && d.B > 0;
+    if (!in.zero_ctrl) HIP_TRY(hipMemsetAsync(g.ctrl, 0, ctrl_words(d) * 4, s));
     if (dg) {
         in.fwd_only = 1;  // (the deformed attributes are not kept: no backward can use the workspace)
         StageTimer st_(0, s);

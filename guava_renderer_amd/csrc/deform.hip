@@ -32,6 +32,7 @@
 
 #include "../../include/gsr.h"
 #include "../../include/gsr_deform.h"
+#include "deform_internal.h"
 #include "gsr_internal.h"
 #include "preprocess_dev.h"
 
@@ -650,19 +651,58 @@ __global__ __launch_bounds__(256) void k_lbs_joints_csr(int B, int V, int J, con
 // tree (16 threads per joint, one matrix element each): every joint of a level in one step, so
 // SMPL-X's 54 sequential products become its tree depth (~10) barrier steps -- each product is
 // the same expression as the sequential chain's, so the results are identical.
-// rot == null: each joint's rotation from the pose (rodrigues_one), as the single-frame path does
+// rot == null: each joint's rotation from the pose (rodrigues_one), as the single-frame path does.
+// jrow != null (single frame, CSR regressor): the rest joints are regressed here first -- each of the
+// 16 waves takes joints w, w + 16, ... with k_lbs_joints_csr's per-lane chains and xor tree (the same
+// sums, bit for bit) -- and written to `joints`, one launch fewer per lbs call.
+struct ChainJoints {
+    const int32_t* row;
+    const int32_t* col;
+    const float* val;
+    const float* vs;    // v_shaped of the frame
+    const float* joff;  // or null
+};
 __global__ __launch_bounds__(16 * GSR_LBS_MAX_JOINTS) void k_lbs_chain(int J, Parents par,
                                                                      const float* __restrict__ rot,
-                                                                     const float* __restrict__ joints,
+                                                                     float* __restrict__ joints,
                                                                      float* __restrict__ jtrans,
                                                                      float* __restrict__ A,
-                                                                     const float* __restrict__ pose, int pose2rot) {
+                                                                     const float* __restrict__ pose, int pose2rot,
+                                                                     ChainJoints cj) {
     __shared__ float tm[GSR_LBS_MAX_JOINTS][16];
     __shared__ float ch[GSR_LBS_MAX_JOINTS][16];
     __shared__ int depth[GSR_LBS_MAX_JOINTS];
+    __shared__ float sjt[GSR_LBS_MAX_JOINTS * 3];
     __shared__ int maxd;
     const int b = blockIdx.x, t = threadIdx.x;
     const float* Jb = joints + (int64_t)b * J * 3;
+    if (cj.row) {
+        const int w = t >> 6, lane = t & 63;
+        for (int j = w; j < J; j += 16) {
+            float x = 0.f, y = 0.f, z = 0.f;
+            for (int k = cj.row[j] + lane; k < cj.row[j + 1]; k += 64) {
+                const int v = cj.col[k];
+                const float wv = cj.val[k];
+                x = fmaf(wv, cj.vs[3 * v], x);
+                y = fmaf(wv, cj.vs[3 * v + 1], y);
+                z = fmaf(wv, cj.vs[3 * v + 2], z);
+            }
+#pragma unroll
+            for (int off = 32; off > 0; off >>= 1) {
+                x += __shfl_xor(x, off);
+                y += __shfl_xor(y, off);
+                z += __shfl_xor(z, off);
+            }
+            if (lane < 3) {
+                float v = lane == 0 ? x : lane == 1 ? y : z;
+                if (cj.joff) v = v + cj.joff[j * 3 + lane];
+                sjt[3 * j + lane] = v;
+                joints[j * 3 + lane] = v;
+            }
+        }
+        __syncthreads();
+        Jb = sjt;
+    }
     if (t == 0) maxd = 0;
     if (t < J) {
         float R[9];
@@ -1114,7 +1154,7 @@ __global__ __launch_bounds__(256) void k_deform_preprocess(int fpw, GsrDeformInp
         }
         preprocess_block_sums(d, g, b, blockIdx.x, tiles, gid);
     }
-    if (threadIdx.x == 0 && blockIdx.x == 0 && blockIdx.y == 0) g.ctrl[kCtrlFwdOnly] = 1u;
+    zero_ctrl_words(d, in, g);  // (in.fwd_only is set: no backward reads this workspace)
 }
 
 void launch_deform_preprocess(const Dims& d, const Inputs& in, const GeomArena& g, const Outputs& o,
@@ -1255,10 +1295,26 @@ int gsr_lbs_sp(int B, int V, int J, int NB, const float* v_template, int64_t v_t
                float* joints_transformed, float* joints, float* vert_transforms,
                float* joint_transforms, float* v_shaped, char* workspace, const GsrLbsSparse* sp,
                void* stream) {
+    return gsr::lbs_run(B, V, J, NB, v_template, v_template_stride, betas, shapedirs_t, pose, pose2rot, posedirs,
+                        J_regressor, parents_host, lbs_weights_t, joints_offset, verts, joints_transformed, joints,
+                        vert_transforms, joint_transforms, v_shaped, workspace, sp, stream, true);
+}
+
+}  // extern "C"
+
+// gsr_lbs_sp, or (skin = false) everything up to the skinning: the joint transforms A and v_posed stay
+// in the workspace (lbs_skin_splice reads them)
+int gsr::lbs_run(int B, int V, int J, int NB, const float* v_template, int64_t v_template_stride,
+                 const float* betas, const float* shapedirs_t, const float* pose, int pose2rot,
+                 const float* posedirs, const float* J_regressor, const int32_t* parents_host,
+                 const float* lbs_weights_t, const float* joints_offset, float* verts,
+                 float* joints_transformed, float* joints, float* vert_transforms,
+                 float* joint_transforms, float* v_shaped, char* workspace, const GsrLbsSparse* sp,
+                 void* stream, bool skin) {
     if (B <= 0 || V <= 0) return api_fail(GSR_ERR_ARG, "gsr_lbs: B and V must be positive");
     if (int rc = check_sparse(sp, J, betas ? NB : 0, V, "gsr_lbs")) return rc;
     if (J < 1 || J > GSR_LBS_MAX_JOINTS) return api_fail(GSR_ERR_ARG, "gsr_lbs: J must be in [1, 64]");
-    if (!v_template || !pose || !J_regressor || !parents_host || !lbs_weights_t || !verts || !workspace)
+    if (!v_template || !pose || !J_regressor || !parents_host || !lbs_weights_t || (skin && !verts) || !workspace)
         return api_fail(GSR_ERR_ARG, "gsr_lbs: null required pointer");
     if (J > 1 && !posedirs) return api_fail(GSR_ERR_ARG, "gsr_lbs: posedirs is null");
     if (v_template_stride != 0 && v_template_stride != (int64_t)V * 3)
@@ -1297,11 +1353,20 @@ int gsr_lbs_sp(int B, int V, int J, int NB, const float* v_template, int64_t v_t
     launch_blend(B, M, NB, NP, v_template, v_template_stride, betas, shapedirs_t, a.feat, posedirs, vs, a.vp, s, sp,
                  fused ? pose : nullptr, pose2rot);
     if (int rc = hip_check("lbs_blend")) return rc;
-    launch_joints(B, V, J, J_regressor, sp, vs, joints_offset, jr, s);
-    if (int rc = hip_check("lbs_joints")) return rc;
+    // single frame with the CSR regressor: the joints are regressed inside the chain's workgroup
+    // (GSR_CHAIN_JOINTS=0: their own launch, A/B)
+    static const bool chain_joints_on = tune_env("GSR_CHAIN_JOINTS", 1) != 0;
+    ChainJoints cj{nullptr, nullptr, nullptr, nullptr, nullptr};
+    if (B == 1 && sp && sp->jreg_row && chain_joints_on) {
+        cj = ChainJoints{sp->jreg_row, sp->jreg_col, sp->jreg_val, vs, joints_offset};
+    } else {
+        launch_joints(B, V, J, J_regressor, sp, vs, joints_offset, jr, s);
+        if (int rc = hip_check("lbs_joints")) return rc;
+    }
     hipLaunchKernelGGL(k_lbs_chain, dim3(B), dim3(16 * GSR_LBS_MAX_JOINTS), 0, s, J, par, fused ? nullptr : a.rot,
-                       jr, joints_transformed, A, pose, pose2rot);
+                       jr, joints_transformed, A, pose, pose2rot, cj);
     if (int rc = hip_check("lbs_chain")) return rc;
+    if (!skin) return 0;
     if (sp && sp->skin_k > 0) {
         const dim3 g((V + 255) / 256, B);
         if (sp->skin_k <= 4)
@@ -1319,6 +1384,97 @@ int gsr_lbs_sp(int B, int V, int J, int NB, const float* v_template, int64_t v_t
     }
     return hip_check("lbs_skin");
 }
+
+// The FLAME head's skinning fused into the splice (EHM.py:67-75, :121-124): per head vertex, the ELL
+// skinning of k_lbs_skin_ell (the same fmaf chains and vertex expression, so the same head vertex),
+// then k_splice_head's eyelids, head scale and re-anchoring, written straight into the body template:
+// the head vertices never reach memory and one launch goes.
+template <int KMAX>
+__global__ __launch_bounds__(256) void k_skin_splice(int Vh, int Jh, int K, const int32_t* __restrict__ sj,
+                                                     const float* __restrict__ sw, const float* __restrict__ A,
+                                                     const float* __restrict__ v_posed, int Vb,
+                                                     const int32_t* __restrict__ idx,
+                                                     const float* __restrict__ r_eyelid,
+                                                     const float* __restrict__ l_eyelid,
+                                                     const float* __restrict__ eyelid,
+                                                     const float* __restrict__ head_scale,
+                                                     const float* __restrict__ hjoints, int hj0, int hj1,
+                                                     const float* __restrict__ bjoints, int Jb, int bj0, int bj1,
+                                                     float* __restrict__ body, uint32_t* __restrict__ bad) {
+    __shared__ float As[GSR_LBS_MAX_JOINTS * 16];
+    const int b = blockIdx.y;
+    for (int i = threadIdx.x; i < Jh * 16; i += blockDim.x) As[i] = A[(int64_t)b * Jh * 16 + i];
+    __syncthreads();
+    const int v = blockIdx.x * blockDim.x + threadIdx.x;
+    if (v >= Vh) return;
+    const int d = idx[v];
+    if (d < 0 || d >= Vb) {
+        if (bad) atomicOr(bad, 2u);
+        return;
+    }
+    int jj[KMAX];
+    float ww[KMAX];
+#pragma unroll
+    for (int u = 0; u < KMAX; u++) {
+        jj[u] = u < K ? min((int)sj[(int64_t)u * Vh + v], Jh - 1) : 0;
+        ww[u] = u < K ? sw[(int64_t)u * Vh + v] : 0.f;
+    }
+    float T[16];
+#pragma unroll
+    for (int e = 0; e < 16; e++) T[e] = 0.f;
+#pragma unroll
+    for (int u = 0; u < KMAX; u++) {
+        if (u >= K) break;
+        const float* Aj = As + 16 * jj[u];
+#pragma unroll
+        for (int e = 0; e < 16; e++) T[e] = fmaf(ww[u], Aj[e], T[e]);
+    }
+    const float* vp = v_posed + ((int64_t)b * Vh + v) * 3;
+    const float px = vp[0], py = vp[1], pz = vp[2];
+    const float* hjb = hjoints + (int64_t)b * Jh * 3;
+    const float* bjt = bjoints + (int64_t)b * Jb * 3;
+#pragma unroll
+    for (int c = 0; c < 3; c++) {
+        float h = T[4 * c] * px + T[4 * c + 1] * py + T[4 * c + 2] * pz + T[4 * c + 3] * 1.0f;
+        if (eyelid) {
+            h = h + r_eyelid[3 * v + c] * eyelid[2 * b + 1];
+            h = h + l_eyelid[3 * v + c] * eyelid[2 * b];
+        }
+        if (head_scale) h = h * head_scale[3 * b + c];
+        float hs = 0.f, bs = 0.f;
+        for (int j = hj0; j < hj1; j++) hs += hjb[3 * j + c];
+        for (int j = bj0; j < bj1; j++) bs += bjt[3 * j + c];
+        body[((int64_t)b * Vb + d) * 3 + c] = (h - hs / (float)(hj1 - hj0)) + bs / (float)(bj1 - bj0);
+    }
+}
+
+// the launch for gsr_ehm_forward: A and v_posed from the head's lbs workspace (lbs_run(skin = false));
+// returns 1 (nothing launched) when the head has no ELL skinning weights
+int gsr::lbs_skin_splice(int B, int Vh, int Jh, const GsrLbsSparse* sp_h, const char* ws_h, int Vb,
+                         const int32_t* head_index, const float* r_eyelid, const float* l_eyelid,
+                         const float* eyelid, const float* head_scale, const float* head_joints, int hj0, int hj1,
+                         const float* body_joints, int Jb, int bj0, int bj1, float* body_v_shaped,
+                         uint32_t* bad_index_flag, void* stream) {
+    if (!sp_h || sp_h->skin_k <= 0) return 1;
+    if (hj0 < 0 || hj1 <= hj0 || hj1 > Jh || bj0 < 0 || bj1 <= bj0 || bj1 > Jb)
+        return api_fail(GSR_ERR_ARG, "gsr_ehm_forward: bad reference joint ranges");
+    if (eyelid && (!r_eyelid || !l_eyelid)) return api_fail(GSR_ERR_ARG, "gsr_ehm_forward: eyelid bases missing");
+    LbsArena a;
+    carve_lbs(const_cast<char*>(ws_h), B, Vh, Jh, &a);
+    const dim3 g((Vh + 255) / 256, B);
+    hipStream_t s = (hipStream_t)stream;
+#define GSR_SKS(KM)                                                                                              \
+    hipLaunchKernelGGL(k_skin_splice<KM>, g, dim3(256), 0, s, Vh, Jh, sp_h->skin_k, sp_h->skin_joint,            \
+                       sp_h->skin_weight, a.A, a.vp, Vb, head_index, r_eyelid, l_eyelid, eyelid, head_scale,     \
+                       head_joints, hj0, hj1, body_joints, Jb, bj0, bj1, body_v_shaped, bad_index_flag)
+    if (sp_h->skin_k <= 4) GSR_SKS(4);
+    else if (sp_h->skin_k <= 8) GSR_SKS(8);
+    else GSR_SKS(16);
+#undef GSR_SKS
+    return hip_check("skin_splice");
+}
+
+extern "C" {
 
 int gsr_blend_joints(int B, int V, int J, int NB, const float* v_template, int64_t v_template_stride,
                      const float* betas, const float* shapedirs_t, const float* J_regressor,

@@ -15,6 +15,7 @@
 
 #include "../../include/gsr.h"
 #include "../../include/gsr_deform.h"
+#include "deform_internal.h"
 #include "gsr_internal.h"
 
 namespace gsr {
@@ -200,18 +201,25 @@ int gsr_ehm_forward(const GsrEhm* ehm, int B, const GsrEhmParam* params, const G
     if (hipError_t err = hipGetLastError(); err != hipSuccess)
         return api_fail(GSR_ERR_HIP, (std::string("ehm_pack: ") + hipGetErrorString(err)).c_str());
 
-    // FLAME head lbs (EHM.py:67-70): head vertices and posed joints
-    int rc = gsr_lbs_sp(B, Vh, Jh, NBh, e.flame.v_template, 0, a.betas_h, e.flame.shapedirs_t, a.pose_h, 1,
-                        e.flame.posedirs, e.flame.J_regressor, e.flame.parents_host, e.flame.lbs_weights_t, nullptr,
-                        a.hv, a.hj, nullptr, nullptr, nullptr, nullptr, a.ws_h, e.flame.sparse, stream);
+    // FLAME head lbs (EHM.py:67-70): posed joints, and the head vertices unless the skinning is fused
+    // into the splice below (ELL weights; GSR_EHM_SKIN_SPLICE=0: separate, A/B)
+    static const bool skin_splice_on = tune_env("GSR_EHM_SKIN_SPLICE", 1) != 0;
+    const bool fuse = skin_splice_on && e.flame.sparse && e.flame.sparse->skin_k > 0;
+    int rc = lbs_run(B, Vh, Jh, NBh, e.flame.v_template, 0, a.betas_h, e.flame.shapedirs_t, a.pose_h, 1,
+                     e.flame.posedirs, e.flame.J_regressor, e.flame.parents_host, e.flame.lbs_weights_t, nullptr,
+                     a.hv, a.hj, nullptr, nullptr, nullptr, nullptr, a.ws_h, e.flame.sparse, stream, !fuse);
     if (rc) return rc;
     // body template: blend shapes + joints (+ offset) (EHM.py:114-118)
     rc = gsr_blend_joints_sp(B, Vb, Jb, NBb, e.body.v_template, 0, a.betas_b, e.body.shapedirs_t, e.body.J_regressor,
                              joff, a.vt, a.tj, e.body.sparse, stream);
     if (rc) return rc;
     // head splice (EHM.py:72-75, :121-124)
-    rc = gsr_splice_head(B, Vb, Vh, e.head_index, a.hv, e.r_eyelid, e.l_eyelid, eyelid, hscale, a.hj, Jh, e.hj0,
-                         e.hj1, a.tj, Jb, e.bj0, e.bj1, a.vt, e.bad_index_flag, stream);
+    if (fuse)
+        rc = lbs_skin_splice(B, Vh, Jh, e.flame.sparse, a.ws_h, Vb, e.head_index, e.r_eyelid, e.l_eyelid, eyelid,
+                             hscale, a.hj, e.hj0, e.hj1, a.tj, Jb, e.bj0, e.bj1, a.vt, e.bad_index_flag, stream);
+    else
+        rc = gsr_splice_head(B, Vb, Vh, e.head_index, a.hv, e.r_eyelid, e.l_eyelid, eyelid, hscale, a.hj, Jh, e.hj0,
+                             e.hj1, a.tj, Jb, e.bj0, e.bj1, a.vt, e.bad_index_flag, stream);
     if (rc) return rc;
     // body lbs_wobeta (EHM.py:134-137)
     return gsr_lbs_sp(B, Vb, Jb, 0, a.vt, (int64_t)Vb * 3, nullptr, nullptr, a.pose_b, 1, e.body.posedirs,

@@ -194,6 +194,7 @@ struct Inputs {
     float scale_mod;
     int prefiltered, antialiasing;
     int fwd_only;         // GSR_FORWARD_ONLY: preprocess writes only what binning and compositing read
+    int zero_ctrl;        // the forward's first kernel zeroes the control words (no memset launch)
     uint32_t xcd_map;     // render work-queue mapping (queue_item): 1 = tile-affine (strip order tile-major)
 };
 

@@ -29,7 +29,7 @@ __global__ __launch_bounds__(kScanBlock) void k_preprocess(Dims d, Inputs in, Ge
         }
         tiles = preprocess_one(d, in, g, o, b, gid, p, cp, sc, q, in.opac[in.s_opac * b + i]);
     }
-    if (in.fwd_only && threadIdx.x == 0 && blockIdx.x == 0 && b == 0) g.ctrl[kCtrlFwdOnly] = 1u;
+    zero_ctrl_words(d, in, g);
     preprocess_block_sums(d, g, b, blockIdx.x, tiles, gid);
 }
 

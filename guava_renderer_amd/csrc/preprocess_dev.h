@@ -158,4 +158,22 @@ __device__ __forceinline__ void preprocess_block_sums(const Dims& d, const GeomA
     __syncthreads();  // red[] is reused by the next frame of a multi-frame caller
 }
 
+
+// The control words of a forward (ctrl + the per-frame fstat rows) start at zero: the first kernel
+// of the forward (k_preprocess / k_deform_preprocess) zeroes them, one strided word per thread,
+// instead of a memset launch before it (in.zero_ctrl).  None of those words is read or accumulated
+// during that kernel except kCtrlError (a prefiltered forward's atomicOr: the host then keeps the
+// memset) and kCtrlFwdOnly (written here from in.fwd_only).
+__device__ __forceinline__ void zero_ctrl_words(const Dims& d, const Inputs& in, const GeomArena& g) {
+    const int64_t t = ((int64_t)blockIdx.y * gridDim.x + blockIdx.x) * blockDim.x + threadIdx.x;
+    if (in.zero_ctrl) {
+        const int64_t n = (int64_t)kCtrlWords + (int64_t)kFsWords * d.B;
+        const int64_t T = (int64_t)gridDim.x * gridDim.y * blockDim.x;
+        for (int64_t k = t; k < n; k += T)
+            if (k != kCtrlFwdOnly) g.ctrl[k] = 0u;
+        if (t == 0) g.ctrl[kCtrlFwdOnly] = in.fwd_only ? 1u : 0u;
+    } else if (in.fwd_only && t == 0) {
+        g.ctrl[kCtrlFwdOnly] = 1u;
+    }
+}
 }  // namespace gsr
