@@ -836,6 +836,28 @@ __host__ __device__ __forceinline__ uint32_t strip_mask(float4 co, float4 pre, f
     return bits;
 }
 
+// Quad mask of one instance (single-frame arenas, BinArena.qmask): bit 4 s + q is set unless no
+// pixel centre of quad q (4x4; x offset 4 (q & 1), y offset 4 (q >> 1)) of strip s can reach
+// alpha >= 1/255 -- the same box_reach test on the same conic and threshold as the strip mask, on the
+// quad's rectangle, for the strips whose bit `sm` keeps (a quad bit implies its strip bit).  The
+// single-frame quad render waves walk only their quad's entries with it.
+__device__ __forceinline__ uint32_t quad_mask(float4 co, float4 pre, float2 m, int tx, int ty, uint32_t sm) {
+    const uint32_t mode = __builtin_bit_cast(uint32_t, pre.w);
+    uint32_t bits = 0;
+#pragma unroll
+    for (int st = 0; st < kStrips; st++) {
+        if (!((sm >> st) & 1u)) continue;
+        if (mode == 2u) {
+            bits |= 0xFu << (4 * st);
+            continue;
+        }
+        int sx0, sy0;
+        strip_origin(tx, ty, st, sx0, sy0);
+        bits |= quad_reach4(co.x, co.y, co.z, pre.x, pre.y, pre.z, m, (float)sx0, (float)sy0) << (4 * st);
+    }
+    return bits;
+}
+
 // ---------------------------------------------------------------- 5. ordered scatter
 // One workgroup per chunk of d.chunk depth-ordered Gaussians (one count-table row), in d.chunk/kSlots
 // passes of kSlots Gaussians (one per thread, "slot").  A pass spreads its instances evenly over the
@@ -978,6 +1000,7 @@ __global__ __launch_bounds__(kSlots) __attribute__((amdgpu_waves_per_eu(6))) voi
             const uint32_t sm = (ABL & 1) ? 0xFu : strip_mask(s_co[o], s_pre[o], s_m[o], tx, ty);
             if (ABL & 2) sink += base[t] + lr + sm;
             else bn.point_list[base[t] + lr] = s_gi[o] | (sm << 28);
+            if (bn.qmask) bn.qmask[base[t] + lr] = quad_mask(s_co[o], s_pre[o], s_m[o], tx, ty, sm);
         }
         if ((pass + 1) * kSlots < d.chunk && j0 + kSlots < V) {  // uniform: advance base[] past this pass
             __syncthreads();

@@ -166,11 +166,14 @@ size_t carve_image(char* base, const Dims& d, ImageArena* im) {
     return align_up(off) + 256;
 }
 
-size_t carve_bin(char* base, int64_t R, BinArena* b) {
+// qmask: the single-frame quad masks after the list (forward entry points of one frame, and batch
+// workspaces of B = 1)
+size_t carve_bin(char* base, int64_t R, BinArena* b, bool qmask) {
     const size_t n = (size_t)(R > 0 ? R : 1);
     size_t off = 0;
     BinArena a;
     a.point_list = take<uint32_t>(base, off, n);
+    a.qmask = qmask ? take<uint32_t>(base, off, n) : nullptr;
     if (b) *b = a;
     return align_up(off) + 256;
 }
@@ -224,7 +227,7 @@ size_t gsr_geometry_bytes(int P, int width, int height) {
 size_t gsr_image_bytes(int width, int height) {
     return carve_image(nullptr, make_dims(1, 1, width, height), nullptr);
 }
-size_t gsr_binning_bytes(int64_t R) { return carve_bin(nullptr, R, nullptr); }
+size_t gsr_binning_bytes(int64_t R) { return carve_bin(nullptr, R, nullptr, true); }
 
 // Instances one frame can produce at most: every Gaussian in every tile (getRect clamps to the
 // grid), capped at the int range of num_rendered.
@@ -302,10 +305,10 @@ static int forward_single(gsr_alloc_fn geometryBuffer, gsr_alloc_fn binningBuffe
         const int64_t cap = async_bound(d);
         { StageTimer st_(1, s); launch_scan_blocksums(d, g, cap, s); }
         STAGE(debug, s, "scan");
-        char* bb = binningBuffer(alloc_ctx, carve_bin(nullptr, cap, nullptr));
+        char* bb = binningBuffer(alloc_ctx, carve_bin(nullptr, cap, nullptr, true));
         if (!bb) return fail(GSR_ERR_ALLOC, "binningBuffer allocation failed");
         BinArena bn;
-        carve_bin(bb, cap, &bn);
+        carve_bin(bb, cap, &bn, true);
         int rc = run_binning_and_render(d, in, g, im, bn, o, numerics, debug, s);
         if (rc < 0) return rc;
         if (status_host != kNoStatus)
@@ -322,10 +325,10 @@ static int forward_single(gsr_alloc_fn geometryBuffer, gsr_alloc_fn binningBuffe
     if (ctrl_h[kCtrlOverflow] || ctrl_h[kCtrlRLo] > 0x7FFFFFFFu)
         return fail(GSR_ERR_CAPACITY, "instance count exceeds 2^31 - 1 (num_rendered is an int)");
     const int64_t R = ctrl_h[kCtrlRLo];
-    char* bb = binningBuffer(alloc_ctx, carve_bin(nullptr, R, nullptr));
+    char* bb = binningBuffer(alloc_ctx, carve_bin(nullptr, R, nullptr, true));
     if (!bb) return fail(GSR_ERR_ALLOC, "binningBuffer allocation failed");
     BinArena bn;
-    carve_bin(bb, R, &bn);
+    carve_bin(bb, R, &bn, true);
     int rc = run_binning_and_render(d, in, g, im, bn, o, numerics, debug, s);
     if (rc < 0) return rc;
     return (int)R;
@@ -417,7 +420,7 @@ int gsr_backward_ex(int P, int D, int M, int R, const float* background, int wid
     BinArena bn;
     carve_geom(geom_buffer, d, &g);
     carve_image(image_buffer, d, &im);
-    carve_bin(binning_buffer, R, &bn);
+    carve_bin(binning_buffer, R, &bn, true);
     Inputs in{};
     env_tuning(in);
     in.means3D = means3D;
@@ -474,7 +477,7 @@ int gsr_backward(int P, int D, int M, int R, const float* background, int width,
 size_t gsr_batch_status_offset(int B, int P, int width, int height, int64_t R_capacity) {
     const Dims d = make_dims(B, P, width, height);
     return carve_geom(nullptr, d, nullptr) + carve_image(nullptr, d, nullptr) +
-           carve_bin(nullptr, R_capacity, nullptr);
+           carve_bin(nullptr, R_capacity, nullptr, B == 1);
 }
 
 size_t gsr_batch_workspace_bytes(int B, int P, int width, int height, int64_t R_capacity) {
@@ -485,10 +488,10 @@ static void carve_workspace(char* ws, const Dims& d, int64_t R_cap, GeomArena* g
                             BinArena* bn) {
     const size_t gsz = carve_geom(nullptr, d, nullptr);
     const size_t isz = carve_image(nullptr, d, nullptr);
-    const size_t bsz = carve_bin(nullptr, R_cap, nullptr);
+    const size_t bsz = carve_bin(nullptr, R_cap, nullptr, d.B == 1);
     carve_geom(ws, d, g);
     carve_image(ws + gsz, d, im);
-    carve_bin(ws + gsz + isz, R_cap, bn);
+    carve_bin(ws + gsz + isz, R_cap, bn, d.B == 1);
     g->sticky = reinterpret_cast<uint32_t*>(ws + gsz + isz + bsz);
 }
 

@@ -62,4 +62,44 @@ __host__ __device__ __forceinline__ bool box_reach(float a, float b, float c, fl
     return !(q > K + slack);
 }
 
+// box_reach of the four 4x4 quads of an 8x8 strip at (sx0, sy0) at once, bit q = quad q (x offset
+// 4 (q & 1), y offset 4 (q >> 1)): the same expressions as box_reach / rect_qmin on each quad (so the
+// same bits), with the per-column and per-row terms shared between quads and rect_qmin's branches
+// turned into selects of the same values (no divergent paths per quad).
+__host__ __device__ __forceinline__ uint32_t quad_reach4(float a, float b, float c, float K, float ia, float ic,
+                                                         float2 m, float sx0, float sy0) {
+    float dxl[2], dxh[2], mx[2], dyl[2], dyh[2], my[2];
+    bool xin[2], yin[2];
+#pragma unroll
+    for (int h = 0; h < 2; h++) {
+        const float x0 = sx0 + 4.0f * (float)h, y0 = sy0 + 4.0f * (float)h;
+        dxl[h] = m.x - (x0 + (4.0f - 1.0f));
+        dxh[h] = m.x - x0;
+        mx[h] = fmaxf(fabsf(dxl[h]), fabsf(dxh[h]));
+        dyl[h] = m.y - (y0 + (4.0f - 1.0f));
+        dyh[h] = m.y - y0;
+        my[h] = fmaxf(fabsf(dyl[h]), fabsf(dyh[h]));
+        xin[h] = dxl[h] <= 0.f && dxh[h] >= 0.f;
+        yin[h] = dyl[h] <= 0.f && dyh[h] >= 0.f;
+    }
+    uint32_t bits = 0;
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+        const int hx = q & 1, hy = q >> 1;
+        const float slack = 1e-4f * (a * mx[hx] * mx[hx] + 2.f * fabsf(b) * mx[hx] * my[hy] + c * my[hy] * my[hy]) +
+                            1e-3f * K + 1e-3f;
+        const float X = dxl[hx] > 0.f ? dxl[hx] : dxh[hx];
+        const float y = fminf(fmaxf(-b * X * ic, dyl[hy]), dyh[hy]);
+        const float qx = a * X * X + 2.f * b * X * y + c * y * y;
+        const float Y = dyl[hy] > 0.f ? dyl[hy] : dyh[hy];
+        const float x = fminf(fmaxf(-b * Y * ia, dxl[hx]), dxh[hx]);
+        const float qy = a * x * x + 2.f * b * x * Y + c * Y * Y;
+        float qm = xin[hx] ? 3.0e38f : qx;
+        qm = yin[hy] ? qm : fminf(qm, qy);
+        qm = (xin[hx] && yin[hy]) ? 0.f : qm;
+        bits |= (!(qm > K + slack)) ? (1u << q) : 0u;
+    }
+    return bits;
+}
+
 }  // namespace gsr

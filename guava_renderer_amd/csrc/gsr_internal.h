@@ -130,6 +130,8 @@ struct BinArena {
     uint32_t* point_list;  // per tile, depth-sorted: Gaussian index (within its frame, bits 0..27) |
                            // strip mask << 28, bit s set <=> the Gaussian can reach alpha >= 1/255
                            // somewhere in the tile's pixel strip s (strip_origin; render_fwd's wave unit)
+    uint32_t* qmask;       // single-frame arenas only (else null): per point_list entry, bit 4 s + q set
+                           // <=> it can reach alpha >= 1/255 in quad q (4x4) of strip s (the quad waves)
 };
 
 struct Dims {
@@ -171,7 +173,7 @@ inline Dims make_dims(int B, int P, int W, int H) {
 // Arena carving (base == nullptr -> size query).
 size_t carve_geom(char* base, const Dims& d, GeomArena* g);
 size_t carve_image(char* base, const Dims& d, ImageArena* im);
-size_t carve_bin(char* base, int64_t R, BinArena* b);
+size_t carve_bin(char* base, int64_t R, BinArena* b, bool qmask = false);
 // Upper bound on P: the render kernels address a frame's feature rows (128 B per Gaussian) through
 // a buffer resource with 32-bit byte offsets, so P * 128 must stay below 2^31.
 constexpr int kMaxGaussians = 1 << 24;

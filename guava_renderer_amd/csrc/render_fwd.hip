@@ -763,41 +763,56 @@ __global__ __launch_bounds__(GSR_TILE_PIX) __attribute__((amdgpu_waves_per_eu(4)
 // (global) load while this step blends; the chunk after next's list entries and the next chunk's
 // records are loaded one refill ahead.
 #ifndef GSR_QUAD_WPE
-#define GSR_QUAD_WPE 4
+#define GSR_QUAD_WPE 3  // (the 3-deep operand pipeline's registers: 4 waves would spill; measured -4%)
 #endif
-constexpr int kQRing = 128;  // ring entries per wave (a refill adds <= 64 and runs below 8)
+#ifndef GSR_QUAD_AHEAD
+#define GSR_QUAD_AHEAD 3  // steps between a step's record / feature loads and their use (2 or 3)
+#endif
+constexpr int kQRing = 512;  // ring entries per wave (a refill adds <= 256 and runs below 12)
+constexpr uint32_t kQNull = 0x07FFFFFFu;  // the null Gaussian: record / feature offsets out of range
 
-template <bool EXACT>
+// TL (gsr_render_timeline): per quad item, (start, end) in 100 MHz ticks, steps | refills << 16, list
+// entries walked
+template <bool EXACT, bool TL = false>
 __global__ __launch_bounds__(GSR_TILE_PIX) __attribute__((amdgpu_waves_per_eu(GSR_QUAD_WPE))) void k_render_quad(
-    Dims d, Inputs in, GeomArena g, ImageArena im, BinArena bn, Outputs o) {
+    Dims d, Inputs in, GeomArena g, ImageArena im, BinArena bn, Outputs o, int prio_n) {
     if (g.ctrl[kCtrlOverflow]) {
         overflow_fill(d, o);
         return;
     }
-    __shared__ uint4 qrec_all[GSR_TILE_PIX / 64][kQRing * 2];  // ring records: (x, y, o, 1/depth), (A, B, C, index)
-    __shared__ uint32_t qpos_all[GSR_TILE_PIX / 64][kQRing];   // ring list positions (1-based)
-    uint4* qrec = qrec_all[threadIdx.x >> 6];
+    __shared__ uint32_t qg_all[GSR_TILE_PIX / 64][kQRing];    // ring Gaussian indices
+    __shared__ uint32_t qpos_all[GSR_TILE_PIX / 64][kQRing];  // ring list positions (1-based)
+    uint32_t* qg = qg_all[threadIdx.x >> 6];
     uint32_t* qpos = qpos_all[threadIdx.x >> 6];
     const uint32_t ne = g.ctrl[kCtrlNonEmpty];
     const uint32_t nquad = 16u * ne;  // 4 strips x 4 quads per non-empty tile
     const uint32_t nempty = (uint32_t)(d.B * d.T) - ne;
     const int lane = threadIdx.x & 63;
     const int j = lane & 15, qq = lane >> 4;
+    const uint32_t sel1 = (qq & 1) ? 0xFFFFFFFFu : 0u, sel2 = (qq & 2) ? 0xFFFFFFFFu : 0u;
     const int64_t HW = (int64_t)d.H * d.W;
     uint32_t q = __builtin_amdgcn_s_getreg((3 << 11) | 20) & 7u;  // HW_REG_XCC_ID
     uint32_t q_left = 8;
     for (;;) {
         uint32_t item = 0xFFFFFFFFu;
+        uint32_t k_item = 0;
         while (q_left) {
             uint32_t k = 0;
             if (lane == 0) k = atomicAdd(&g.ctrl[kCtrlXcdQueue + kCtrlXcdStride * q], 1u);
             k = __builtin_amdgcn_readfirstlane(k);
+            k_item = k;
             item = queue_item_n<4>(q, k, ne, nempty, in.xcd_map, g.ctrl);
             if (item != 0xFFFFFFFFu) break;
             q = (q + 1) & 7u;
             q_left--;
         }
         if (!q_left) break;
+        // the first items of each queue are the longest quads (longest-first strip order): their
+        // waves take issue priority over the co-resident shorter ones, whose slack covers them
+        if (prio_n > 0) {
+            if (k_item < (uint32_t)prio_n) __builtin_amdgcn_s_setprio(1);
+            else __builtin_amdgcn_s_setprio(0);
+        }
         if (item >= nquad) {  // empty tile: background everywhere, T = 1
             const int tile_g = (int)im.work_list[ne + (item - nquad)];
             const int b = tile_g / d.T;
@@ -818,6 +833,8 @@ __global__ __launch_bounds__(GSR_TILE_PIX) __attribute__((amdgpu_waves_per_eu(GS
             }
             continue;
         }
+        const uint64_t t_start = TL ? __builtin_amdgcn_s_memrealtime() : 0;
+        uint32_t n_steps = 0, n_refills = 0, n_walk = 0;
         const uint32_t code = im.strip_list[item >> 2];
         const int quad = (int)(item & 3u);
         const int tile_g = (int)(code >> 2);
@@ -834,7 +851,6 @@ __global__ __launch_bounds__(GSR_TILE_PIX) __attribute__((amdgpu_waves_per_eu(GS
         float T = 1.0f, invd = 0.f;
         uint32_t last = 0;
         floatx4 qa0 = {0.f, 0.f, 0.f, 0.f}, qa1 = {0.f, 0.f, 0.f, 0.f};
-        const uint32_t smask_bit = 1u << (28 + strip);
         if (im.strip_cnt[(int64_t)tile_g * kStrips + strip] != 0u) {
             const uint2 range = im.ranges[tile_g];
             const int n = (int)(range.y - range.x);
@@ -845,82 +861,102 @@ __global__ __launch_bounds__(GSR_TILE_PIX) __attribute__((amdgpu_waves_per_eu(GS
             const __amdgpu_buffer_rsrc_t frs = __builtin_amdgcn_make_buffer_rsrc(
                 (void*)(in.colors + in.s_colors * b), 0, (int)min((int64_t)d.P * GSR_C * 4, (int64_t)0x7FFFFFFF),
                 0x00020000);
-            const float qbx = (float)qx0, qby = (float)qy0;
-            // list walk: chunk c's records (lane i: entry c*64 + i, when a strip survivor) and chunk
-            // c+1's entries are in flight one refill ahead
-            int base = 0;                  // first list position of the next chunk to test
+            // list walk, 256 entries per refill (4 per lane): the entries and their quad masks
+            // (binning's box test of this quad, BinArena.qmask) are contiguous loads with no
+            // dependent ones, double-buffered one refill ahead; the survivors' Gaussian indices and
+            // list positions go to the ring
+            const uint32_t qbit = 4u * (uint32_t)strip + (uint32_t)quad;
+            const uint32_t* __restrict__ qm = bn.qmask + range.x;
+            int base = 0;                  // first list position of the next refill
             uint32_t head = 0, tail = 0;   // ring counters (head advances by 4: entries never wrap in a step)
-            uint32_t e_cur = lane < n ? plist[lane] : 0u;
-            uint32_t e_nxt = 64 + lane < n ? plist[64 + lane] : 0u;
-            auto load_rec = [&](uint32_t e, int pos0, float4& r0, float4& r1) {
-                const bool sb = pos0 + lane < n && (e & smask_bit) != 0u;
-                const uint32_t off = sb ? (e & kIndexMask) * 32u : 0x80000000u;  // out of range: zeros
-                r0 = rec_load(rrs, off);
-                r1 = rec_load(rrs, off + 16u);
+            uint32_t ec[4], mc[4], en[4], mn[4];
+            auto load_chunks = [&](int b0, uint32_t (&e)[4], uint32_t (&m)[4]) {
+#pragma unroll
+                for (int u = 0; u < 4; u++) {
+                    const int p = b0 + 64 * u + lane;
+                    e[u] = p < n ? plist[p] : 0u;
+                    m[u] = p < n ? (uint32_t)qm[p] : 0u;  // (zero past the list's end: nothing kept)
+                }
             };
-            float4 c0, c1;
-            load_rec(e_cur, 0, c0, c1);
+            load_chunks(0, ec, mc);
+            load_chunks(256, en, mn);
             auto refill = [&]() {
-                // chunk at `base`: records c0 / c1 (zeros where not a strip survivor), entries e_cur
-                const bool sb = base + lane < n && (e_cur & smask_bit) != 0u;
-                bool keep = false;
-                if (sb) {
-                    const float a = -2.0f * c1.x, bb = -c1.y, c = -2.0f * c1.z;  // the conic (exact scalings)
-                    const float4 pre = strip_pre(make_float4(a, bb, c, c0.z));
-                    const uint32_t mode = __builtin_bit_cast(uint32_t, pre.w);
-                    keep = mode == 2u || (mode == 0u && box_reach(a, bb, c, pre.x, pre.y, pre.z,
-                                                                  make_float2(c0.x, c0.y), qbx, qby, 4.0f, 4.0f));
+#pragma unroll
+                for (int u = 0; u < 4; u++) {
+                    const bool keep = ((mc[u] >> qbit) & 1u) != 0u;
+                    const uint64_t km = __ballot(keep);
+                    if (keep) {
+                        const uint32_t slot = (tail + __builtin_amdgcn_mbcnt_hi((uint32_t)(km >> 32),
+                                                                                __builtin_amdgcn_mbcnt_lo((uint32_t)km, 0u))) &
+                                              (kQRing - 1);
+                        qg[slot] = ec[u] & kIndexMask;
+                        qpos[slot] = (uint32_t)(base + 64 * u + lane + 1);
+                    }
+                    tail += (uint32_t)__builtin_popcountll(km);
                 }
-                const uint64_t km = __ballot(keep);
-                if (keep) {
-                    const uint32_t slot = (tail + __builtin_amdgcn_mbcnt_hi((uint32_t)(km >> 32),
-                                                                            __builtin_amdgcn_mbcnt_lo((uint32_t)km, 0u))) &
-                                          (kQRing - 1);
-                    qrec[2 * slot] = __builtin_bit_cast(uint4, c0);
-                    qrec[2 * slot + 1] = make_uint4(__float_as_uint(c1.x), __float_as_uint(c1.y), __float_as_uint(c1.z),
-                                                    e_cur & kIndexMask);
-                    qpos[slot] = (uint32_t)(base + lane + 1);
+                base += 256;
+                if (TL) n_refills++;
+#pragma unroll
+                for (int u = 0; u < 4; u++) {
+                    ec[u] = en[u];
+                    mc[u] = mn[u];
                 }
-                tail += (uint32_t)__builtin_popcountll(km);
-                base += 64;
-                // next chunk: its records from the entries in hand, the entries after it
-                e_cur = e_nxt;
-                load_rec(e_cur, base, c0, c1);
-                e_nxt = base + 64 + lane < n ? plist[base + 64 + lane] : 0u;
+                load_chunks(base + 256, en, mn);
                 __builtin_amdgcn_wave_barrier();
             };
-            // fill so that entries [head, head + 8) exist, or the list is exhausted
+            // fill so that entries [head, head + 4 (GSR_QUAD_AHEAD + 1)) exist; once the list is
+            // exhausted, the ring slots past its last entry hold the null Gaussian (an index whose record and feature
+            // offsets are out of range: zeros, opacity 0, nothing taken), so the step operands are read
+            // without a validity branch
+            bool nulled = false;
             auto ensure = [&]() {
-                while (tail - head < 8u && base < n) refill();
+                while (tail - head < 4u * (GSR_QUAD_AHEAD + 1) && base < n) refill();
+                if (base >= n && !nulled) {
+                    nulled = true;
+                    if (lane < 4 * (GSR_QUAD_AHEAD + 1)) {
+                        const uint32_t slot = (tail + (uint32_t)lane) & (kQRing - 1);
+                        qg[slot] = kQNull;
+                        qpos[slot] = 0u;
+                    }
+                    __builtin_amdgcn_wave_barrier();
+                }
             };
-            // one step's operands, lane group qq: ring entry head + qq (the null Gaussian past tail)
-            auto operands = [&](uint32_t h, float4& r0, float4& r1, uint4& pos4, float& f0, float& f1) {
-                const uint32_t slot = (h + (uint32_t)qq) & (kQRing - 1);
-                const bool valid = h + (uint32_t)qq < tail;
-                const uint4 u0 = qrec[2 * slot], u1 = qrec[2 * slot + 1];
-                r0 = valid ? __builtin_bit_cast(float4, u0) : make_float4(0.f, 0.f, 0.f, 0.f);
-                r1 = valid ? __builtin_bit_cast(float4, u1) : make_float4(0.f, 0.f, 0.f, 0.f);
-                pos4 = *reinterpret_cast<const uint4*>(&qpos[h & (kQRing - 1)]);
-                const uint32_t fo = valid ? u1.w * (uint32_t)(GSR_C * 4) + (uint32_t)j * 4u : 0x80000000u;
+            // one step's render records (lane group qq: ring entry h + qq) and feature words (A operands:
+            // channels j and 16 + j), from global memory two steps ahead of their use
+            auto records = [&](uint32_t h, float4& r0, float4& r1, float& f0, float& f1) {
+                const uint32_t gi = qg[(h + (uint32_t)qq) & (kQRing - 1)];
+                r0 = rec_load(rrs, gi * 32u);
+                r1 = rec_load(rrs, gi * 32u + 16u);
+                const uint32_t fo = gi * (uint32_t)(GSR_C * 4) + (uint32_t)j * 4u;
                 f0 = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(frs, (int)fo, 0, 0));
                 f1 = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(frs, (int)(fo + 64u), 0, 0));
             };
+            auto positions = [&](uint32_t h) { return *reinterpret_cast<const uint4*>(&qpos[h & (kQRing - 1)]); };
             ensure();
             __builtin_amdgcn_wave_barrier();
-            float4 r0, r1;
-            uint4 p4;
-            float f0, f1;
-            operands(head, r0, r1, p4, f0, f1);
+            float4 r0, r1, nr0, nr1;
+            float f0, f1, nf0, nf1;
+            records(head, r0, r1, f0, f1);
+            records(head + 4u, nr0, nr1, nf0, nf1);
+#if GSR_QUAD_AHEAD == 3
+            float4 mr0, mr1;  // the step after next's
+            float mf0, mf1;
+            records(head + 8u, mr0, mr1, mf0, mf1);
+#endif
+            uint4 p4 = positions(head);
+            float al = alpha_of<EXACT>(r0, r1, pfx, pfy);
             while (head < tail) {
-                // the next step's operands first (their loads run under this step's blend)
+                // the operands of the step after next first (their loads run under this step's blend)
                 ensure();
                 __builtin_amdgcn_wave_barrier();
-                float4 nr0, nr1;
-                uint4 np4;
-                float nf0, nf1;
-                operands(head + 4u, nr0, nr1, np4, nf0, nf1);
+                float4 nnr0, nnr1;
+                float nnf0, nnf1;
+                records(head + 4u * GSR_QUAD_AHEAD, nnr0, nnr1, nnf0, nnf1);
+                const uint4 np4 = positions(head + 4u);
+                // the next step's alpha (independent of this step's transmittance chain, so the two
+                // interleave: a lone tail wave is latency-bound, one dependent instruction after another)
+                const float nal = alpha_of<EXACT>(nr0, nr1, pfx, pfy);
                 // this step
-                const float al = alpha_of<EXACT>(r0, r1, pfx, pfy);
                 const auto a16 = __builtin_amdgcn_permlane16_swap(__float_as_uint(al), __float_as_uint(al), false, false);
                 const auto a02 = __builtin_amdgcn_permlane32_swap(a16[0], a16[0], false, false);
                 const auto a13 = __builtin_amdgcn_permlane32_swap(a16[1], a16[1], false, false);
@@ -932,13 +968,33 @@ __global__ __launch_bounds__(GSR_TILE_PIX) __attribute__((amdgpu_waves_per_eu(GS
                 const float w1 = take_step(__uint_as_float(a13[0]), __uint_as_float(i13[0]), p4.y, T, invd, last, done);
                 const float w2 = take_step(__uint_as_float(a02[1]), __uint_as_float(i02[1]), p4.z, T, invd, last, done);
                 const float w3 = take_step(__uint_as_float(a13[1]), __uint_as_float(i13[1]), p4.w, T, invd, last, done);
-                const float wq = qq == 0 ? w0 : qq == 1 ? w1 : qq == 2 ? w2 : w3;
+                // Gaussian qq's weight, by two bit selects on loop-invariant lane masks (v_bfi_b32; a
+                // ternary chain on qq compiled to divergent branches)
+                const uint32_t w01 = (__float_as_uint(w1) & sel1) | (__float_as_uint(w0) & ~sel1);
+                const uint32_t w23 = (__float_as_uint(w3) & sel1) | (__float_as_uint(w2) & ~sel1);
+                const float wq = __uint_as_float((w23 & sel2) | (w01 & ~sel2));
                 qa0 = __builtin_amdgcn_mfma_f32_16x16x4f32(f0, wq, qa0, 0, 0, 0);
                 qa1 = __builtin_amdgcn_mfma_f32_16x16x4f32(f1, wq, qa1, 0, 0, 0);
                 head += 4u;
-                r0 = nr0; r1 = nr1; p4 = np4; f0 = nf0; f1 = nf1;
+                if (TL) n_steps++;
+#if GSR_QUAD_AHEAD == 3
+                r0 = nr0; r1 = nr1; nr0 = mr0; nr1 = mr1; mr0 = nnr0; mr1 = nnr1; p4 = np4;
+                f0 = nf0; f1 = nf1; nf0 = mf0; nf1 = mf1; mf0 = nnf0; mf1 = nnf1; al = nal;
+#else
+                r0 = nr0; r1 = nr1; nr0 = nnr0; nr1 = nnr1; p4 = np4;
+                f0 = nf0; f1 = nf1; nf0 = nnf0; nf1 = nnf1; al = nal;
+#endif
                 if (!__any(!done)) break;  // every pixel of the quad finished
             }
+            if (TL) n_walk = (uint32_t)min(base, n);
+        }
+        if (TL && lane == 0 && item < o.timeline_cap) {
+            const uint64_t t_end = __builtin_amdgcn_s_memrealtime();
+            uint32_t* rec = o.timeline + 4 * (size_t)item;
+            rec[0] = (uint32_t)t_start;
+            rec[1] = (uint32_t)t_end;
+            rec[2] = min(n_steps, 0xFFFFu) | (min(n_refills, 0xFFFFu) << 16);
+            rec[3] = n_walk;
         }
         // epilogue: group 0 stores final_T / n_contrib / inverse depth, every lane its channels
         // 4 qq + r and 16 + 4 qq + r of pixel j
@@ -1000,17 +1056,23 @@ void launch_render_fwd(const Dims& d, const Inputs& in_, const GeomArena& g, con
     }
     if (o.stats) {
         GSR_LAUNCH(0, true, false)
+    } else if (o.timeline && d.B == 1 && quad_mode && !split && b.qmask) {  // the quad kernel's own timeline
+        const dim3 gq(min((4 * nwaves + 3) / 4, persistent_grid(quad_wg)));
+        if (exact) hipLaunchKernelGGL((k_render_quad<true, true>), gq, bl, 0, s, d, in, g, im, b, o, 0);
+        else hipLaunchKernelGGL((k_render_quad<false, true>), gq, bl, 0, s, d, in, g, im, b, o, 0);
     } else if (o.timeline) {
         GSR_LAUNCH(0, false, true)
     } else if (o.out_refine) {  // (4-wave register budget: 4 workgroups per CU)
         const dim3 grf(min((nwaves + 3) / 4, persistent_grid(4)));
         if (exact) hipLaunchKernelGGL((k_render_fwd_refine<true>), grf, bl, 0, s, d, in, g, im, b, o);
         else hipLaunchKernelGGL((k_render_fwd_refine<false>), grf, bl, 0, s, d, in, g, im, b, o);
-    } else if (d.B == 1 && quad_mode && !split) {
-        // one frame, quad waves with their own cull: the longest quads' chains are what count here
+    } else if (d.B == 1 && quad_mode && !split && b.qmask) {
+        // one frame, quad waves walking their quad masks: the longest quads' chains are what count here
         const dim3 gq(min((4 * nwaves + 3) / 4, persistent_grid(quad_wg)));
-        if (exact) hipLaunchKernelGGL((k_render_quad<true>), gq, bl, 0, s, d, in, g, im, b, o);
-        else hipLaunchKernelGGL((k_render_quad<false>), gq, bl, 0, s, d, in, g, im, b, o);
+        // GSR_QUAD_PRIO: queue items per XCD that run at issue priority 1 (A/B)
+        static const int prio_n = tune_env("GSR_QUAD_PRIO", 0);
+        if (exact) hipLaunchKernelGGL((k_render_quad<true>), gq, bl, 0, s, d, in, g, im, b, o, prio_n);
+        else hipLaunchKernelGGL((k_render_quad<false>), gq, bl, 0, s, d, in, g, im, b, o, prio_n);
     } else if (d.B == 1 && half_mode) {
         // one frame, half-strip waves: a strip's two halves run in parallel, each lane one
         // (pixel, Gaussian) alpha per k-step -- the longest strip's time is what counts here

@@ -23,8 +23,10 @@ NUM_CHANNELS = 32
 # images x many Gaussians) size the buffer from the synchronous R read-back as the reference does.
 # The no-sync forward's buffer is the P x tiles bound, so it is only used when nobody keeps the
 # buffer (exact_binning=False: inference -- GaussianRasterizer_32 under no_grad drops it with the
-# call); a forward whose buffers autograd saves for backward sizes it to the exact R.
-ASYNC_BINNING_MB = int(os.environ.get("GSR_ASYNC_BINNING_MB", "512"))
+# call); a forward whose buffers autograd saves for backward sizes it to the exact R.  A frame's
+# buffer holds 8 B per bound instance (list entry + quad mask): 1 GB covers 100k Gaussians at 512^2
+# (the bound is P x tiles; the inference path keeps one such arena per stream, of 288 GB of HBM).
+ASYNC_BINNING_MB = int(os.environ.get("GSR_ASYNC_BINNING_MB", "1024"))
 # numerics of the reference-signature calls that pass none (GaussianRasterizer_32 as GUAVA calls it):
 # 0 = bit-identical to the oracle.  A deployment can opt into a tolerance mode for the unchanged
 # caller, e.g. GSR_NUMERICS=split_bf16 (or fast_exp), comma-separated.
