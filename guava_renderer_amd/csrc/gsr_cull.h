@@ -62,6 +62,34 @@ __host__ __device__ __forceinline__ bool box_reach(float a, float b, float c, fl
     return !(q > K + slack);
 }
 
+// The pixel-centre bounding box (xmin, ymin, xmax, ymax) of where a Gaussian can reach alpha >=
+// 1/255, for the single-frame quad masks: the ellipse Q <= K has half-extents sqrt(K c / det) and
+// sqrt(K a / det) (det = ac - b^2), taken here for K' = 1.01 K + 0.01 -- a 1% margin that exceeds the
+// float rounding of the blend's power by orders of magnitude for any conic with |b| <= 0.995
+// sqrt(ac) (terms at most 400x Q there).  Flatter conics (and mode 2) get an unbounded box: every
+// quad of their kept strips stays.  Per Gaussian, once.
+__host__ __device__ __forceinline__ float4 reach_bbox(float4 co, float4 pre, float2 m) {
+    const float a = co.x, b = co.y, c = co.z;
+    const uint32_t mode = __builtin_bit_cast(uint32_t, pre.w);
+    const float det = a * c - b * b;
+    if (mode != 0u || !(b * b <= 0.990025f * (a * c)) || !(det > 0.f))
+        return make_float4(-3.0e38f, -3.0e38f, 3.0e38f, 3.0e38f);
+    const float K2 = 1.01f * pre.x + 0.01f;
+    const float hx = sqrtf(K2 * c / det) * 1.001f + 1e-3f, hy = sqrtf(K2 * a / det) * 1.001f + 1e-3f;
+    return make_float4(m.x - hx, m.y - hy, m.x + hx, m.y + hy);
+}
+// The four quads (bit q: x offset 4 (q & 1), y offset 4 (q >> 1)) of the 8x8 strip at (sx0, sy0)
+// whose pixel centres meet the box.
+__host__ __device__ __forceinline__ uint32_t quad_bits_bbox(float4 bb, float sx0, float sy0) {
+    uint32_t bits = 0;
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+        const float x0 = sx0 + 4.0f * (float)(q & 1), y0 = sy0 + 4.0f * (float)(q >> 1);
+        bits |= (bb.x <= x0 + 3.0f && bb.z >= x0 && bb.y <= y0 + 3.0f && bb.w >= y0) ? (1u << q) : 0u;
+    }
+    return bits;
+}
+
 // box_reach of the four 4x4 quads of an 8x8 strip at (sx0, sy0) at once, bit q = quad q (x offset
 // 4 (q & 1), y offset 4 (q >> 1)): the same expressions as box_reach / rect_qmin on each quad (so the
 // same bits), with the per-column and per-row terms shared between quads and rect_qmin's branches

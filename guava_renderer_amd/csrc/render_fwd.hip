@@ -766,7 +766,7 @@ __global__ __launch_bounds__(GSR_TILE_PIX) __attribute__((amdgpu_waves_per_eu(4)
 #define GSR_QUAD_WPE 3  // (the 3-deep operand pipeline's registers: 4 waves would spill; measured -4%)
 #endif
 #ifndef GSR_QUAD_AHEAD
-#define GSR_QUAD_AHEAD 3  // steps between a step's record / feature loads and their use (2 or 3)
+#define GSR_QUAD_AHEAD 3  // steps between a step's record / feature loads and their use (>= 2)
 #endif
 constexpr int kQRing = 512;  // ring entries per wave (a refill adds <= 256 and runs below 12)
 constexpr uint32_t kQNull = 0x07FFFFFFu;  // the null Gaussian: record / feature offsets out of range
@@ -934,28 +934,27 @@ __global__ __launch_bounds__(GSR_TILE_PIX) __attribute__((amdgpu_waves_per_eu(GS
             auto positions = [&](uint32_t h) { return *reinterpret_cast<const uint4*>(&qpos[h & (kQRing - 1)]); };
             ensure();
             __builtin_amdgcn_wave_barrier();
-            float4 r0, r1, nr0, nr1;
-            float f0, f1, nf0, nf1;
-            records(head, r0, r1, f0, f1);
-            records(head + 4u, nr0, nr1, nf0, nf1);
-#if GSR_QUAD_AHEAD == 3
-            float4 mr0, mr1;  // the step after next's
-            float mf0, mf1;
-            records(head + 8u, mr0, mr1, mf0, mf1);
-#endif
+            // operand pipeline: slot k holds step head + 4k's records and feature words (k < AHEAD)
+            constexpr int AHEAD = GSR_QUAD_AHEAD;
+            float4 pr0[AHEAD], pr1[AHEAD];
+            float pf0[AHEAD], pf1[AHEAD];
+#pragma unroll
+            for (int k = 0; k < AHEAD; k++) records(head + 4u * k, pr0[k], pr1[k], pf0[k], pf1[k]);
             uint4 p4 = positions(head);
-            float al = alpha_of<EXACT>(r0, r1, pfx, pfy);
+            float al = alpha_of<EXACT>(pr0[0], pr1[0], pfx, pfy);
             while (head < tail) {
                 // the operands of the step after next first (their loads run under this step's blend)
                 ensure();
                 __builtin_amdgcn_wave_barrier();
                 float4 nnr0, nnr1;
                 float nnf0, nnf1;
-                records(head + 4u * GSR_QUAD_AHEAD, nnr0, nnr1, nnf0, nnf1);
+                records(head + 4u * AHEAD, nnr0, nnr1, nnf0, nnf1);
                 const uint4 np4 = positions(head + 4u);
                 // the next step's alpha (independent of this step's transmittance chain, so the two
                 // interleave: a lone tail wave is latency-bound, one dependent instruction after another)
-                const float nal = alpha_of<EXACT>(nr0, nr1, pfx, pfy);
+                const float nal = alpha_of<EXACT>(pr0[1 % AHEAD], pr1[1 % AHEAD], pfx, pfy);
+                const float4 r0 = pr0[0];
+                const float f0 = pf0[0], f1 = pf1[0];
                 // this step
                 const auto a16 = __builtin_amdgcn_permlane16_swap(__float_as_uint(al), __float_as_uint(al), false, false);
                 const auto a02 = __builtin_amdgcn_permlane32_swap(a16[0], a16[0], false, false);
@@ -977,13 +976,13 @@ __global__ __launch_bounds__(GSR_TILE_PIX) __attribute__((amdgpu_waves_per_eu(GS
                 qa1 = __builtin_amdgcn_mfma_f32_16x16x4f32(f1, wq, qa1, 0, 0, 0);
                 head += 4u;
                 if (TL) n_steps++;
-#if GSR_QUAD_AHEAD == 3
-                r0 = nr0; r1 = nr1; nr0 = mr0; nr1 = mr1; mr0 = nnr0; mr1 = nnr1; p4 = np4;
-                f0 = nf0; f1 = nf1; nf0 = mf0; nf1 = mf1; mf0 = nnf0; mf1 = nnf1; al = nal;
-#else
-                r0 = nr0; r1 = nr1; nr0 = nnr0; nr1 = nnr1; p4 = np4;
-                f0 = nf0; f1 = nf1; nf0 = nnf0; nf1 = nnf1; al = nal;
-#endif
+#pragma unroll
+                for (int k = 0; k + 1 < AHEAD; k++) {
+                    pr0[k] = pr0[k + 1]; pr1[k] = pr1[k + 1]; pf0[k] = pf0[k + 1]; pf1[k] = pf1[k + 1];
+                }
+                pr0[AHEAD - 1] = nnr0; pr1[AHEAD - 1] = nnr1; pf0[AHEAD - 1] = nnf0; pf1[AHEAD - 1] = nnf1;
+                p4 = np4;
+                al = nal;
                 if (!__any(!done)) break;  // every pixel of the quad finished
             }
             if (TL) n_walk = (uint32_t)min(base, n);

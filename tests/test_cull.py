@@ -1,8 +1,8 @@
 """The culling tests that decide which (Gaussian, pixel rectangle) pairs the GPU never blends
 (csrc/gsr_cull.h): built for the host with hipcc and run on random conics (tools/quad_mask_check.cpp).
-The single-frame quad masks must equal box_reach on each quad and never clear a quad holding a pixel
-centre at alpha >= 1/255 (float64 brute force) -- so the quad render waves' lists stay
-decision-preserving."""
+quad_reach4 must equal box_reach on each quad, and the single-frame quad masks binning stores (reach
+boxes) must never clear a quad holding a pixel centre at alpha >= 1/255 (float64 brute force) -- so
+the quad render waves' lists stay decision-preserving."""
 import os
 import shutil
 import subprocess
@@ -24,3 +24,4 @@ def test_quad_masks_match_box_reach_and_never_drop(tmp_path):
     print(out.stdout)
     assert out.returncode == 0, out.stdout
     assert "mismatches vs box_reach 0, missed 0" in out.stdout
+    assert "reach boxes: missed 0," in out.stdout

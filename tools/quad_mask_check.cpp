@@ -1,7 +1,8 @@
-// Host check of the single-frame quad masks (gsr_cull.h quad_reach4, used by binning.hip quad_mask):
-// (1) every bit equals box_reach on that 4x4 quad (the shared-term form computes the same values), and
-// (2) no quad with a pixel centre at Q <= K = 2 ln(255 o) (float64 brute force over its 16 pixels) is
-// ever cleared -- the masks only drop pairs the blend skips anyway.  Random conics around one strip,
+// Host check of the single-frame quad tests (gsr_cull.h): (1) quad_reach4 equals box_reach on each
+// 4x4 quad (the shared-term form computes the same values); (2) the quad masks binning stores
+// (binning.hip quad_mask: reach_bbox + quad_bits_bbox) never clear a quad with a pixel centre at
+// Q <= K = 2 ln(255 o) (float64 brute force over its 16 pixels) -- they only drop pairs the blend
+// skips anyway -- and report how many quads they keep beyond those.  Random conics around one strip,
 // including means inside, on the edges and far away, and thin rotated ellipses:
 //   hipcc -O2 -std=c++17 -ffp-contract=off --offload-arch=gfx950 -I guava_renderer_amd/csrc \
 //         tools/quad_mask_check.cpp -o /tmp/qmc && /tmp/qmc
@@ -14,7 +15,7 @@ int main() {
     using namespace gsr;
     std::mt19937 rng(11);
     std::uniform_real_distribution<float> U(0.f, 1.f);
-    long n = 0, mismatch = 0, missed = 0, need = 0, kept = 0;
+    long n = 0, mismatch = 0, missed = 0, need = 0, kept = 0, bb_missed = 0, bb_kept = 0;
     for (int it = 0; it < 400000; it++) {
         const float sx0 = 8.f * (float)(it % 5), sy0 = 8.f * (float)((it / 5) % 3);
         const float s1 = std::exp(-3.f + 6.f * U(rng)), s2 = std::exp(-3.f + 6.f * U(rng));
@@ -30,6 +31,7 @@ int main() {
         const float4 pre = strip_pre(make_float4(a, b, c, o));
         if (__builtin_bit_cast(uint32_t, pre.w) != 0u) continue;
         const uint32_t bits = quad_reach4(a, b, c, pre.x, pre.y, pre.z, m, sx0, sy0);
+        const uint32_t bbits = quad_bits_bbox(reach_bbox(make_float4(a, b, c, o), pre, m), sx0, sy0);
         for (int q = 0; q < 4; q++) {
             const float x0 = sx0 + 4.f * (q & 1), y0 = sy0 + 4.f * (q >> 1);
             const bool ref = box_reach(a, b, c, pre.x, pre.y, pre.z, m, x0, y0, 4.f, 4.f);
@@ -46,9 +48,12 @@ int main() {
                 }
             need += reach;
             missed += reach && !got;
+            const bool bgot = (bbits >> q) & 1u;
+            bb_kept += bgot;
+            bb_missed += reach && !bgot;
         }
     }
-    std::printf("quads %ld: mismatches vs box_reach %ld, missed %ld, needed %ld, kept %ld\n", n, mismatch, missed,
-                need, kept);
-    return (mismatch || missed) ? 1 : 0;
+    std::printf("quads %ld: mismatches vs box_reach %ld, missed %ld, needed %ld, kept %ld; "
+                "reach boxes: missed %ld, kept %ld\n", n, mismatch, missed, need, kept, bb_missed, bb_kept);
+    return (mismatch || missed || bb_missed) ? 1 : 0;
 }

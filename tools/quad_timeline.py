@@ -65,3 +65,10 @@ for i in np.argsort(-dur)[:10]:
     print(f"  {idx[i]:6d} {start[i] / 1000:8.1f} {dur[i] / 1000:7.1f} {steps[i]:6d} {refills[i]:7d} {walk[i]:7d}")
 print(f"sum of item durations {dur.sum() / 1000:.0f} us over {len(r)} items; "
       f"work-weighted: refills {refills.sum()}, steps {steps.sum()}")
+A = np.stack([steps, refills, np.ones_like(steps)], 1).astype(np.float64)
+coef = np.linalg.lstsq(A, dur, rcond=None)[0]
+print(f"fit over items: duration = {coef[0]:.0f} ns/step + {coef[1]:.0f} ns/refill + {coef[2]:.0f} ns")
+late = start > 60000
+if late.any():
+    coef2 = np.linalg.lstsq(A[late], dur[late], rcond=None)[0]
+    print(f"items starting after 60 us ({late.sum()}): {coef2[0]:.0f} ns/step + {coef2[1]:.0f} ns/refill + {coef2[2]:.0f}")
