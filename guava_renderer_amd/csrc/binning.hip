@@ -859,6 +859,50 @@ __device__ __forceinline__ uint32_t quad_mask(float4 co, float4 pre, float2 m, i
     return bits;
 }
 
+// The quad masks of a single-frame list, in place: the scatter leaves each entry's tile in its qmask
+// word, and this flat pass (all of the list's entries at full occupancy, 4 per thread in flight;
+// the scatter itself runs one workgroup per 256 Gaussians at one frame, latency-bound, and computing
+// the masks there cost it 2.4x) replaces it with quad_mask.
+__global__ __launch_bounds__(256) void k_quad_masks(Dims d, GeomArena g, BinArena bn) {
+    if (g.ctrl[kCtrlOverflow]) return;
+    const uint32_t R = g.ctrl[kCtrlRLo];  // (one frame: the list length)
+    const uint32_t stride = gridDim.x * 256u * 4u;
+    for (uint32_t p0 = blockIdx.x * 1024u + threadIdx.x; p0 < R; p0 += stride) {
+        uint32_t e[4], t[4];
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            const uint32_t p = p0 + 256u * u;
+            e[u] = p < R ? bn.point_list[p] : 0u;
+            t[u] = p < R ? bn.qmask[p] : 0u;
+        }
+        float4 r0[4], r1[4];
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            const int64_t gi = (int64_t)(e[u] & kIndexMask);
+            r0[u] = (e[u] >> 28) ? g.rrec[2 * gi] : make_float4(0.f, 0.f, 0.f, 0.f);
+            r1[u] = (e[u] >> 28) ? g.rrec[2 * gi + 1] : make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            const uint32_t p = p0 + 256u * u;
+            if (p >= R) continue;
+            const uint32_t sm = e[u] >> 28;
+            uint32_t mask = 0;
+            if (sm) {
+                // the scatter's conic / opacity / mean of the render record (exact rescaling)
+                const float4 co = make_float4(-2.0f * r1[u].x, -r1[u].y, -2.0f * r1[u].z, r0[u].z);
+                mask = quad_mask(co, strip_pre(co), make_float2(r0[u].x, r0[u].y), (int)t[u] % d.gx,
+                                 (int)t[u] / d.gx, sm);
+            }
+            bn.qmask[p] = mask;
+        }
+    }
+}
+
+void launch_quad_masks(const Dims& d, const GeomArena& g, const BinArena& b, hipStream_t s) {
+    if (b.qmask && d.B == 1 && d.P > 0) hipLaunchKernelGGL(k_quad_masks, dim3(1024), dim3(256), 0, s, d, g, b);
+}
+
 // ---------------------------------------------------------------- 5. ordered scatter
 // One workgroup per chunk of d.chunk depth-ordered Gaussians (one count-table row), in d.chunk/kSlots
 // passes of kSlots Gaussians (one per thread, "slot").  A pass spreads its instances evenly over the
@@ -1001,7 +1045,7 @@ __global__ __launch_bounds__(kSlots) __attribute__((amdgpu_waves_per_eu(6))) voi
             const uint32_t sm = (ABL & 1) ? 0xFu : strip_mask(s_co[o], s_pre[o], s_m[o], tx, ty);
             if (ABL & 2) sink += base[t] + lr + sm;
             else bn.point_list[base[t] + lr] = s_gi[o] | (sm << 28);
-            if (bn.qmask) bn.qmask[base[t] + lr] = quad_mask(s_co[o], s_pre[o], s_m[o], tx, ty, sm);
+            if (bn.qmask) bn.qmask[base[t] + lr] = (uint32_t)t;  // (k_quad_masks turns it into the mask)
         }
         if ((pass + 1) * kSlots < d.chunk && j0 + kSlots < V) {  // uniform: advance base[] past this pass
             __syncthreads();
@@ -1321,6 +1365,7 @@ void launch_strip_order(const Dims& d, const GeomArena& g, const ImageArena& im,
     if (d.B == 0 || d.T == 0) return;
     const int nt = d.B * d.T;
     hipLaunchKernelGGL(k_strip_count, dim3((nt + 3) / 4), dim3(256), 0, s, d, im, b);
+    launch_quad_masks(d, g, b, s);
     const int tile_major = strip_order_tile_major();
     // (one frame: the tile-affine walk of one longest-first list, measured 1.5% faster there)
     const int map = tile_major ? (d.B == 1 ? 1 : xcd_queue_map()) : 0;
