@@ -860,42 +860,74 @@ __device__ __forceinline__ uint32_t quad_mask(float4 co, float4 pre, float2 m, i
 }
 
 // The quad masks of a single-frame list, in place: the scatter leaves each entry's tile in its qmask
-// word, and this flat pass (all of the list's entries at full occupancy, 4 per thread in flight;
-// the scatter itself runs one workgroup per 256 Gaussians at one frame, latency-bound, and computing
-// the masks there cost it 2.4x) replaces it with quad_mask.
+// word, and this flat pass replaces it with quad_mask.  The box tests run on (entry, strip) pairs
+// compacted across the wave (an entry keeps ~1.2 of its 4 strips): each wave stages its 64 entries'
+// conic, mean and strip origins in LDS, lists the pairs, and evaluates quad_reach4 on 64 pairs at a
+// time -- one pass per kept strip instead of the wave running every strip any lane keeps.  (The
+// scatter itself runs one workgroup per 256 Gaussians at one frame, latency-bound; computing the
+// masks there cost it 2.4x.)
 __global__ __launch_bounds__(256) void k_quad_masks(Dims d, GeomArena g, BinArena bn) {
+    __shared__ float4 s_co[4][64], s_pre[4][64];
+    __shared__ float2 s_m[4][64];
+    __shared__ int2 s_org[4][64];         // tile (tx, ty) of the entry
+    __shared__ uint32_t s_pair[4][256];   // (lane | strip << 8) per pair
+    __shared__ uint32_t s_bits[4][64];
     if (g.ctrl[kCtrlOverflow]) return;
     const uint32_t R = g.ctrl[kCtrlRLo];  // (one frame: the list length)
-    const uint32_t stride = gridDim.x * 256u * 4u;
-    for (uint32_t p0 = blockIdx.x * 1024u + threadIdx.x; p0 < R; p0 += stride) {
-        uint32_t e[4], t[4];
-#pragma unroll
-        for (int u = 0; u < 4; u++) {
-            const uint32_t p = p0 + 256u * u;
-            e[u] = p < R ? bn.point_list[p] : 0u;
-            t[u] = p < R ? bn.qmask[p] : 0u;
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    for (uint32_t p0 = (blockIdx.x * 4u + (uint32_t)wv) * 64u; p0 < R; p0 += gridDim.x * 256u) {
+        const uint32_t p = p0 + (uint32_t)lane;
+        const uint32_t e = p < R ? bn.point_list[p] : 0u;
+        const uint32_t t = p < R ? bn.qmask[p] : 0u;
+        const uint32_t sm = e >> 28;
+        if (sm) {
+            const int64_t gi = (int64_t)(e & kIndexMask);
+            const float4 r0 = g.rrec[2 * gi], r1 = g.rrec[2 * gi + 1];
+            // the scatter's conic / opacity / mean of the render record (exact rescaling)
+            const float4 co = make_float4(-2.0f * r1.x, -r1.y, -2.0f * r1.z, r0.z);
+            s_co[wv][lane] = co;
+            s_pre[wv][lane] = strip_pre(co);
+            s_m[wv][lane] = make_float2(r0.x, r0.y);
+            s_org[wv][lane] = make_int2((int)(t % (uint32_t)d.gx), (int)(t / (uint32_t)d.gx));
         }
-        float4 r0[4], r1[4];
+        s_bits[wv][lane] = 0u;
+        // the wave's (entry, strip) pairs
+        uint32_t np = 0;
 #pragma unroll
-        for (int u = 0; u < 4; u++) {
-            const int64_t gi = (int64_t)(e[u] & kIndexMask);
-            r0[u] = (e[u] >> 28) ? g.rrec[2 * gi] : make_float4(0.f, 0.f, 0.f, 0.f);
-            r1[u] = (e[u] >> 28) ? g.rrec[2 * gi + 1] : make_float4(0.f, 0.f, 0.f, 0.f);
-        }
-#pragma unroll
-        for (int u = 0; u < 4; u++) {
-            const uint32_t p = p0 + 256u * u;
-            if (p >= R) continue;
-            const uint32_t sm = e[u] >> 28;
-            uint32_t mask = 0;
-            if (sm) {
-                // the scatter's conic / opacity / mean of the render record (exact rescaling)
-                const float4 co = make_float4(-2.0f * r1[u].x, -r1[u].y, -2.0f * r1[u].z, r0[u].z);
-                mask = quad_mask(co, strip_pre(co), make_float2(r0[u].x, r0[u].y), (int)t[u] % d.gx,
-                                 (int)t[u] / d.gx, sm);
+        for (int st = 0; st < kStrips; st++) {
+            const bool has = (sm >> st) & 1u;
+            const uint64_t bm = __ballot(has);
+            if (has) {
+                const uint32_t rk = __builtin_amdgcn_mbcnt_hi((uint32_t)(bm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bm, 0u));
+                s_pair[wv][np + rk] = (uint32_t)lane | ((uint32_t)st << 8);
             }
-            bn.qmask[p] = mask;
+            np += (uint32_t)__popcll(bm);
         }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        for (uint32_t k0 = 0; k0 < np; k0 += 64u) {
+            if (k0 + (uint32_t)lane < np) {
+                const uint32_t pr = s_pair[wv][k0 + lane];
+                const int l = (int)(pr & 0xFFu), st = (int)(pr >> 8);
+                const float4 co = s_co[wv][l], pre = s_pre[wv][l];
+                uint32_t qb;
+                if (__builtin_bit_cast(uint32_t, pre.w) == 2u) {
+                    qb = 0xFu;
+                } else {
+                    const int2 og = s_org[wv][l];
+                    int sx0, sy0;
+                    strip_origin(og.x, og.y, st, sx0, sy0);
+                    qb = quad_reach4(co.x, co.y, co.z, pre.x, pre.y, pre.z, s_m[wv][l], (float)sx0, (float)sy0);
+                }
+                atomicOr(&s_bits[wv][l], qb << (4 * st));
+            }
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        if (p < R) bn.qmask[p] = s_bits[wv][lane];
+        __builtin_amdgcn_wave_barrier();
     }
 }
 
