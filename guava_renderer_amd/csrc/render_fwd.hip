@@ -369,7 +369,7 @@ __device__ __forceinline__ void render_fwd_body(const Dims& d, const Inputs& in,
                                               1.0f, 0.f, 0u);
                 }
             }
-            if (TL && lane == 0 && item < o.timeline_cap) {  // empty tiles: k-steps 0xFFFFFFFF
+            if (TL && lane == 0 && item < (o.timeline_cap & 0x7FFFFFFFu)) {  // empty tiles: k-steps 0xFFFFFFFF
                 uint32_t* rec = o.timeline + 4 * (size_t)item;
                 rec[0] = (uint32_t)te_start;
                 rec[1] = (uint32_t)__builtin_amdgcn_s_memrealtime();
@@ -686,7 +686,7 @@ __device__ __forceinline__ void render_fwd_body(const Dims& d, const Inputs& in,
                 }
             }
         }
-        if (TL && lane == 0 && item < o.timeline_cap) {  // (start, end) in 100 MHz ticks, k-steps, XCC
+        if (TL && lane == 0 && item < (o.timeline_cap & 0x7FFFFFFFu)) {  // (start, end) in 100 MHz ticks, k-steps, XCC
             const uint64_t t_end = __builtin_amdgcn_s_memrealtime();
             uint32_t* rec = o.timeline + 4 * (size_t)item;
             rec[0] = (uint32_t)t_start;
@@ -835,6 +835,7 @@ __global__ __launch_bounds__(GSR_TILE_PIX) __attribute__((amdgpu_waves_per_eu(GS
         }
         const uint64_t t_start = TL ? __builtin_amdgcn_s_memrealtime() : 0;
         uint32_t n_steps = 0, n_refills = 0, n_walk = 0;
+        uint64_t ph_issue = 0, ph_alpha = 0, ph_blend = 0;
         const uint32_t code = im.strip_list[item >> 2];
         const int quad = (int)(item & 3u);
         const int tile_g = (int)(code >> 2);
@@ -925,11 +926,23 @@ __global__ __launch_bounds__(GSR_TILE_PIX) __attribute__((amdgpu_waves_per_eu(GS
             // channels j and 16 + j), from global memory two steps ahead of their use
             auto records = [&](uint32_t h, float4& r0, float4& r1, float& f0, float& f1) {
                 const uint32_t gi = qg[(h + (uint32_t)qq) & (kQRing - 1)];
+#ifdef GSR_QUAD_ABL_NOLOAD  /* timing ablation (A/B builds only, wrong images): no operand loads */
+                r0 = make_float4(pfx + 0.5f * (float)(gi & 7u), pfy + 0.5f, 0.5f, 1.0f);
+                r1 = make_float4(-0.05f, 0.01f, -0.05f, __uint_as_float(gi));
+                f0 = (float)(gi & 3u);
+                f1 = f0;
+#else
                 r0 = rec_load(rrs, gi * 32u);
                 r1 = rec_load(rrs, gi * 32u + 16u);
+#ifdef GSR_QUAD_ABL_NOFEAT  /* timing ablation (A/B builds only, wrong images): no feature loads */
+                f0 = (float)(gi & 3u);
+                f1 = f0;
+#else
                 const uint32_t fo = gi * (uint32_t)(GSR_C * 4) + (uint32_t)j * 4u;
                 f0 = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(frs, (int)fo, 0, 0));
                 f1 = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(frs, (int)(fo + 64u), 0, 0));
+#endif
+#endif
             };
             auto positions = [&](uint32_t h) { return *reinterpret_cast<const uint4*>(&qpos[h & (kQRing - 1)]); };
             ensure();
@@ -943,6 +956,10 @@ __global__ __launch_bounds__(GSR_TILE_PIX) __attribute__((amdgpu_waves_per_eu(GS
             uint4 p4 = positions(head);
             float al = alpha_of<EXACT>(pr0[0], pr1[0], pfx, pfy);
             while (head < tail) {
+                // (TL: core-clock sums of the step's phases -- operand issue incl. refills, the next
+                // alpha (its records' wait), this step's blend + MFMAs)
+                uint64_t c0 = 0, c1 = 0, c2 = 0;
+                if (TL) { __builtin_amdgcn_sched_barrier(0); c0 = __builtin_amdgcn_s_memtime(); __builtin_amdgcn_sched_barrier(0); }
                 // the operands of the step after next first (their loads run under this step's blend)
                 ensure();
                 __builtin_amdgcn_wave_barrier();
@@ -950,9 +967,15 @@ __global__ __launch_bounds__(GSR_TILE_PIX) __attribute__((amdgpu_waves_per_eu(GS
                 float nnf0, nnf1;
                 records(head + 4u * AHEAD, nnr0, nnr1, nnf0, nnf1);
                 const uint4 np4 = positions(head + 4u);
+                if (TL) { __builtin_amdgcn_sched_barrier(0); c1 = __builtin_amdgcn_s_memtime(); __builtin_amdgcn_sched_barrier(0); }
                 // the next step's alpha (independent of this step's transmittance chain, so the two
                 // interleave: a lone tail wave is latency-bound, one dependent instruction after another)
                 const float nal = alpha_of<EXACT>(pr0[1 % AHEAD], pr1[1 % AHEAD], pfx, pfy);
+                if (TL) {
+                    __builtin_amdgcn_sched_barrier(0);
+                    c2 = __builtin_amdgcn_s_memtime() + (uint64_t)(__float_as_uint(nal) & 0u);
+                    __builtin_amdgcn_sched_barrier(0);
+                }
                 const float4 r0 = pr0[0];
                 const float f0 = pf0[0], f1 = pf1[0];
                 // this step
@@ -975,7 +998,15 @@ __global__ __launch_bounds__(GSR_TILE_PIX) __attribute__((amdgpu_waves_per_eu(GS
                 qa0 = __builtin_amdgcn_mfma_f32_16x16x4f32(f0, wq, qa0, 0, 0, 0);
                 qa1 = __builtin_amdgcn_mfma_f32_16x16x4f32(f1, wq, qa1, 0, 0, 0);
                 head += 4u;
-                if (TL) n_steps++;
+                if (TL) {
+                    __builtin_amdgcn_sched_barrier(0);
+                    const uint64_t c3 = __builtin_amdgcn_s_memtime() + (uint64_t)(__float_as_uint(qa0[0] + qa1[0]) & 0u);
+                    __builtin_amdgcn_sched_barrier(0);
+                    n_steps++;
+                    ph_issue += c1 - c0;
+                    ph_alpha += c2 - c1;
+                    ph_blend += c3 - c2;
+                }
 #pragma unroll
                 for (int k = 0; k + 1 < AHEAD; k++) {
                     pr0[k] = pr0[k + 1]; pr1[k] = pr1[k + 1]; pf0[k] = pf0[k + 1]; pf1[k] = pf1[k + 1];
@@ -987,13 +1018,20 @@ __global__ __launch_bounds__(GSR_TILE_PIX) __attribute__((amdgpu_waves_per_eu(GS
             }
             if (TL) n_walk = (uint32_t)min(base, n);
         }
-        if (TL && lane == 0 && item < o.timeline_cap) {
+        if (TL && lane == 0 && item < (o.timeline_cap & 0x7FFFFFFFu)) {
             const uint64_t t_end = __builtin_amdgcn_s_memrealtime();
             uint32_t* rec = o.timeline + 4 * (size_t)item;
             rec[0] = (uint32_t)t_start;
             rec[1] = (uint32_t)t_end;
             rec[2] = min(n_steps, 0xFFFFu) | (min(n_refills, 0xFFFFu) << 16);
             rec[3] = n_walk;
+            if (o.timeline_cap & 0x80000000u) {  // phase sums requested: a second block of records
+                uint32_t* ph = o.timeline + 4 * (size_t)(o.timeline_cap & 0x7FFFFFFFu) + 4 * (size_t)item;
+                ph[0] = (uint32_t)ph_issue;
+                ph[1] = (uint32_t)ph_alpha;
+                ph[2] = (uint32_t)ph_blend;
+                ph[3] = 0u;
+            }
         }
         // epilogue: group 0 stores final_T / n_contrib / inverse depth, every lane its channels
         // 4 qq + r and 16 + 4 qq + r of pixel j

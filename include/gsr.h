@@ -270,7 +270,10 @@ int gsr_profile_read(double* ms, int* counts, int n);
 int gsr_render_counters(uint64_t* device_counters);
 /* Work-item timeline of the render kernel (a lightly instrumented variant runs while set):
  * record i (4 uint32: start, end in 100 MHz ticks, MFMA k-steps, XCD) for the first `capacity`
- * work items in longest-first order (strip items first, 4 per non-empty tile). */
+ * work items in longest-first order (strip items first, 4 per non-empty tile).  Single-frame quad
+ * waves: (start, end, steps | refills << 16, list entries walked); with capacity | 0x80000000 they
+ * also write, after the `capacity` records, 4 uint32 of core-clock sums per item (operand issue,
+ * next-step alpha, blend + MFMA), so the buffer must then hold 8 x capacity words. */
 int gsr_render_timeline(uint32_t* device_records, uint32_t capacity);
 
 /* Byte offset, inside a batch workspace, of its 4 sticky status words (uint32): [0] = 1 once any

@@ -36,18 +36,20 @@ a = {"xyz": dg["xyz"], "rotation": dg["rotation"], "scaling": dg["scaling"],
      "opacity": pipe.gauss.opacity.unsqueeze(0), "features_color": pipe.gauss.colors.unsqueeze(0)}
 L = _lib.load()
 cap = 1 << 16
-buf = torch.zeros((cap * 4,), dtype=torch.int32, device=dev)
+buf = torch.zeros((cap * 8,), dtype=torch.int32, device=dev)  # records, then the quad kernel's phase sums
 with torch.no_grad():
     for _ in range(5):
         bench._render_model(a, cam, 1, dev, GaussianRasterizationSettings, GaussianRasterizer_32)
     torch.cuda.synchronize()
-    L.gsr_render_timeline(buf.data_ptr(), cap)
+    L.gsr_render_timeline(buf.data_ptr(), cap | 0x80000000)  # (records + phase sums)
     bench._render_model(a, cam, 1, dev, GaussianRasterizationSettings, GaussianRasterizer_32)
     torch.cuda.synchronize()
     L.gsr_render_timeline(None, 0)
-r = buf.view(cap, 4).cpu().numpy().astype(np.int64) & 0xFFFFFFFF
+allr = buf.view(2 * cap, 4).cpu().numpy().astype(np.int64) & 0xFFFFFFFF
+r, ph = allr[:cap], allr[cap:]
 used = (r[:, 0] != 0) | (r[:, 1] != 0)
 r = r[used]
+ph = ph[used]
 idx = np.nonzero(used)[0]
 t0 = r[:, 0].min()
 start, end = (r[:, 0] - t0) * 10.0, (r[:, 1] - t0) * 10.0  # ns (100 MHz ticks)
@@ -72,3 +74,8 @@ late = start > 60000
 if late.any():
     coef2 = np.linalg.lstsq(A[late], dur[late], rcond=None)[0]
     print(f"items starting after 60 us ({late.sum()}): {coef2[0]:.0f} ns/step + {coef2[1]:.0f} ns/refill + {coef2[2]:.0f}")
+ph_steps = np.maximum(steps, 1)[:, None]
+lt = np.argsort(-end)[:20]
+print("latest-ending 20 items, core cycles per step: issue+refill %.0f, next alpha (records' wait) %.0f, "
+      "blend+MFMA %.0f" % tuple((ph[lt, :3] / ph_steps[lt]).mean(0)))
+print("all items: %.0f / %.0f / %.0f cycles per step" % tuple(ph[:, :3].sum(0) / max(steps.sum(), 1)))

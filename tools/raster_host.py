@@ -94,3 +94,15 @@ with torch.no_grad():
     t2 = time.perf_counter()
     print(f"rasterizer call alone: issue {1e6 * (t1 - t0) / N:6.1f} us/call (inside C {1e6 * acc['c'] / N:6.1f}), "
           f"GPU-bound total {1e6 * (t2 - t0) / N:6.1f} us/call", flush=True)
+
+# cProfile of the rasterizer call alone (Python side; the C call counts as the caller's own time)
+import cProfile  # noqa: E402
+import pstats  # noqa: E402
+with torch.no_grad():
+    pr = cProfile.Profile()
+    pr.enable()
+    for _ in range(N):
+        r(**args)
+    pr.disable()
+    torch.cuda.synchronize()
+pstats.Stats(pr).sort_stats("tottime").print_stats(25)
