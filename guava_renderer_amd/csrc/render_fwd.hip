@@ -765,10 +765,18 @@ __global__ __launch_bounds__(GSR_TILE_PIX) __attribute__((amdgpu_waves_per_eu(4)
 #ifndef GSR_QUAD_WPE
 #define GSR_QUAD_WPE 3  // (the 3-deep operand pipeline's registers: 4 waves would spill; measured -4%)
 #endif
-#ifndef GSR_QUAD_AHEAD
-#define GSR_QUAD_AHEAD 3  // steps between a step's record / feature loads and their use (>= 2)
+#ifndef GSR_QUAD_SLOTS
+#define GSR_QUAD_SLOTS 4  // operand slots: a step's record / feature loads are issued 3 steps before their use
 #endif
-constexpr int kQRing = 512;  // ring entries per wave (a refill adds <= 256 and runs below 12)
+template <int K>
+struct QSlot {
+    static constexpr int k = K;
+};
+#ifndef GSR_QUAD_RCH
+#define GSR_QUAD_RCH 4  // 64-entry list chunks per refill
+#endif
+constexpr int kQRch = GSR_QUAD_RCH;
+constexpr int kQRing = kQRch <= 4 ? 512 : 1024;  // ring entries per wave (a refill adds <= 64 kQRch and runs below 12)
 constexpr uint32_t kQNull = 0x07FFFFFFu;  // the null Gaussian: record / feature offsets out of range
 
 // TL (gsr_render_timeline): per quad item, (start, end) in 100 MHz ticks, steps | refills << 16, list
@@ -870,20 +878,20 @@ __global__ __launch_bounds__(GSR_TILE_PIX) __attribute__((amdgpu_waves_per_eu(GS
             const uint32_t* __restrict__ qm = bn.qmask + range.x;
             int base = 0;                  // first list position of the next refill
             uint32_t head = 0, tail = 0;   // ring counters (head advances by 4: entries never wrap in a step)
-            uint32_t ec[4], mc[4], en[4], mn[4];
-            auto load_chunks = [&](int b0, uint32_t (&e)[4], uint32_t (&m)[4]) {
+            uint32_t ec[kQRch], mc[kQRch], en[kQRch], mn[kQRch];
+            auto load_chunks = [&](int b0, uint32_t (&e)[kQRch], uint32_t (&m)[kQRch]) {
 #pragma unroll
-                for (int u = 0; u < 4; u++) {
+                for (int u = 0; u < kQRch; u++) {
                     const int p = b0 + 64 * u + lane;
                     e[u] = p < n ? plist[p] : 0u;
                     m[u] = p < n ? (uint32_t)qm[p] : 0u;  // (zero past the list's end: nothing kept)
                 }
             };
             load_chunks(0, ec, mc);
-            load_chunks(256, en, mn);
+            load_chunks(64 * kQRch, en, mn);
             auto refill = [&]() {
 #pragma unroll
-                for (int u = 0; u < 4; u++) {
+                for (int u = 0; u < kQRch; u++) {
                     const bool keep = ((mc[u] >> qbit) & 1u) != 0u;
                     const uint64_t km = __ballot(keep);
                     if (keep) {
@@ -895,26 +903,26 @@ __global__ __launch_bounds__(GSR_TILE_PIX) __attribute__((amdgpu_waves_per_eu(GS
                     }
                     tail += (uint32_t)__builtin_popcountll(km);
                 }
-                base += 256;
+                base += 64 * kQRch;
                 if (TL) n_refills++;
 #pragma unroll
-                for (int u = 0; u < 4; u++) {
+                for (int u = 0; u < kQRch; u++) {
                     ec[u] = en[u];
                     mc[u] = mn[u];
                 }
-                load_chunks(base + 256, en, mn);
+                load_chunks(base + 64 * kQRch, en, mn);
                 __builtin_amdgcn_wave_barrier();
             };
-            // fill so that entries [head, head + 4 (GSR_QUAD_AHEAD + 1)) exist; once the list is
+            // fill so that entries [head, head + 4 GSR_QUAD_SLOTS) exist; once the list is
             // exhausted, the ring slots past its last entry hold the null Gaussian (an index whose record and feature
             // offsets are out of range: zeros, opacity 0, nothing taken), so the step operands are read
             // without a validity branch
             bool nulled = false;
             auto ensure = [&]() {
-                while (tail - head < 4u * (GSR_QUAD_AHEAD + 1) && base < n) refill();
+                while (tail - head < 4u * GSR_QUAD_SLOTS && base < n) refill();
                 if (base >= n && !nulled) {
                     nulled = true;
-                    if (lane < 4 * (GSR_QUAD_AHEAD + 1)) {
+                    if (lane < 4 * GSR_QUAD_SLOTS) {
                         const uint32_t slot = (tail + (uint32_t)lane) & (kQRing - 1);
                         qg[slot] = kQNull;
                         qpos[slot] = 0u;
@@ -923,7 +931,7 @@ __global__ __launch_bounds__(GSR_TILE_PIX) __attribute__((amdgpu_waves_per_eu(GS
                 }
             };
             // one step's render records (lane group qq: ring entry h + qq) and feature words (A operands:
-            // channels j and 16 + j), from global memory two steps ahead of their use
+            // channels j and 16 + j), from global memory GSR_QUAD_SLOTS - 1 steps ahead of their use
             auto records = [&](uint32_t h, float4& r0, float4& r1, float& f0, float& f1) {
                 const uint32_t gi = qg[(h + (uint32_t)qq) & (kQRing - 1)];
 #ifdef GSR_QUAD_ABL_NOLOAD  /* timing ablation (A/B builds only, wrong images): no operand loads */
@@ -947,42 +955,46 @@ __global__ __launch_bounds__(GSR_TILE_PIX) __attribute__((amdgpu_waves_per_eu(GS
             auto positions = [&](uint32_t h) { return *reinterpret_cast<const uint4*>(&qpos[h & (kQRing - 1)]); };
             ensure();
             __builtin_amdgcn_wave_barrier();
-            // operand pipeline: slot k holds step head + 4k's records and feature words (k < AHEAD)
-            constexpr int AHEAD = GSR_QUAD_AHEAD;
-            float4 pr0[AHEAD], pr1[AHEAD];
-            float pf0[AHEAD], pf1[AHEAD];
+            // operand pipeline of GSR_QUAD_SLOTS slots: step i's records and feature words sit in slot
+            // i % NS, loaded NS - 1 steps ahead (step i issues step i + NS - 1's loads into the slot step
+            // i - 1 freed).  The step loop is unrolled by NS so that every slot is one fixed set of
+            // registers: a rotated array compiles to register copies, and a copy of a register whose
+            // load is still in flight waits for it (s_waitcnt vmcnt(0) every step: no prefetch at all).
+            constexpr int NS = GSR_QUAD_SLOTS;
+            float4 pr0[NS], pr1[NS];
+            float pf0[NS], pf1[NS];
 #pragma unroll
-            for (int k = 0; k < AHEAD; k++) records(head + 4u * k, pr0[k], pr1[k], pf0[k], pf1[k]);
+            for (int k = 0; k + 1 < NS; k++) records(head + 4u * k, pr0[k], pr1[k], pf0[k], pf1[k]);
             uint4 p4 = positions(head);
             float al = alpha_of<EXACT>(pr0[0], pr1[0], pfx, pfy);
-            while (head < tail) {
+            auto step = [&](auto slot) {
+                constexpr int c = decltype(slot)::k;
+                constexpr int nx = (c + 1) % NS, ld = (c + NS - 1) % NS;
                 // (TL: core-clock sums of the step's phases -- operand issue incl. refills, the next
                 // alpha (its records' wait), this step's blend + MFMAs)
                 uint64_t c0 = 0, c1 = 0, c2 = 0;
                 if (TL) { __builtin_amdgcn_sched_barrier(0); c0 = __builtin_amdgcn_s_memtime(); __builtin_amdgcn_sched_barrier(0); }
-                // the operands of the step after next first (their loads run under this step's blend)
+                // the operands of step i + NS - 1 first (their loads run under this step and the next ones)
                 ensure();
                 __builtin_amdgcn_wave_barrier();
-                float4 nnr0, nnr1;
-                float nnf0, nnf1;
-                records(head + 4u * AHEAD, nnr0, nnr1, nnf0, nnf1);
+                records(head + 4u * (NS - 1), pr0[ld], pr1[ld], pf0[ld], pf1[ld]);
                 const uint4 np4 = positions(head + 4u);
                 if (TL) { __builtin_amdgcn_sched_barrier(0); c1 = __builtin_amdgcn_s_memtime(); __builtin_amdgcn_sched_barrier(0); }
                 // the next step's alpha (independent of this step's transmittance chain, so the two
                 // interleave: a lone tail wave is latency-bound, one dependent instruction after another)
-                const float nal = alpha_of<EXACT>(pr0[1 % AHEAD], pr1[1 % AHEAD], pfx, pfy);
+                const float nal = alpha_of<EXACT>(pr0[nx], pr1[nx], pfx, pfy);
                 if (TL) {
                     __builtin_amdgcn_sched_barrier(0);
                     c2 = __builtin_amdgcn_s_memtime() + (uint64_t)(__float_as_uint(nal) & 0u);
                     __builtin_amdgcn_sched_barrier(0);
                 }
-                const float4 r0 = pr0[0];
-                const float f0 = pf0[0], f1 = pf1[0];
+                const float rw = pr0[c].w;
+                const float f0 = pf0[c], f1 = pf1[c];
                 // this step
                 const auto a16 = __builtin_amdgcn_permlane16_swap(__float_as_uint(al), __float_as_uint(al), false, false);
                 const auto a02 = __builtin_amdgcn_permlane32_swap(a16[0], a16[0], false, false);
                 const auto a13 = __builtin_amdgcn_permlane32_swap(a16[1], a16[1], false, false);
-                const auto i16 = __builtin_amdgcn_permlane16_swap(__float_as_uint(r0.w), __float_as_uint(r0.w), false,
+                const auto i16 = __builtin_amdgcn_permlane16_swap(__float_as_uint(rw), __float_as_uint(rw), false,
                                                                   false);
                 const auto i02 = __builtin_amdgcn_permlane32_swap(i16[0], i16[0], false, false);
                 const auto i13 = __builtin_amdgcn_permlane32_swap(i16[1], i16[1], false, false);
@@ -1007,14 +1019,18 @@ __global__ __launch_bounds__(GSR_TILE_PIX) __attribute__((amdgpu_waves_per_eu(GS
                     ph_alpha += c2 - c1;
                     ph_blend += c3 - c2;
                 }
-#pragma unroll
-                for (int k = 0; k + 1 < AHEAD; k++) {
-                    pr0[k] = pr0[k + 1]; pr1[k] = pr1[k + 1]; pf0[k] = pf0[k + 1]; pf1[k] = pf1[k + 1];
-                }
-                pr0[AHEAD - 1] = nnr0; pr1[AHEAD - 1] = nnr1; pf0[AHEAD - 1] = nnf0; pf1[AHEAD - 1] = nnf1;
                 p4 = np4;
                 al = nal;
-                if (!__any(!done)) break;  // every pixel of the quad finished
+                return head < tail && __any(!done);  // (false: the list is done or every pixel of the quad finished)
+            };
+            static_assert(NS == 3 || NS == 4, "GSR_QUAD_SLOTS");
+            while (head < tail) {
+                if (!step(QSlot<0>{})) break;
+                if (!step(QSlot<1>{})) break;
+                if (!step(QSlot<2>{})) break;
+                if constexpr (NS == 4) {
+                    if (!step(QSlot<3 % NS>{})) break;
+                }
             }
             if (TL) n_walk = (uint32_t)min(base, n);
         }
