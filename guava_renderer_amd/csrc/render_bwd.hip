@@ -58,6 +58,11 @@ __device__ __forceinline__ bf16x8 bf8(unsigned a, unsigned b, unsigned c, unsign
     return __builtin_bit_cast(bf16x8, (uint4x){a, b, c, d});
 }
 
+// 16 bytes at byte offset off of a buffer resource (zeros outside its range)
+__device__ __forceinline__ float4 bwd_load16(__amdgpu_buffer_rsrc_t rs, uint32_t off) {
+    return __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rs, (int)off, 0, 0));
+}
+
 // lane l's value summed with lane l^32's
 __device__ __forceinline__ float add_halves(float x) {
     const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
@@ -114,10 +119,14 @@ __global__ __launch_bounds__(GSR_TILE_PIX) __attribute__((amdgpu_waves_per_eu(2)
         const float pfx = (float)px, pfy = (float)py;
         const uint32_t smask_bit = 1u << (28 + strip);
         const uint2 range = im.ranges[tile_g];
-        const uint32_t* __restrict__ plist = bn.point_list + range.x;
-        const float4* __restrict__ rrec = g.rrec + (int64_t)b * d.P * 2;
-        const float* __restrict__ colors = SPLIT == 2 ? reinterpret_cast<const float*>(g.fsplit)
-                                                      : in.colors + in.s_colors * b;
+        const uint32_t* __restrict__ plist = bn.point_list + __builtin_amdgcn_readfirstlane(range.x);
+        // render records and feature rows through buffer resources (32-bit offsets, range-checked)
+        const __amdgpu_buffer_rsrc_t rrs = __builtin_amdgcn_make_buffer_rsrc(
+            (void*)(g.rrec + (int64_t)b * d.P * 2), 0, (int)min((int64_t)d.P * 32, (int64_t)0x7FFFFFFF), 0x00020000);
+        const __amdgpu_buffer_rsrc_t frs = __builtin_amdgcn_make_buffer_rsrc(
+            SPLIT == 2 ? (void*)g.fsplit : (void*)(in.colors + in.s_colors * b), 0,
+            (int)min((int64_t)d.P * GSR_C * 4, (int64_t)0x7FFFFFFF), 0x00020000);
+        constexpr uint32_t kOOB = 0x80000000u;
         const int64_t gbase = (int64_t)b * d.P;
         const int64_t cbase = gr.reduce ? 0 : gbase;  // frame-reduced colour gradients: one [P][C] block
 
@@ -174,15 +183,26 @@ __global__ __launch_bounds__(GSR_TILE_PIX) __attribute__((amdgpu_waves_per_eu(2)
         // ---- survivor stream: chunks of 64 list positions, last chunk first (the next lower chunk
         // prefetched); survivors appended to the ring in back-to-front order
         int base = (int)((ns - 1) & ~63u) + 64;
-        uint32_t nidx = base - 64 + lane < (int)ns ? plist[base - 64 + lane] : 0u;
+        // list entries through a buffer resource: the prefetch below is one unconditional load (an
+        // out-of-range offset reads 0), so it lands in nidx's own register -- a conditional load
+        // merged into it by a register copy would wait for the load right after issuing it
+        const __amdgpu_buffer_rsrc_t lrs = __builtin_amdgcn_make_buffer_rsrc(
+            (void*)plist, 0, (int)(ns * 4u), 0x00020000);
+        auto list_load = [&](int pos) {
+            return __builtin_amdgcn_raw_buffer_load_b32(lrs, pos >= 0 ? (int)((uint32_t)pos * 4u) : (int)kOOB, 0, 0);
+        };
+        uint32_t nidx = list_load(base - 64 + lane);
         uint32_t head = 0, tail = 0;  // wave-uniform ring counters
         bool list_done = false;
         auto fill = [&](uint32_t want) {
+            bool first = true;
             while (!list_done && tail - head < want) {
                 base -= 64;
                 if (base < 0) { list_done = true; break; }
-                const uint32_t cidx = nidx;
-                if (base >= 64) nidx = plist[base - 64 + lane];
+                // the prefetched chunk; a second chunk in the same fill is loaded here
+                uint32_t cidx = nidx;
+                if (!first) cidx = list_load(base + lane);
+                first = false;
                 const bool sv = base + lane < (int)ns && (cidx & smask_bit) != 0u;
                 const uint64_t m = __ballot(sv);
                 if (sv) {
@@ -194,6 +214,11 @@ __global__ __launch_bounds__(GSR_TILE_PIX) __attribute__((amdgpu_waves_per_eu(2)
                 }
                 tail += (uint32_t)__popcll(m);
             }
+            // the next lower chunk, one unconditional load at the end (the same chunk again when
+            // none was used), in flight until the next fill: a load merged into nidx on some
+            // paths only would reach it through a register copy that waits for the load at once
+            __builtin_amdgcn_sched_barrier(0);
+            nidx = list_load(base - 64 + lane);  // (0 below the list's start)
             wave_lds_order();
         };
         // a batch, lane-distributed: lane l holds survivor l&31's index and list position, its
@@ -206,27 +231,29 @@ __global__ __launch_bounds__(GSR_TILE_PIX) __attribute__((amdgpu_waves_per_eu(2)
             g_o = valid ? ring_g[slot] : 0u;
             p_o = valid ? ring_p[slot] : 0xFFFFFFFFu;
             head += nb_o;
-            if (valid) {
-                ra_o = rrec[2 * g_o];
-                rc_o = rrec[2 * g_o + 1];
-                const float4* fsrc = reinterpret_cast<const float4*>(colors + (int64_t)g_o * GSR_C + 16 * hi);
+            // branch-free loads (every path issues the same six, so the compiler can count them
+            // in its waits): an invalid lane's offsets fall outside the resources and read zeros
+            const uint32_t ro = valid ? g_o * 32u : kOOB;
+            ra_o = bwd_load16(rrs, ro);
+            rc_o = bwd_load16(rrs, ro + 16u);
+            const uint32_t fo = valid ? g_o * (uint32_t)(GSR_C * 4) + 64u * (uint32_t)hi : kOOB;
 #pragma unroll
-                for (int u = 0; u < 4; u++) {
-                    const float4 v = fsrc[u];
-                    f_o[4 * u] = v.x; f_o[4 * u + 1] = v.y; f_o[4 * u + 2] = v.z; f_o[4 * u + 3] = v.w;
-                }
-            } else {
-                ra_o = make_float4(0.f, 0.f, 0.f, 0.f);
-                rc_o = ra_o;
-#pragma unroll
-                for (int u = 0; u < 16; u++) f_o[u] = 0.f;
+            for (int u = 0; u < 4; u++) {
+                const float4 v = bwd_load16(frs, fo + 16u * (uint32_t)u);
+                f_o[4 * u] = v.x; f_o[4 * u + 1] = v.y; f_o[4 * u + 2] = v.z; f_o[4 * u + 3] = v.w;
             }
         };
-        uint32_t nb, bg_, bp_;
-        float4 ra_, rc_;
-        float fr[16];
+        // a batch's operands; two of them, used in turn (the batch loop below is unrolled by two so
+        // that each is one fixed set of registers: a rotated copy would wait for the next batch's
+        // loads right after issuing them)
+        struct Batch {
+            uint32_t nb, g, p;
+            float4 ra, rc;
+            float fr[16];
+        };
+        Batch bA, bB;
         fill(kBwdBatch);
-        pop(nb, bg_, bp_, ra_, rc_, fr);
+        pop(bA.nb, bA.g, bA.p, bA.ra, bA.rc, bA.fr);
 
         // strip-centred pixel offsets (exact in f32): the moments use lx = x - cx, ly = y - cy
         const float cx = (float)sx0 + 3.5f, cy = (float)sy0 + 3.5f;
@@ -234,19 +261,16 @@ __global__ __launch_bounds__(GSR_TILE_PIX) __attribute__((amdgpu_waves_per_eu(2)
         float T = T_final;
         float accum_dot = 0.f, last_gdot = 0.f, last_alpha = 0.f;
         float accum_inv = 0.f, last_inv = 0.f;
-        while (nb) {
+        auto run_batch = [&](Batch& cur, Batch& nxt) {
             // this batch's records to LDS (read back as wave-uniform values per slot), the list
             // position in the record's spare word
             if (lane < kBwdBatch) {
-                rl[2 * lane] = ra_;
-                rl[2 * lane + 1] = make_float4(rc_.x, rc_.y, rc_.z, __uint_as_float(bp_));
+                rl[2 * lane] = cur.ra;
+                rl[2 * lane + 1] = make_float4(cur.rc.x, cur.rc.y, cur.rc.z, __uint_as_float(cur.p));
             }
             // next batch: survivors into the ring, then its loads in flight during this batch
-            uint32_t nb_n, bg_n, bp_n;
-            float4 ra_n, rc_n;
-            float fr_n[16];
             fill(kBwdBatch);
-            pop(nb_n, bg_n, bp_n, ra_n, rc_n, fr_n);
+            pop(nxt.nb, nxt.g, nxt.p, nxt.ra, nxt.rc, nxt.fr);
 
             // g[s][px] = sum_ch f_s[ch] dL[ch][px]: f32 MFMA, A = f (row s), B = dL (column px)
             floatx16 gd0, gd1;
@@ -260,14 +284,14 @@ __global__ __launch_bounds__(GSR_TILE_PIX) __attribute__((amdgpu_waves_per_eu(2)
                 for (int k = 0; k < 16; k += 2) {
                     unsigned fh0, fl0, fh1, fl1;
                     if (SPLIT == 2) {  // (hi | lo) table words -> (hi | hi), (lo | lo)
-                        const unsigned t0 = __float_as_uint(fr[k]), t1 = __float_as_uint(fr[k + 1]);
+                        const unsigned t0 = __float_as_uint(cur.fr[k]), t1 = __float_as_uint(cur.fr[k + 1]);
                         fh0 = __builtin_amdgcn_perm(t0, t0, 0x01000100u);
                         fl0 = __builtin_amdgcn_perm(t0, t0, 0x03020302u);
                         fh1 = __builtin_amdgcn_perm(t1, t1, 0x01000100u);
                         fl1 = __builtin_amdgcn_perm(t1, t1, 0x03020302u);
                     } else {
-                        split_hh_ll(fr[k], fh0, fl0);
-                        split_hh_ll(fr[k + 1], fh1, fl1);
+                        split_hh_ll(cur.fr[k], fh0, fl0);
+                        split_hh_ll(cur.fr[k + 1], fh1, fl1);
                     }
                     const shortx4 ah = __builtin_bit_cast(shortx4, (uint2x){fh0, fh1});
                     const shortx4 al = __builtin_bit_cast(shortx4, (uint2x){fl0, fl1});
@@ -282,11 +306,11 @@ __global__ __launch_bounds__(GSR_TILE_PIX) __attribute__((amdgpu_waves_per_eu(2)
 #pragma unroll
             for (int k = 0; k < 16; k++) {
                 if (ABL == 5) {  /* timing ablation: VALU stand-in for the g contraction */
-                    gd0[k] = fmaf(fr[k], bh0[k], gd0[k]);
-                    gd1[k] = fmaf(fr[k], bh1[k], gd1[k]);
+                    gd0[k] = fmaf(cur.fr[k], bh0[k], gd0[k]);
+                    gd1[k] = fmaf(cur.fr[k], bh1[k], gd1[k]);
                 } else {
-                    gd0 = __builtin_amdgcn_mfma_f32_32x32x2f32(fr[k], bh0[k], gd0, 0, 0, 0);
-                    gd1 = __builtin_amdgcn_mfma_f32_32x32x2f32(fr[k], bh1[k], gd1, 0, 0, 0);
+                    gd0 = __builtin_amdgcn_mfma_f32_32x32x2f32(cur.fr[k], bh0[k], gd0, 0, 0, 0);
+                    gd1 = __builtin_amdgcn_mfma_f32_32x32x2f32(cur.fr[k], bh1[k], gd1, 0, 0, 0);
                 }
             }
             // to pixel lanes: gd0[r] = g of slot (r&3) + 8(r>>2), gd1[r] = of slot (r&3) + 8(r>>2) + 4
@@ -306,8 +330,8 @@ __global__ __launch_bounds__(GSR_TILE_PIX) __attribute__((amdgpu_waves_per_eu(2)
                 // group starts, so the scheduler sees whole groups); inside a group `act` drops them
                 if (ABL == 2) continue;
                 if (GSR_BWD_SLOT_GROUP == 1) {
-                    if ((uint32_t)s >= nb) continue;  // (not break: this loop must unroll -- static slots)
-                } else if ((s % GSR_BWD_SLOT_GROUP) == 0 && (uint32_t)s >= nb) {
+                    if ((uint32_t)s >= cur.nb) continue;  // (not break: this loop must unroll -- static slots)
+                } else if ((s % GSR_BWD_SLOT_GROUP) == 0 && (uint32_t)s >= cur.nb) {
                     break;
                 }
                 const float gdot = (s & 4) ? gd1[(s & 3) + 4 * (s >> 3)] : gd0[(s & 3) + 4 * (s >> 3)];
@@ -328,7 +352,7 @@ __global__ __launch_bounds__(GSR_TILE_PIX) __attribute__((amdgpu_waves_per_eu(2)
                     G = expf_fast(power);
                     alpha = fminf(0.99f, ra.z * G);
                 }
-                const bool act = (GSR_BWD_SLOT_GROUP == 1 || (uint32_t)s < nb) &&
+                const bool act = (GSR_BWD_SLOT_GROUP == 1 || (uint32_t)s < cur.nb) &&
                                  contributor < last_contributor && !(power > 0.0f) &&  // (outside: last 0)
                                  !(power < -87.0f) && !(alpha < 1.0f / 255.0f);
                 const float one_m = 1.f - alpha;
@@ -364,10 +388,10 @@ __global__ __launch_bounds__(GSR_TILE_PIX) __attribute__((amdgpu_waves_per_eu(2)
 
             // ---- flush: dL/dcolor[s][ch] = sum_px w[s][px] dL[px][ch] on the matrix cores (slot rows,
             // channel columns: each register's atomics cover two whole 128-byte feature rows)
-            if (ABL == 3) { nb = nb_n; bg_ = bg_n; bp_ = bp_n; ra_ = ra_n; rc_ = rc_n;
+            if (ABL == 3) {
 #pragma unroll
-                for (int u = 0; u < 16; u++) fr[u] = fr_n[u] + gd0[u] + gd1[u];
-                continue; }
+                for (int u = 0; u < 16; u++) nxt.fr[u] += gd0[u] + gd1[u];
+                return; }
             floatx16 acc;
 #pragma unroll
             for (int r = 0; r < 16; r++) acc[r] = 0.f;
@@ -417,26 +441,26 @@ __global__ __launch_bounds__(GSR_TILE_PIX) __attribute__((amdgpu_waves_per_eu(2)
 #pragma unroll
                 for (int r = 0; r < 16; r++) {
                     const uint32_t sl = (uint32_t)((r & 3) + 8 * (r >> 2) + 4 * hi);
-                    const uint32_t gsl = __builtin_amdgcn_readlane(bg_, (r & 3) + 8 * (r >> 2)) ;
-                    const uint32_t gsh = __builtin_amdgcn_readlane(bg_, (r & 3) + 8 * (r >> 2) + 4);
+                    const uint32_t gsl = __builtin_amdgcn_readlane(cur.g, (r & 3) + 8 * (r >> 2)) ;
+                    const uint32_t gsh = __builtin_amdgcn_readlane(cur.g, (r & 3) + 8 * (r >> 2) + 4);
                     const uint32_t gs = hi ? gsh : gsl;
                     // slots past the batch hold stale tiles; a zero sum (no pixel took the Gaussian,
                     // or no gradient) adds nothing
-                    if (sl < nb && acc[r] != 0.f) atomicAdd(gr.dL_dcolors + (cbase + gs) * GSR_C + l32, acc[r]);
+                    if (sl < cur.nb && acc[r] != 0.f) atomicAdd(gr.dL_dcolors + (cbase + gs) * GSR_C + l32, acc[r]);
                 }
             }
             // the other terms of slot l&31, from the pixel moments of u about the Gaussian's centre
             // (dx = X - lx, dy = Y - ly); lanes 0-31 write the slot's kGtWords row to LDS (the record
             // tile is free now), then 8 lanes per slot add it to the slot's gterm row
             {
-                const float X = ra_.x - cx, Y = ra_.y - cy;
+                const float X = cur.ra.x - cx, Y = cur.ra.y - cy;
                 const float Sdx = X * S0 - Sx;
                 const float Sdy = Y * S0 - Sy;
                 const float Sdxx = (X * X) * S0 - 2.f * X * Sx + Sxx;
                 const float Sdxy = (X * Y) * S0 - X * Sy - Y * Sx + Sxy;
                 const float Sdyy = (Y * Y) * S0 - 2.f * Y * Sy + Syy;
-                const float o = ra_.z;
-                const float ca = -2.0f * rc_.x, cb = -rc_.y, cc = -2.0f * rc_.z;  // conic a, b, c (exact)
+                const float o = cur.ra.z;
+                const float ca = -2.0f * cur.rc.x, cb = -cur.rc.y, cc = -2.0f * cur.rc.z;  // conic a, b, c (exact)
                 float* row = reinterpret_cast<float*>(rl) + 8 * l32;
                 if (!hi) {
                     // dL/dmean2D = sum dL/dG dG/ddelx ddelx/dx, dG/ddelx = -G (a dx + b dy)
@@ -458,17 +482,20 @@ __global__ __launch_bounds__(GSR_TILE_PIX) __attribute__((amdgpu_waves_per_eu(2)
 #pragma unroll
                 for (int qq = 0; qq < 4; qq++) {
                     const uint32_t sl = (uint32_t)(8 * qq + (lane >> 3));
-                    const uint32_t gs = (uint32_t)__shfl((int)bg_, (int)sl);
+                    const uint32_t gs = (uint32_t)__shfl((int)cur.g, (int)sl);
                     const float val = rows[8 * sl + (lane & 7)];
-                    if (sl < nb && val != 0.f && (lane & 7) != 7 && (INVD || (lane & 7) != kGtInv))
+                    if (sl < cur.nb && val != 0.f && (lane & 7) != 7 && (INVD || (lane & 7) != kGtInv))
                         atomicAdd(g.gterm + (gbase + gs) * kGtWords + (lane & 7), val);
                 }
             }
             wave_lds_order();
 
-            nb = nb_n; bg_ = bg_n; bp_ = bp_n; ra_ = ra_n; rc_ = rc_n;
-#pragma unroll
-            for (int u = 0; u < 16; u++) fr[u] = fr_n[u];
+        };
+        for (;;) {
+            if (!bA.nb) break;
+            run_batch(bA, bB);
+            if (!bB.nb) break;
+            run_batch(bB, bA);
         }
     }
 }
