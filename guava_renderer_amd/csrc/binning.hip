@@ -932,7 +932,10 @@ __global__ __launch_bounds__(256) void k_quad_masks(Dims d, GeomArena g, BinAren
 }
 
 void launch_quad_masks(const Dims& d, const GeomArena& g, const BinArena& b, hipStream_t s) {
-    if (b.qmask && d.B == 1 && d.P > 0) hipLaunchKernelGGL(k_quad_masks, dim3(1024), dim3(256), 0, s, d, g, b);
+    // 2048 workgroups: 8 per CU, every wave resident with about one 64-entry chunk (the pass is
+    // load-latency-bound; 1024 workgroups: 19.6 us per C2 frame, 2048: 17.4, 4096: 17.1; GSR_QMASK_WG A/B)
+    static const int wg = tune_env("GSR_QMASK_WG", 2048);
+    if (b.qmask && d.B == 1 && d.P > 0) hipLaunchKernelGGL(k_quad_masks, dim3(wg), dim3(256), 0, s, d, g, b);
 }
 
 // ---------------------------------------------------------------- 5. ordered scatter
