@@ -115,6 +115,13 @@ __global__ __launch_bounds__(256) void k_split_features(int n4, const float4* __
 
 // one 16-byte half of a render record at a wave-uniform byte offset (voffset, so that the range
 // check turns the null index P into zeros)
+// A wave-uniform 64-bit mask with bit i cleared: one s_bitset0_b64 (mask &= mask - 1 is three SALU:
+// a 64-bit subtract and an and).
+__device__ __forceinline__ uint64_t clear_bit(uint64_t m, int i) {
+    asm("s_bitset0_b64 %0, %1" : "+s"(m) : "s"(i));
+    return m;
+}
+
 __device__ __forceinline__ float4 rec_load(__amdgpu_buffer_rsrc_t rs, uint32_t off) {
     return __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rs, (int)off, 0, 0));
 }
@@ -456,7 +463,7 @@ __device__ __forceinline__ void render_fwd_body(const Dims& d, const Inputs& in,
             }                                                                                       \
             if (ok_) {                                                                              \
                 const int i_ = (int)__builtin_ctzll(mask);                                          \
-                mask &= mask - 1;                                                                   \
+                mask = clear_bit(mask, i_);                                                         \
                 g_ = __builtin_amdgcn_readlane(cidx, i_) & kIndexMask;                              \
                 pos_ = base + i_ + 1;                                                               \
             }                                                                                       \
@@ -471,9 +478,9 @@ __device__ __forceinline__ void render_fwd_body(const Dims& d, const Inputs& in,
             if (__builtin_expect(__builtin_popcountll(mask) >= 2, 1)) {                             \
                 /* common case: both survivors from the chunk in hand, no loop, no refill test */   \
                 const int i0_ = (int)__builtin_ctzll(mask);                                         \
-                mask &= mask - 1;                                                                   \
+                mask = clear_bit(mask, i0_);                                                        \
                 const int i1_ = (int)__builtin_ctzll(mask);                                         \
-                mask &= mask - 1;                                                                   \
+                mask = clear_bit(mask, i1_);                                                        \
                 ga_ = __builtin_amdgcn_readlane(cidx, i0_) & kIndexMask;                            \
                 gb_ = __builtin_amdgcn_readlane(cidx, i1_) & kIndexMask;                            \
                 pa_ = base + i0_ + 1;                                                               \
