@@ -770,10 +770,13 @@ __global__ __launch_bounds__(GSR_TILE_PIX) __attribute__((amdgpu_waves_per_eu(4)
 // (global) load while this step blends; the chunk after next's list entries and the next chunk's
 // records are loaded one refill ahead.
 #ifndef GSR_QUAD_WPE
-#define GSR_QUAD_WPE 3  // (the 3-deep operand pipeline's registers: 4 waves would spill; measured -4%)
+#define GSR_QUAD_WPE 2  // waves per SIMD: 2 leave the registers (220) for 6 operand slots
 #endif
 #ifndef GSR_QUAD_SLOTS
-#define GSR_QUAD_SLOTS 4  // operand slots: a step's record / feature loads are issued 3 steps before their use
+// operand slots: a step's record / feature loads are issued GSR_QUAD_SLOTS - 1 steps before their
+// use.  Per C2 frame: 4 slots at 3 waves per SIMD (168 registers) 122.4 us, 4 at 2 waves 123.5,
+// 5 at 2 waves 119.1, 6 / 7 / 8 at 2 waves 117.6-118.6 (220 / 241 / 256 registers)
+#define GSR_QUAD_SLOTS 6
 #endif
 template <int K>
 struct QSlot {
@@ -1030,13 +1033,25 @@ __global__ __launch_bounds__(GSR_TILE_PIX) __attribute__((amdgpu_waves_per_eu(GS
                 al = nal;
                 return head < tail && __any(!done);  // (false: the list is done or every pixel of the quad finished)
             };
-            static_assert(NS == 3 || NS == 4, "GSR_QUAD_SLOTS");
+            static_assert(NS >= 3 && NS <= 8, "GSR_QUAD_SLOTS");
             while (head < tail) {
                 if (!step(QSlot<0>{})) break;
                 if (!step(QSlot<1>{})) break;
                 if (!step(QSlot<2>{})) break;
-                if constexpr (NS == 4) {
+                if constexpr (NS >= 4) {
                     if (!step(QSlot<3 % NS>{})) break;
+                }
+                if constexpr (NS >= 5) {
+                    if (!step(QSlot<4 % NS>{})) break;
+                }
+                if constexpr (NS >= 6) {
+                    if (!step(QSlot<5 % NS>{})) break;
+                }
+                if constexpr (NS >= 7) {
+                    if (!step(QSlot<6 % NS>{})) break;
+                }
+                if constexpr (NS >= 8) {
+                    if (!step(QSlot<7 % NS>{})) break;
                 }
             }
             if (TL) n_walk = (uint32_t)min(base, n);
