@@ -783,7 +783,7 @@ struct QSlot {
     static constexpr int k = K;
 };
 #ifndef GSR_QUAD_RCH
-#define GSR_QUAD_RCH 4  // 64-entry list chunks per refill
+#define GSR_QUAD_RCH 3  // 64-entry list chunks per refill (per C2 frame at 6 slots: 2 -> 116.5 us, 3 -> 115.9, 4 -> 118.2, 8 -> 119.4)
 #endif
 constexpr int kQRch = GSR_QUAD_RCH;
 constexpr int kQRing = kQRch <= 4 ? 512 : 1024;  // ring entries per wave (a refill adds <= 64 kQRch and runs below 12)
@@ -880,7 +880,7 @@ __global__ __launch_bounds__(GSR_TILE_PIX) __attribute__((amdgpu_waves_per_eu(GS
             const __amdgpu_buffer_rsrc_t frs = __builtin_amdgcn_make_buffer_rsrc(
                 (void*)(in.colors + in.s_colors * b), 0, (int)min((int64_t)d.P * GSR_C * 4, (int64_t)0x7FFFFFFF),
                 0x00020000);
-            // list walk, 256 entries per refill (4 per lane): the entries and their quad masks
+            // list walk, 64 GSR_QUAD_RCH entries per refill (GSR_QUAD_RCH per lane): the entries and their quad masks
             // (binning's box test of this quad, BinArena.qmask) are contiguous loads with no
             // dependent ones, double-buffered one refill ahead; the survivors' Gaussian indices and
             // list positions go to the ring

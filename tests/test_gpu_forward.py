@@ -48,10 +48,11 @@ def test_forward_bit_exact(kind, P, W, H):
 
 def test_quad_list_lengths_around_slot_and_refill_boundaries():
     """A 16x16 frame (one tile, so the single-frame quad waves walk one list): list lengths from 1
-    to 20 -- the quad step takes 4 Gaussians over 4 operand slots with the step loop unrolled by
-    four, so every exit position of the unrolled loop is taken -- and around the 256-entry list
-    refills (250..262, 510..514): bit-exact, like every other forward."""
-    for P in list(range(1, 21)) + [250, 255, 256, 257, 262, 510, 512, 514]:
+    to 28 -- the quad step takes 4 Gaussians, the step loop unrolled by the number of operand
+    slots, so every exit position of the unrolled loop is taken -- and around the list refills
+    (64 GSR_QUAD_RCH entries each: 192 in the product build, 256 in earlier ones): bit-exact, like
+    every other forward."""
+    for P in list(range(1, 29)) + [190, 192, 193, 250, 256, 257, 383, 384, 385, 512, 514]:
         d = make_scene("random", P, 16, 16, seed=100 + P)
         _compare_exact(d)
 
