@@ -45,7 +45,7 @@ namespace gsr {
 #define GSR_PAD_VALU 0  // instrumentation: extra VALU per k-step (A/B builds)
 #endif
 #ifndef GSR_BATCH_NSLOT
-#define GSR_BATCH_NSLOT 5  // pipeline slots of the batched (throughput) kernels (see GSR_RENDER_WPE)
+#define GSR_BATCH_NSLOT 3  // pipeline slots of the batched (throughput) kernels
 #endif
 
 typedef float floatx16 __attribute__((ext_vector_type(16)));
@@ -711,13 +711,12 @@ __device__ __forceinline__ void render_fwd_body(const Dims& d, const Inputs& in,
     }
 }
 
-// Register budget: 4 waves per SIMD (128 registers; the few values spilled live outside the blend
-// loop) for the 5-slot batched kernel (GSR_BATCH_NSLOT), launched 4 workgroups per CU.  32-frame
-// C2 launch, same box: 3 slots at 5 waves 1.341-1.346 ms, 3 slots at 4 waves 1.368, 5 slots at 4
-// waves 1.333 (the deeper pipeline covers what the fifth wave covered).  The half-strip (one frame)
-// kernel keeps a 3-wave budget (launched 3 per CU).
+// Register budget: 5 waves per SIMD (96 registers; the few values spilled live outside the blend
+// loop) for the 3-slot kernel, launched 5 workgroups per CU at 16+ frames: the blend loop is
+// VALU-issue-bound with latency that 4 waves did not cover.  The half-strip (one frame) kernel
+// keeps a 3-wave budget (launched 3 per CU).
 #ifndef GSR_RENDER_WPE
-#define GSR_RENDER_WPE 4
+#define GSR_RENDER_WPE 5
 #endif
 #ifndef GSR_HALF_WPE
 #define GSR_HALF_WPE 3
@@ -1103,9 +1102,8 @@ void launch_render_fwd(const Dims& d, const Inputs& in_, const GeomArena& g, con
     if (nwaves == 0) return;
     // workgroups per CU: at most the resident capacity (GSR_RENDER_WPE waves/SIMD at the kernel's
     // register budget), so no render workgroup waits in the dispatcher ahead of another stream's
-    // kernels (4 at the 5-slot budget; with a 5-wave budget, large batches took all 5 -- -3% at 32
-    // frames -- and small ones 4: 5 was +4% at the 6-frame training batch, where fewer strips per
-    // wave leave a longer tail).
+    // kernels.  Large batches take all 5 (-3% at 32 frames); small ones 4 (5 was +4% at the
+    // 6-frame training batch, where fewer strips per wave leave a longer tail).
     static const int wg_env = tune_env("GSR_RENDER_WG_PER_CU", 0);
     const int wg_per_cu = wg_env > 0 ? wg_env : (d.B >= 16 ? GSR_RENDER_WPE : 4);
     // GSR_RENDER_HALF=0: single-frame launches on the throughput kernel (A/B); GSR_RENDER_HALF_WG: WGs per CU
