@@ -392,6 +392,91 @@ def per_frame_dropin(w, dev, n_frames=256, warmup=16):
             "path": "deform (B=1) + GaussianRasterizer_32 per frame, no_grad (main/test.py:70-76)"}
 
 
+def config_line(a, config, pipeline, dev, numerics, steps, warmup=5):
+    """One of BASELINE.json's other single-GPU configurations as an extra line of the default run
+    (N=1): config 4 (pipeline "train": batch 6, raster fwd + fused-SSIM/L1 loss + raster bwd + Adam)
+    or config 5 (config "c5": 300k Gaussians, 1024x1024, cross-reenactment deform + raster, two
+    batches in flight).  Same timing method as the contract line (wall clock over `steps` steps
+    between device synchronisations); the render kernels' launch times come from HIP events on the
+    launch stream (a separate isolated pass when batches overlap)."""
+    import copy
+    import torch
+    from guava_renderer_amd.batch import profile_enable, profile_read
+    b = copy.copy(a)
+    b.config, b.pipeline = config, pipeline
+    b.batch = 6 if pipeline == "train" else 32
+    b.inflight = 1 if pipeline == "train" else (2 if config == "c5" else 4)
+    b.refine = False
+    wl = _workload(config)
+    W, H, B = wl["W"], wl["H"], b.batch
+    w = Workload(b, wl, B, 0, B, dev, numerics)
+    n_in = max(1, len(w.rasts)) if pipeline != "train" else 1
+    streams = [torch.cuda.current_stream(dev)] + [torch.cuda.Stream(dev) for _ in range(n_in - 1)]
+    cnt = [0]
+
+    def step():
+        i = cnt[0] % n_in
+        cnt[0] += 1
+        with torch.cuda.stream(streams[i]):
+            return w.step_on(i)
+    for _ in range(warmup):
+        step()
+    torch.cuda.synchronize(dev)
+    stages = ("render_fwd", "render_bwd") if pipeline == "train" else ("render_fwd",)
+    profile_read()
+    profile_enable(stages if n_in == 1 else ())
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    torch.cuda.synchronize(dev)
+    el = time.perf_counter() - t0
+    prof = profile_read()
+    profile_enable(())
+    if n_in > 1:  # kernel times from an isolated pass (one batch at a time)
+        profile_enable(stages)
+        for _ in range(max(10, steps // 2)):
+            w.step_on(0)
+        torch.cuda.synchronize(dev)
+        prof = profile_read()
+        profile_enable(())
+    if pipeline == "train":
+        assert w.trainer.skipped_steps == 0, "capacity overflow inside the timed region"
+    else:
+        assert not any(r.status()[1] for r in w.rasts), "capacity overflow inside the timed region"
+    P_vis = int((w.rast.radii > 0).sum().item())
+    out = {"value": round(B * steps / el, 2), "unit": "frames/s", "ms_per_step": round(1e3 * el / steps, 4),
+           "steps": steps, "frames_per_step": B, "batches_in_flight": n_in,
+           "workload": wl["name"] + ("-train" if pipeline == "train" else "-deform+raster-cross"),
+           "gaussians": w.P, "image": [W, H], "visible_gaussians_per_frame": P_vis / B}
+    rms, rc = prof.get("render_fwd", (0.0, 0))
+    if rc:
+        ms = rms / rc
+        ab = _render_alg_bytes(P_vis / B, W, H) * B
+        out["roofline"] = {"kernel": "render_fwd", "avg_launch_ms": round(ms, 4), "alg_bytes_per_launch": ab,
+                           "achieved": round(ab / (ms * 1e-3) / 1e9, 1),
+                           "frac": round(ab / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}
+    bms, bc = prof.get("render_bwd", (0.0, 0))
+    if bc:
+        ms = bms / bc
+        ab = _render_bwd_alg_bytes(P_vis / B, W, H) * B
+        out["roofline_bwd"] = {"kernel": "render_bwd", "avg_launch_ms": round(ms, 4), "alg_bytes_per_launch": ab,
+                               "us_per_frame": round(1e3 * ms / B, 2),
+                               "achieved": round(ab / (ms * 1e-3) / 1e9, 1),
+                               "frac": round(ab / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}
+        pmc = os.path.join(ROOT, "profiles", "pmc_train.json")
+        try:
+            from guava_renderer_amd import build as _build
+            pm = json.load(open(pmc))
+            if pm.get("source_hash") == _build.source_hash() and pm.get("batch") == B:
+                out["roofline_bwd"]["traffic"] = (pm.get("kernels", {}).get("k_render_bwd") or {}).get("hbm_bytes")
+                out["roofline_bwd"]["traffic_source"] = "PMC FETCH_SIZE+WRITE_SIZE, pmc_train.json (this build)"
+        except (OSError, ValueError):
+            pass
+    del w
+    torch.cuda.empty_cache()
+    return out
+
+
 def main():
     a = _args()
     ws = os.environ.get("WORLD_SIZE")
@@ -697,6 +782,11 @@ def main():
         out["stage_ms_per_step"] = {k: round(v[0] / max(v[1], 1), 4) for k, v in prof.items()}
     if extras and world == 1 and a.pipeline == "avatar":
         out["per_frame_dropin"] = per_frame_dropin(w, dev)
+    if extras and world == 1 and a.pipeline == "avatar" and a.config == "c2":
+        # BASELINE configs 4 and 5 on one GPU, beside the contract line (their N>1 forms are the
+        # driver's multi-GPU runs: --pipeline train / --config c5 with --gpus N)
+        out["config4_train"] = config_line(a, "c2", "train", dev, numerics, steps=max(a.steps, 100))
+        out["config5_cross"] = config_line(a, "c5", "avatar", dev, numerics, steps=max(a.steps, 40))
     if rank == 0 and world == 1 and not a.no_cpu_baseline and a.pipeline != "train":
         out["cpu_baseline"] = cpu_baseline(w.scene, w.cams, W, H, a.cpu_seconds, w.avatar_inputs)
     if rank == 0:

@@ -129,6 +129,17 @@ __global__ __launch_bounds__(GSR_TILE_PIX) __attribute__((amdgpu_waves_per_eu(2)
         constexpr uint32_t kOOB = 0x80000000u;
         const int64_t gbase = (int64_t)b * d.P;
         const int64_t cbase = gr.reduce ? 0 : gbase;  // frame-reduced colour gradients: one [P][C] block
+        // the flush's gradient atomics through buffer resources of this frame's rows (P < 2^24, so
+        // P x 128 B fits the 32-bit range): a lane that adds nothing gets an out-of-range offset, so
+        // every atomic is issued unconditionally -- no branch around it, and the compiler's memory-
+        // counter waits for the next batch's loads count exactly past them instead of waiting for
+        // the atomics themselves (a branch-skipped atomic makes the count unknown: vmcnt(0)-like waits)
+        const __amdgpu_buffer_rsrc_t crs = __builtin_amdgcn_make_buffer_rsrc(
+            (void*)(gr.dL_dcolors + cbase * GSR_C), 0, (int)min((int64_t)d.P * GSR_C * 4, (int64_t)0x7FFFFFFF),
+            0x00020000);
+        const __amdgpu_buffer_rsrc_t grs = __builtin_amdgcn_make_buffer_rsrc(
+            (void*)(g.gterm + gbase * kGtWords), 0, (int)min((int64_t)d.P * kGtWords * 4, (int64_t)0x7FFFFFFF),
+            0x00020000);
 
         const float T_final = inside ? im.final_T[pix] : 0.f;
         const uint32_t last_contributor = inside ? im.n_contrib[pix] : 0u;
@@ -191,34 +202,48 @@ __global__ __launch_bounds__(GSR_TILE_PIX) __attribute__((amdgpu_waves_per_eu(2)
         auto list_load = [&](int pos) {
             return __builtin_amdgcn_raw_buffer_load_b32(lrs, pos >= 0 ? (int)((uint32_t)pos * 4u) : (int)kOOB, 0, 0);
         };
+        // the next two lower chunks are kept in flight (nidx, nidx2): a fill takes one or two chunks
+        // (about 27 of a chunk's 64 entries reach a strip), and a chunk loaded inside the fill is
+        // waited for at once -- behind the previous batch's gradient atomics, which stay counted in
+        // the memory counter for thousands of cycles
         uint32_t nidx = list_load(base - 64 + lane);
+        uint32_t nidx2 = list_load(base - 128 + lane);
         uint32_t head = 0, tail = 0;  // wave-uniform ring counters
         bool list_done = false;
+        auto take_chunk = [&](uint32_t cidx) {
+            const bool sv = base + lane < (int)ns && (cidx & smask_bit) != 0u;
+            const uint64_t m = __ballot(sv);
+            if (sv) {
+                // rank among the chunk's survivors counted from the back (higher positions first)
+                const uint32_t above = lane == 63 ? 0u : (uint32_t)__popcll(m >> (lane + 1));
+                const uint32_t slot = (tail + above) & (kBwdRing - 1);
+                ring_g[slot] = cidx & kIndexMask;
+                ring_p[slot] = (uint32_t)(base + lane);
+            }
+            tail += (uint32_t)__popcll(m);
+        };
         auto fill = [&](uint32_t want) {
-            bool first = true;
-            while (!list_done && tail - head < want) {
+            if (!list_done && tail - head < want) {
+                base -= 64;
+                if (base < 0) list_done = true;
+                else take_chunk(nidx);
+            }
+            if (!list_done && tail - head < want) {
+                base -= 64;
+                if (base < 0) list_done = true;
+                else take_chunk(nidx2);
+            }
+            while (!list_done && tail - head < want) {  // (rare: a third chunk, loaded here)
                 base -= 64;
                 if (base < 0) { list_done = true; break; }
-                // the prefetched chunk; a second chunk in the same fill is loaded here
-                uint32_t cidx = nidx;
-                if (!first) cidx = list_load(base + lane);
-                first = false;
-                const bool sv = base + lane < (int)ns && (cidx & smask_bit) != 0u;
-                const uint64_t m = __ballot(sv);
-                if (sv) {
-                    // rank among the chunk's survivors counted from the back (higher positions first)
-                    const uint32_t above = lane == 63 ? 0u : (uint32_t)__popcll(m >> (lane + 1));
-                    const uint32_t slot = (tail + above) & (kBwdRing - 1);
-                    ring_g[slot] = cidx & kIndexMask;
-                    ring_p[slot] = (uint32_t)(base + lane);
-                }
-                tail += (uint32_t)__popcll(m);
+                take_chunk(list_load(base + lane));
             }
-            // the next lower chunk, one unconditional load at the end (the same chunk again when
-            // none was used), in flight until the next fill: a load merged into nidx on some
+            // the next two lower chunks, unconditional loads at the end (the same chunks again when
+            // none was used), in flight until the next fill: a load merged into a register on some
             // paths only would reach it through a register copy that waits for the load at once
             __builtin_amdgcn_sched_barrier(0);
             nidx = list_load(base - 64 + lane);  // (0 below the list's start)
+            nidx2 = list_load(base - 128 + lane);
             wave_lds_order();
         };
         // a batch, lane-distributed: lane l holds survivor l&31's index and list position, its
@@ -254,6 +279,14 @@ __global__ __launch_bounds__(GSR_TILE_PIX) __attribute__((amdgpu_waves_per_eu(2)
         Batch bA, bB;
         fill(kBwdBatch);
         pop(bA.nb, bA.g, bA.p, bA.ra, bA.rc, bA.fr);
+        // as many (empty: out-of-range) atomics as a batch's flush issues, so that every path into
+        // the batch loop has the same memory-counter history: the first batch's waits for its
+        // loads then count past a flush's atomics as on every later entry, instead of the loop
+        // head taking this path's smaller count and waiting for the previous flush's atomics
+        if (ABL != 1) {
+#pragma unroll
+            for (int r = 0; r < 16 + 4; r++) __builtin_amdgcn_raw_ptr_buffer_atomic_fadd_f32(0.f, crs, (int)kOOB, 0, 0);
+        }
 
         // strip-centred pixel offsets (exact in f32): the moments use lx = x - cx, ly = y - cy
         const float cx = (float)sx0 + 3.5f, cy = (float)sy0 + 3.5f;
@@ -445,8 +478,9 @@ __global__ __launch_bounds__(GSR_TILE_PIX) __attribute__((amdgpu_waves_per_eu(2)
                     const uint32_t gsh = __builtin_amdgcn_readlane(cur.g, (r & 3) + 8 * (r >> 2) + 4);
                     const uint32_t gs = hi ? gsh : gsl;
                     // slots past the batch hold stale tiles; a zero sum (no pixel took the Gaussian,
-                    // or no gradient) adds nothing
-                    if (sl < cur.nb && acc[r] != 0.f) atomicAdd(gr.dL_dcolors + (cbase + gs) * GSR_C + l32, acc[r]);
+                    // or no gradient) adds nothing: those lanes' offsets fall outside the resource
+                    const uint32_t off = (sl < cur.nb && acc[r] != 0.f) ? (gs * GSR_C + (uint32_t)l32) * 4u : kOOB;
+                    __builtin_amdgcn_raw_ptr_buffer_atomic_fadd_f32(acc[r], crs, (int)off, 0, 0);
                 }
             }
             // the other terms of slot l&31, from the pixel moments of u about the Gaussian's centre
@@ -484,8 +518,9 @@ __global__ __launch_bounds__(GSR_TILE_PIX) __attribute__((amdgpu_waves_per_eu(2)
                     const uint32_t sl = (uint32_t)(8 * qq + (lane >> 3));
                     const uint32_t gs = (uint32_t)__shfl((int)cur.g, (int)sl);
                     const float val = rows[8 * sl + (lane & 7)];
-                    if (sl < cur.nb && val != 0.f && (lane & 7) != 7 && (INVD || (lane & 7) != kGtInv))
-                        atomicAdd(g.gterm + (gbase + gs) * kGtWords + (lane & 7), val);
+                    const bool add = sl < cur.nb && val != 0.f && (lane & 7) != 7 && (INVD || (lane & 7) != kGtInv);
+                    const uint32_t off = add ? (gs * (uint32_t)kGtWords + (uint32_t)(lane & 7)) * 4u : kOOB;
+                    __builtin_amdgcn_raw_ptr_buffer_atomic_fadd_f32(val, grs, (int)off, 0, 0);
                 }
             }
             wave_lds_order();

@@ -137,7 +137,8 @@ GRAD_ELEM_TOL = 1e-3    # |a - b| <= 1e-3 * |b| on every element with |b| >= GRA
 GRAD_ELEM_FLOOR = 1e-3
 
 
-NOISE_FACTOR = 3.0      # per-element bound relative to the reference algorithm's own f32 reordering noise
+NOISE_FACTOR = 1.5      # per-element bound relative to the reference algorithm's own f32 reordering noise
+                        # (worst measured GPU / reordering ratio 1.26)
 
 
 def grad_check(name, a, b, scale_tol=GRAD_SCALE_TOL, elem_tol=GRAD_ELEM_TOL, floor=GRAD_ELEM_FLOOR,

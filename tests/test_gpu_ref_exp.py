@@ -56,6 +56,11 @@ def test_forward_default_vs_reference_arithmetic(P, W, gpt, against):
     print(f"P={P} {W}x{W} vs {'literal reference arithmetic' if against else 'libm expf'}: n_contrib mismatch {nc_mism:.2e}, decision-flip pixels {int(flips.sum())} "
           f"({flips.mean():.2e}), L_inf on the other pixels {err[:, keep].max():.3g} "
           f"(RGB {err[:3][:, keep].max():.3g}), worst flipped pixel {worst_flip:.3g}")
+    # each flipped pixel: its position, its 32-channel L_inf and its RGB L_inf
+    errf = err.reshape(err.shape[0], -1)
+    for p in np.flatnonzero(np.asarray(flips).reshape(-1))[:16]:
+        print(f"  flipped pixel (x={p % W}, y={p // W}): all channels {float(errf[:, p].max()):.3g}, "
+              f"RGB {float(errf[:3, p].max()):.3g}")
     assert nc_mism <= FLIP_RATE, nc_mism
     assert flips.mean() <= FLIP_RATE, flips.mean()
     assert err[:, keep].max() <= TOL, err[:, keep].max()

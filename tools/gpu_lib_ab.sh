@@ -34,7 +34,9 @@ for r in $(seq 1 ${R:-2}); do
 import json, sys
 d = json.loads(open(sys.argv[2]).read().strip().splitlines()[-1])
 rf = d.get("roofline", {})
-print(f"{sys.argv[1]:36s} fps={d['value']:9.1f} ms={d['ms_per_step']:.4f} render_fwd={rf.get('avg_launch_ms')} frac={rf.get('frac')}")
+rb = d.get("roofline_bwd", {})
+print(f"{sys.argv[1]:36s} fps={d['value']:9.1f} ms={d['ms_per_step']:.4f} render_fwd={rf.get('avg_launch_ms')} frac={rf.get('frac')}"
+      + (f" render_bwd={rb.get('avg_launch_ms')} ({rb.get('us_per_frame')} us/frame)" if rb else ""))
 PY
     ) || exit $?
   done
