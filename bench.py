@@ -83,6 +83,12 @@ def _args():
                     help="headline in the split-bf16 colour-accumulation mode (tolerance, include/gsr.h)")
     ap.add_argument("--gather", default="u8", choices=["u8", "f32", "none"],
                     help="N>1 consumer exchange: 8-bit RGB (to8b, default), f32 RGB, or none")
+    ap.add_argument("--cu-split", type=int, default=None,
+                    help="render placement (include/gsr.h gsr_set_render_stream): the batches' deform + binning "
+                         "chains on streams masked to this many CUs, every compositing kernel on one render "
+                         "stream masked to the other CUs (0: the same routing without masks)")
+    ap.add_argument("--cu-mode", default="spread", choices=["spread", "lo"],
+                    help="which CUs the --cu-split slice takes (parallel.cu_masks)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-extras", action="store_true",
@@ -528,6 +534,10 @@ def main():
     # batch is complete work -- deform, binning, compositing; only consecutive batches overlap)
     n_inflight = max(1, len(w.rasts))
     streams = [torch.cuda.current_stream(dev)] + [torch.cuda.Stream(dev) for _ in range(n_inflight - 1)]
+    placement = None
+    if a.cu_split is not None and a.pipeline in ("avatar", "raster"):
+        placement = parallel.SplitPlacement(n_inflight, a.cu_split, dev, mode=a.cu_mode)
+        streams = placement.streams
 
     # consumer boundary at N>1: every rank receives all ranks' frames as the consumer writes them
     # (8-bit RGB, main/test.py:85) over RCCL/xGMI, each batch's exchange overlapped with the next
@@ -725,6 +735,8 @@ def main():
                        if world > 1 and a.pipeline != "train" and a.gather != "none" else
                        ", gradient all-reduce per step" if world > 1 and a.pipeline == "train" else ""),
                    "batches_in_flight": n_inflight,
+                   "placement": ({"prep_cus": placement.prep_cus, "render_cus": placement.render_cus,
+                                  "mode": placement.mode} if placement is not None else "shared"),
                    "exp": "hw" if a.fast_exp else "exact-poly",
                    "colour_accum": "split-bf16 mfma (<=1e-4)" if split_head else "f32 mfma (bit-exact)",
                    "instances_per_step": R_total, "visible_gaussians_per_frame": P_vis / B},

@@ -16,6 +16,7 @@ EXPORTS = ("gsr_version", "gsr_last_error", "gsr_geometry_bytes",
            "gsr_backward_batch", "gsr_backward_batch_shared", "gsr_batch_status", "gsr_profile_enable", "gsr_profile_read",
            "gsr_render_counters", "gsr_render_timeline", "gsr_forward_batch_refine",
            "gsr_refine_prepare", "gsr_batch_status_offset", "gsr_frames_to8b",
+           "gsr_stream_create_cu_mask", "gsr_stream_destroy", "gsr_set_render_stream",
            # include/gsr_deform.h
            "gsr_lbs_workspace_bytes", "gsr_lbs", "gsr_lbs_sp", "gsr_blend_joints", "gsr_blend_joints_sp",
            "gsr_lbs_tiled_floats", "gsr_lbs_tile_bases",
@@ -211,6 +212,12 @@ def load(path=None):
     L.gsr_render_timeline.restype = _i
     L.gsr_frames_to8b.argtypes = [_i, _i, _i, _i, _vp, _i64, _vp, _vp]
     L.gsr_frames_to8b.restype = _i
+    L.gsr_stream_create_cu_mask.argtypes = [_u32, ctypes.POINTER(_u32), ctypes.POINTER(_vp)]
+    L.gsr_stream_create_cu_mask.restype = _i
+    L.gsr_stream_destroy.argtypes = [_vp]
+    L.gsr_stream_destroy.restype = _i
+    L.gsr_set_render_stream.argtypes = [_vp, _vp]
+    L.gsr_set_render_stream.restype = _i
     L.gsr_lbs_workspace_bytes.argtypes = [_i, _i, _i, _i]
     L.gsr_lbs_workspace_bytes.restype = _sz
     L.gsr_lbs_tiled_floats.argtypes = [_i, _i]

@@ -297,15 +297,65 @@ constexpr int kLdsBuckets = 16384;
 static_assert(kLdsBuckets % kCountThreads == 0, "bucket claims: whole rows of the workgroup");
 // PER Gaussians per thread: kCountPer, or fewer for the single-frame launch (more workgroups for a
 // latency-bound grid)
-template <int PER>
-__global__ __launch_bounds__(kCountThreads) void k_bucket_count_lds(Dims d, GeomArena g) {
+// TOT (one frame, no host read-back of R): k_frame_totals folded in -- every workgroup reduces the
+// frame's block summaries itself (a few hundred words) for the key range and the overflow test, and
+// workgroup 0 writes what k_frame_totals writes; one launch fewer per single-frame forward
+template <int PER, bool TOT = false>
+__global__ __launch_bounds__(kCountThreads) void k_bucket_count_lds(Dims d, GeomArena g, int64_t R_cap) {
     extern __shared__ uint32_t hist[];  // NB
-    if (g.ctrl[kCtrlOverflow]) return;
     const int b = blockIdx.y;
+    uint32_t kmin, kmax;
+    if constexpr (TOT) {
+        __shared__ uint32_t red[3][kCountThreads / 64];
+        uint32_t r = 0, km = 0, nkm = 0;
+        for (int i = threadIdx.x; i < d.nblk; i += kCountThreads) {
+            r += g.blocksums[i];
+            km = max(km, g.blockkey[2 * i]);
+            nkm = max(nkm, g.blockkey[2 * i + 1]);
+        }
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) {
+            r += __shfl_xor(r, off);
+            km = max(km, (uint32_t)__shfl_xor(km, off));
+            nkm = max(nkm, (uint32_t)__shfl_xor(nkm, off));
+        }
+        if ((threadIdx.x & 63) == 0) {
+            red[0][threadIdx.x >> 6] = r;
+            red[1][threadIdx.x >> 6] = km;
+            red[2][threadIdx.x >> 6] = nkm;
+        }
+        __syncthreads();
+        r = 0; km = 0; nkm = 0;
+#pragma unroll
+        for (int w = 0; w < kCountThreads / 64; w++) {
+            r += red[0][w];
+            km = max(km, red[1][w]);
+            nkm = max(nkm, red[2][w]);
+        }
+        const uint32_t ovf = ((uint64_t)r > (uint64_t)R_cap || r >= 0xFFFFFFF0u) ? 1u : 0u;
+        if (blockIdx.x == 0 && threadIdx.x == 0) {  // (k_frame_totals' words, B = 1)
+            g.fstat[kFsR] = r;
+            g.fstat[kFsKeyMax] = km;
+            g.fstat[kFsNotKeyMax] = nkm;
+            g.fstat[kFsRBase] = 0u;
+            g.ctrl[kCtrlRLo] = r;
+            g.ctrl[kCtrlOverflow] = ovf;
+            if (g.sticky) {
+                if (ovf) g.sticky[kStickyOverflow] = 1u;
+                g.sticky[kStickyRMax] = max(g.sticky[kStickyRMax], r);
+            }
+        }
+        if (ovf) return;
+        kmin = ~nkm;
+        kmax = km;
+    } else {
+        if (g.ctrl[kCtrlOverflow]) return;
+        kmin = ~g.fstat[kFsWords * b + kFsNotKeyMax];
+        kmax = g.fstat[kFsWords * b + kFsKeyMax];
+    }
     const int i0 = blockIdx.x * kCountThreads * PER;
     for (int k = threadIdx.x; k < d.NB; k += kCountThreads) hist[k] = 0u;
     __syncthreads();
-    const uint32_t kmin = ~g.fstat[kFsWords * b + kFsNotKeyMax], kmax = g.fstat[kFsWords * b + kFsKeyMax];
     const float scale = bucket_scale(kmin, kmax, d.NB);
     uint32_t bk[PER], ls[PER];
 #pragma unroll
@@ -463,20 +513,33 @@ __global__ __launch_bounds__(NT) void k_bucket_sort(Dims d, GeomArena g) {
     }
 }
 
-void launch_depth_sort(const Dims& d, const GeomArena& g, hipStream_t s) {
+void launch_depth_sort(const Dims& d, const GeomArena& g, hipStream_t s, int64_t fused_totals_cap) {
     if (d.P == 0 || d.B == 0) return;
+    // fused_totals_cap >= 0: launch_scan_blocksums deferred the frame totals to the bucket count
+    const bool fuse = fused_totals_cap >= 0 && d.B == 1 && d.NB <= kLdsBuckets;
+    if (fused_totals_cap >= 0 && !fuse) launch_scan_blocksums(d, g, fused_totals_cap, s);
     if (d.NB <= kLdsBuckets) {  // every bucket has a claim slot (kClaims per thread)
         // GSR_B1_COUNT_PER: Gaussians per thread of the single-frame count, 2 (49 workgroups at 100k
         // Gaussians: -5 us per frame against 8) or kCountPer (A/B)
         static const int b1_per = tune_env("GSR_B1_COUNT_PER", 2);
         if (d.B == 1 && b1_per == 2) {
             const int per_wg = kCountThreads * 2;
-            hipLaunchKernelGGL(k_bucket_count_lds<2>, dim3((d.P + per_wg - 1) / per_wg, d.B), dim3(kCountThreads),
-                               (size_t)d.NB * 4, s, d, g);
+            const dim3 gr((d.P + per_wg - 1) / per_wg, d.B);
+            if (fuse)
+                hipLaunchKernelGGL((k_bucket_count_lds<2, true>), gr, dim3(kCountThreads), (size_t)d.NB * 4, s, d, g,
+                                   fused_totals_cap);
+            else
+                hipLaunchKernelGGL((k_bucket_count_lds<2>), gr, dim3(kCountThreads), (size_t)d.NB * 4, s, d, g,
+                                   (int64_t)0);
         } else {
             const int per_wg = kCountThreads * kCountPer;
-            hipLaunchKernelGGL(k_bucket_count_lds<kCountPer>, dim3((d.P + per_wg - 1) / per_wg, d.B),
-                               dim3(kCountThreads), (size_t)d.NB * 4, s, d, g);
+            const dim3 gr((d.P + per_wg - 1) / per_wg, d.B);
+            if (fuse)
+                hipLaunchKernelGGL((k_bucket_count_lds<kCountPer, true>), gr, dim3(kCountThreads), (size_t)d.NB * 4,
+                                   s, d, g, fused_totals_cap);
+            else
+                hipLaunchKernelGGL((k_bucket_count_lds<kCountPer>), gr, dim3(kCountThreads), (size_t)d.NB * 4, s, d,
+                                   g, (int64_t)0);
         }
     } else {
         hipLaunchKernelGGL(k_bucket_count, dim3(d.nblk, d.B), dim3(kScanBlock), 0, s, d, g);
@@ -866,7 +929,10 @@ __device__ __forceinline__ uint32_t quad_mask(float4 co, float4 pre, float2 m, i
 // time -- one pass per kept strip instead of the wave running every strip any lane keeps.  (The
 // scatter itself runs one workgroup per 256 Gaussians at one frame, latency-bound; computing the
 // masks there cost it 2.4x.)
-__global__ __launch_bounds__(256) void k_quad_masks(Dims d, GeomArena g, BinArena bn) {
+// (Measured: adding k_strip_count's per-tile strip counts here, one atomic per (tile run, strip) of
+// each wave's 64 entries, took the pass from 16 to 36 us per C2 frame -- the waves of a long tile
+// all add to the same four words -- against 9 us for the separate count launch.)
+__global__ __launch_bounds__(256) void k_quad_masks(Dims d, GeomArena g, ImageArena im, BinArena bn) {
     __shared__ float4 s_co[4][64], s_pre[4][64];
     __shared__ float2 s_m[4][64];
     __shared__ int2 s_org[4][64];         // tile (tx, ty) of the entry
@@ -931,11 +997,12 @@ __global__ __launch_bounds__(256) void k_quad_masks(Dims d, GeomArena g, BinAren
     }
 }
 
-void launch_quad_masks(const Dims& d, const GeomArena& g, const BinArena& b, hipStream_t s) {
+void launch_quad_masks(const Dims& d, const GeomArena& g, const ImageArena& im, const BinArena& b,
+                       hipStream_t s) {
     // 2048 workgroups: 8 per CU, every wave resident with about one 64-entry chunk (the pass is
     // load-latency-bound; 1024 workgroups: 19.6 us per C2 frame, 2048: 17.4, 4096: 17.1; GSR_QMASK_WG A/B)
     static const int wg = tune_env("GSR_QMASK_WG", 2048);
-    if (b.qmask && d.B == 1 && d.P > 0) hipLaunchKernelGGL(k_quad_masks, dim3(wg), dim3(256), 0, s, d, g, b);
+    if (b.qmask && d.B == 1 && d.P > 0) hipLaunchKernelGGL(k_quad_masks, dim3(wg), dim3(256), 0, s, d, g, im, b);
 }
 
 // ---------------------------------------------------------------- 5. ordered scatter
@@ -1400,7 +1467,7 @@ void launch_strip_order(const Dims& d, const GeomArena& g, const ImageArena& im,
     if (d.B == 0 || d.T == 0) return;
     const int nt = d.B * d.T;
     hipLaunchKernelGGL(k_strip_count, dim3((nt + 3) / 4), dim3(256), 0, s, d, im, b);
-    launch_quad_masks(d, g, b, s);
+    launch_quad_masks(d, g, im, b, s);
     const int tile_major = strip_order_tile_major();
     // (one frame: the tile-affine walk of one longest-first list, measured 1.5% faster there)
     const int map = tile_major ? (d.B == 1 ? 1 : xcd_queue_map()) : 0;

@@ -118,6 +118,19 @@ int persistent_grid(int per_cu) {
     return cus * per_cu;
 }
 
+// CU counts of the CU-masked streams made by gsr_stream_create_cu_mask
+static std::mutex g_cu_mu;
+static std::unordered_map<hipStream_t, int> g_stream_cus;
+
+int persistent_grid_on(hipStream_t s, int per_cu) {
+    {
+        std::lock_guard<std::mutex> lk(g_cu_mu);
+        const auto it = g_stream_cus.find(s);
+        if (it != g_stream_cus.end()) return it->second * per_cu;
+    }
+    return persistent_grid(per_cu);
+}
+
 size_t carve_geom(char* base, const Dims& d, GeomArena* g) {
     const size_t n = (size_t)d.B * d.P;
     size_t off = 0;
@@ -186,10 +199,28 @@ void launch_deform_preprocess(const Dims& d, const Inputs& in, const GeomArena& 
 
 namespace {
 
+// Render placement (gsr_set_render_stream): forwards enqueued on a registered stream run their
+// compositing kernel on its render stream, ordered by two events (the render waits for the binning,
+// the stream's later work waits for the render).
+struct RenderRoute {
+    hipStream_t render;
+    hipEvent_t ready, done;
+};
+std::mutex g_route_mu;
+std::unordered_map<hipStream_t, RenderRoute> g_routes;
+
+bool render_route(hipStream_t s, RenderRoute* r) {
+    std::lock_guard<std::mutex> lk(g_route_mu);
+    const auto it = g_routes.find(s);
+    if (it == g_routes.end()) return false;
+    *r = it->second;
+    return true;
+}
+
 // Shared forward sequence once R is known and the binning arena exists.
 int run_binning_and_render(const Dims& d, const Inputs& in, const GeomArena& g, const ImageArena& im,
                            const BinArena& bn, const Outputs& o, uint32_t numerics, int debug, hipStream_t s) {
-    { StageTimer st_(2, s); launch_depth_sort(d, g, s); }
+    { StageTimer st_(2, s); launch_depth_sort(d, g, s, in.fuse_totals ? in.totals_cap : -1); }
     STAGE(debug, s, "depth_sort");
     { StageTimer st_(3, s); launch_chunk_count(d, g, im, s); }
     STAGE(debug, s, "chunk_count");
@@ -201,7 +232,19 @@ int run_binning_and_render(const Dims& d, const Inputs& in, const GeomArena& g, 
         launch_strip_order(d, g, im, bn, s);
     }
     STAGE(debug, s, "ordered_scatter");
-    { StageTimer st_(6, s); launch_render_fwd(d, in, g, im, bn, o, exact_exp(numerics), split_bf16(numerics), s); }
+    RenderRoute rt;
+    const bool routed = render_route(s, &rt);
+    hipStream_t rs = s;
+    if (routed) {
+        HIP_TRY(hipEventRecord(rt.ready, s));
+        HIP_TRY(hipStreamWaitEvent(rt.render, rt.ready, 0));
+        rs = rt.render;
+    }
+    { StageTimer st_(6, rs); launch_render_fwd(d, in, g, im, bn, o, exact_exp(numerics), split_bf16(numerics), rs); }
+    if (routed) {
+        HIP_TRY(hipEventRecord(rt.done, rs));
+        HIP_TRY(hipStreamWaitEvent(s, rt.done, 0));
+    }
     STAGE(debug, s, "render_fwd");
     return 0;
 }
@@ -299,16 +342,21 @@ static int forward_single(gsr_alloc_fn geometryBuffer, gsr_alloc_fn binningBuffe
     // forward (its culling-error word is set during that kernel) or an empty one (no kernel)
     in.zero_ctrl = !in.prefiltered && d.P > 0 && d.B > 0;
     if (!in.zero_ctrl) HIP_TRY(hipMemsetAsync(g.ctrl, 0, ctrl_words(d) * 4, s));
+    // quad masks (4 B per instance and a pass) only for a forward that composites on the quad kernel
+    const bool quad = render_uses_quad(d, split_bf16(numerics), o);
     { StageTimer st_(0, s); launch_preprocess(d, in, g, o, s); }
     STAGE(debug, s, "preprocess");
     if (status_host) {
         const int64_t cap = async_bound(d);
-        { StageTimer st_(1, s); launch_scan_blocksums(d, g, cap, s); }
+        // nothing reads R on the host before the binning: the frame totals go into the depth sort's
+        // first kernel (launch_depth_sort)
+        in.fuse_totals = 1;
+        in.totals_cap = cap;
         STAGE(debug, s, "scan");
-        char* bb = binningBuffer(alloc_ctx, carve_bin(nullptr, cap, nullptr, true));
+        char* bb = binningBuffer(alloc_ctx, carve_bin(nullptr, cap, nullptr, quad));
         if (!bb) return fail(GSR_ERR_ALLOC, "binningBuffer allocation failed");
         BinArena bn;
-        carve_bin(bb, cap, &bn, true);
+        carve_bin(bb, cap, &bn, quad);
         int rc = run_binning_and_render(d, in, g, im, bn, o, numerics, debug, s);
         if (rc < 0) return rc;
         if (status_host != kNoStatus)
@@ -325,10 +373,10 @@ static int forward_single(gsr_alloc_fn geometryBuffer, gsr_alloc_fn binningBuffe
     if (ctrl_h[kCtrlOverflow] || ctrl_h[kCtrlRLo] > 0x7FFFFFFFu)
         return fail(GSR_ERR_CAPACITY, "instance count exceeds 2^31 - 1 (num_rendered is an int)");
     const int64_t R = ctrl_h[kCtrlRLo];
-    char* bb = binningBuffer(alloc_ctx, carve_bin(nullptr, R, nullptr, true));
+    char* bb = binningBuffer(alloc_ctx, carve_bin(nullptr, R, nullptr, quad));
     if (!bb) return fail(GSR_ERR_ALLOC, "binningBuffer allocation failed");
     BinArena bn;
-    carve_bin(bb, R, &bn, true);
+    carve_bin(bb, R, &bn, quad);
     int rc = run_binning_and_render(d, in, g, im, bn, o, numerics, debug, s);
     if (rc < 0) return rc;
     return (int)R;
@@ -576,6 +624,9 @@ static int forward_batch_impl(int B, int P, int width, int height, const float* 
         o.keep = refine->keep_channels;
         o.slope = refine->negative_slope;
     }
+    // a B = 1 workspace carries the quad-mask slab; the masks are computed only when the quad kernel
+    // will read them
+    if (!render_uses_quad(d, split_bf16(numerics), o)) bn.qmask = nullptr;
     // the control words are zeroed by the first kernel (zero_ctrl_words), except for a prefiltered
     // forward (its culling-error word is set during that kernel) or an empty one (no kernel)
     in.zero_ctrl = !in.prefiltered && d.P > 0 && d.B > 0;
@@ -588,7 +639,13 @@ static int forward_batch_impl(int B, int P, int width, int height, const float* 
         StageTimer st_(0, s);
         launch_preprocess(d, in, g, o, s);
     }
-    { StageTimer st_(1, s); launch_scan_blocksums(d, g, R_capacity, s); }
+    if (d.B == 1) {  // (the frame totals in the depth sort's first kernel: launch_depth_sort)
+        in.fuse_totals = 1;
+        in.totals_cap = R_capacity;
+    } else {
+        StageTimer st_(1, s);
+        launch_scan_blocksums(d, g, R_capacity, s);
+    }
     int rc = run_binning_and_render(d, in, g, im, bn, o, numerics, 0, s);
     if (rc < 0) return rc;
     note_workspace(workspace, in.fwd_only != 0);
@@ -788,6 +845,61 @@ int gsr_batch_status(const char* workspace, int B, int P, int64_t* R_total, int*
     (void)B; (void)P;
     if (R_total) *R_total = ctrl_h[kCtrlRLo];
     if (overflow) *overflow = ctrl_h[kCtrlOverflow] ? 1 : 0;
+    return 0;
+}
+
+int gsr_stream_create_cu_mask(uint32_t n_words, const uint32_t* cu_mask, void** stream_out) {
+    if (!stream_out || !cu_mask || n_words == 0) return fail(GSR_ERR_ARG, "gsr_stream_create_cu_mask: bad arguments");
+    int cus = 0;
+    for (uint32_t i = 0; i < n_words; i++) cus += __builtin_popcount(cu_mask[i]);
+    if (cus == 0) return fail(GSR_ERR_ARG, "gsr_stream_create_cu_mask: empty CU mask");
+    hipStream_t st = nullptr;
+    HIP_TRY(hipExtStreamCreateWithCUMask(&st, n_words, cu_mask));
+    {
+        std::lock_guard<std::mutex> lk(g_cu_mu);
+        g_stream_cus[st] = cus;
+    }
+    *stream_out = (void*)st;
+    return 0;
+}
+
+int gsr_stream_destroy(void* stream) {
+    hipStream_t st = (hipStream_t)stream;
+    if (!st) return 0;
+    {
+        std::lock_guard<std::mutex> lk(g_route_mu);
+        for (auto it = g_routes.begin(); it != g_routes.end();) {
+            if (it->first == st || it->second.render == st) {
+                hipEventDestroy(it->second.ready);
+                hipEventDestroy(it->second.done);
+                it = g_routes.erase(it);
+            } else {
+                ++it;
+            }
+        }
+    }
+    {
+        std::lock_guard<std::mutex> lk(g_cu_mu);
+        g_stream_cus.erase(st);
+    }
+    HIP_TRY(hipStreamDestroy(st));
+    return 0;
+}
+
+int gsr_set_render_stream(void* stream, void* render_stream) {
+    hipStream_t st = (hipStream_t)stream, rs = (hipStream_t)render_stream;
+    std::lock_guard<std::mutex> lk(g_route_mu);
+    const auto it = g_routes.find(st);
+    if (it != g_routes.end()) {
+        hipEventDestroy(it->second.ready);
+        hipEventDestroy(it->second.done);
+        g_routes.erase(it);
+    }
+    if (!rs || rs == st) return 0;
+    RenderRoute r{rs, nullptr, nullptr};
+    HIP_TRY(hipEventCreateWithFlags(&r.ready, hipEventDisableTiming));
+    HIP_TRY(hipEventCreateWithFlags(&r.done, hipEventDisableTiming));
+    g_routes[st] = r;
     return 0;
 }
 

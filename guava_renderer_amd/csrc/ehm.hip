@@ -137,8 +137,9 @@ int gsr_ehm_forward(const GsrEhm* ehm, int B, const GsrEhmParam* params, const G
         return api_fail(GSR_ERR_ARG, "gsr_ehm_forward: eyelid_params need both eyelid bases");
     const GsrEhmParam& gp = params[GSR_EHM_BODY_GLOBAL];
     const GsrEhmParam& bpo = params[GSR_EHM_BODY_POSE];
-    if ((gp.p && gp.width < 3) || (bpo.p && bpo.width < 63))
-        return api_fail(GSR_ERR_ARG, "gsr_ehm_forward: global_pose needs 3 columns, body_pose 63");
+    // (EHM.py:107-114 concatenates them as they are: another width would misalign the pose row)
+    if ((gp.p && gp.width != 3) || (bpo.p && bpo.width != 63))
+        return api_fail(GSR_ERR_ARG, "gsr_ehm_forward: global_pose must be 3 columns wide, body_pose 63");
 
     EhmArena a;
     carve_ehm(workspace, e, B, &a);
@@ -154,9 +155,15 @@ int gsr_ehm_forward(const GsrEhm* ehm, int B, const GsrEhmParam* params, const G
     const int w_exp = params[GSR_EHM_BODY_EXP].width;
     const int n_shape = NBb - w_exp;
     if (n_shape < 0) return api_fail(GSR_ERR_ARG, "gsr_ehm_forward: exp is wider than the body blend");
+    // FLAME betas (EHM.py:53-62): shape_params zero-padded to flame.n_shape, then the expression, so
+    // the expression starts at n_shape = NB - its width whatever the shape width passed
+    const int we_h = params[GSR_EHM_FLAME_EXPR].p ? params[GSR_EHM_FLAME_EXPR].width : 0;
+    const int n_shape_h = NBh - we_h;
+    if (n_shape_h < 0 || ws_h > n_shape_h)
+        return api_fail(GSR_ERR_ARG, "gsr_ehm_forward: FLAME betas: shape + expression wider than the FLAME blend");
     if (int rc = add_block(tab, a.betas_h, NBh,
-                           {cp(GSR_EHM_FLAME_SHAPE, 0, ws_h),
-                            cp(GSR_EHM_FLAME_EXPR, ws_h, params[GSR_EHM_FLAME_EXPR].width)}, "FLAME betas"))
+                           {cp(GSR_EHM_FLAME_SHAPE, 0, ws_h), cp(GSR_EHM_FLAME_EXPR, n_shape_h, we_h)},
+                           "FLAME betas"))
         return rc;
     if (int rc = add_block(tab, a.pose_h, 3 * Jh,
                            {cp(GSR_EHM_FLAME_JAW, 6, params[GSR_EHM_FLAME_JAW].width),

@@ -174,6 +174,7 @@ inline Dims make_dims(int B, int P, int W, int H) {
 size_t carve_geom(char* base, const Dims& d, GeomArena* g);
 size_t carve_image(char* base, const Dims& d, ImageArena* im);
 size_t carve_bin(char* base, int64_t R, BinArena* b, bool qmask = false);
+
 // Upper bound on P: the render kernels address a frame's feature rows (128 B per Gaussian) through
 // a buffer resource with 32-bit byte offsets, so P * 128 must stay below 2^31.
 constexpr int kMaxGaussians = 1 << 24;
@@ -198,6 +199,8 @@ struct Inputs {
     int fwd_only;         // GSR_FORWARD_ONLY: preprocess writes only what binning and compositing read
     int zero_ctrl;        // the forward's first kernel zeroes the control words (no memset launch)
     uint32_t xcd_map;     // render work-queue mapping (queue_item): 1 = tile-affine (strip order tile-major)
+    int fuse_totals;      // B = 1, no host read-back of R: the frame totals are reduced inside the
+    int64_t totals_cap;   // depth sort's bucket count (launch_depth_sort), against this R capacity
 };
 
 struct Outputs {
@@ -240,6 +243,12 @@ int api_fail(int status, const char* msg);
 
 // Workgroups for a persistent (work-queue) launch: CUs of the current device x per_cu.
 int persistent_grid(int per_cu);
+// whether a forward of these dims / numerics / outputs composites on the single-frame quad kernel
+// (the only reader of the binning arena's quad masks): otherwise no mask is carved or computed
+bool render_uses_quad(const Dims& d, bool split, const Outputs& o);
+// persistent grid of a launch on stream s: the CUs that stream may use (a CU-masked stream made by
+// gsr_stream_create_cu_mask) times per_cu
+int persistent_grid_on(hipStream_t s, int per_cu);
 // GSR_STRIP_ORDER: "strip" orders the render work by each strip's survivors; "tile" (default) by
 // tile (its longest strip), the 4 strips consecutive and dealt to one XCD queue (L2 reuse).
 int strip_order_tile_major();
@@ -311,7 +320,7 @@ void launch_preprocess(const Dims& d, const Inputs& in, const GeomArena& g, cons
                        hipStream_t s);
 void launch_scan_blocksums(const Dims& d, const GeomArena& g, int64_t R_cap, hipStream_t s);
 // per-frame depth sort of the visible Gaussians -> g.order
-void launch_depth_sort(const Dims& d, const GeomArena& g, hipStream_t s);
+void launch_depth_sort(const Dims& d, const GeomArena& g, hipStream_t s, int64_t fused_totals_cap = -1);
 // instance counts per (depth chunk, tile), scanned per tile -> g.table, im.tile_count
 void launch_chunk_count(const Dims& d, const GeomArena& g, const ImageArena& im, hipStream_t s);
 void launch_tile_scan(const Dims& d, const GeomArena& g, const ImageArena& im, hipStream_t s);

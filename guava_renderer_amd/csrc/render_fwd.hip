@@ -786,7 +786,11 @@ struct QSlot {
 #define GSR_QUAD_RCH 3  // 64-entry list chunks per refill (per C2 frame at 6 slots: 2 -> 116.5 us, 3 -> 115.9, 4 -> 118.2, 8 -> 119.4)
 #endif
 constexpr int kQRch = GSR_QUAD_RCH;
-constexpr int kQRing = kQRch <= 4 ? 512 : 1024;  // ring entries per wave (a refill adds <= 64 kQRch and runs below 12)
+constexpr int kQRing = kQRch <= 4 ? 512 : 1024;  // ring entries per wave
+// live entries: a refill (ensure) runs while fewer than 4 GSR_QUAD_SLOTS are queued and adds at most
+// 64 kQRch; behind the head, up to 4 GSR_QUAD_SLOTS entries of the steps whose operands are in flight;
+// past the tail, 4 GSR_QUAD_SLOTS null entries once the list is exhausted
+static_assert(kQRing >= 64 * kQRch + 12 * GSR_QUAD_SLOTS, "quad ring too small for a refill beside the slots in flight");
 constexpr uint32_t kQNull = 0x07FFFFFFu;  // the null Gaussian: record / feature offsets out of range
 
 // TL (gsr_render_timeline): per quad item, (start, end) in 100 MHz ticks, steps | refills << 16, list
@@ -1094,6 +1098,16 @@ __global__ __launch_bounds__(GSR_TILE_PIX) __attribute__((amdgpu_waves_per_eu(GS
     }
 }
 
+// GSR_RENDER_QUAD=0: single-frame launches on the half-strip kernel (A/B)
+static bool quad_mode_on() {
+    static const bool v = tune_env("GSR_RENDER_QUAD", 1) != 0;
+    return v;
+}
+
+bool render_uses_quad(const Dims& d, bool split, const Outputs& o) {
+    return d.B == 1 && quad_mode_on() && !split && !o.stats && !o.out_refine;
+}
+
 void launch_render_fwd(const Dims& d, const Inputs& in_, const GeomArena& g, const ImageArena& im,
                        const BinArena& b, const Outputs& o, bool exact, bool split, hipStream_t s) {
     Inputs in = in_;  // one frame: strip_list is one longest-first list (launch_strip_order)
@@ -1108,11 +1122,11 @@ void launch_render_fwd(const Dims& d, const Inputs& in_, const GeomArena& g, con
     const int wg_per_cu = wg_env > 0 ? wg_env : (d.B >= 16 ? GSR_RENDER_WPE : 4);
     // GSR_RENDER_HALF=0: single-frame launches on the throughput kernel (A/B); GSR_RENDER_HALF_WG: WGs per CU
     static const bool half_mode = tune_env("GSR_RENDER_HALF", 1) != 0;
-    // GSR_RENDER_QUAD=0: single-frame launches on the half-strip kernel (A/B); GSR_RENDER_QUAD_WG: WGs per CU
-    static const bool quad_mode = tune_env("GSR_RENDER_QUAD", 1) != 0;
+    // (GSR_RENDER_QUAD_WG: quad-kernel workgroups per CU)
+    const bool quad_mode = quad_mode_on();
     static const int quad_wg = tune_env("GSR_RENDER_QUAD_WG", GSR_QUAD_WPE);
     static const int half_wg = tune_env("GSR_RENDER_HALF_WG", GSR_HALF_WPE);
-    const int grid = min((nwaves + 3) / 4, persistent_grid(wg_per_cu));
+    const int grid = min((nwaves + 3) / 4, persistent_grid_on(s, wg_per_cu));
     const dim3 gr(grid), bl(GSR_TILE_PIX);
 #ifdef GSR_TUNING
     static const int ablate = tune_env("GSR_RENDER_ABLATE", 0);

@@ -451,13 +451,22 @@ class EHMDeformer:
             off += B * w
         betas_h, pose_h, sc, pose, hsb = views
         segs = []
+        # FLAME betas: shape zero-padded to flame.n_shape, then the expression (EHM.py:53-62)
+        n_shape_h = NBh - fp["expression_params"].shape[-1]
+        if fp["shape_params"].shape[-1] > n_shape_h:
+            raise ValueError(f"FLAME shape_params ({fp['shape_params'].shape[-1]}) + expression_params "
+                             f"({fp['expression_params'].shape[-1]}) wider than the FLAME blend ({NBh})")
         _seg(segs, betas_h, 0, fp["shape_params"], B)
-        _seg(segs, betas_h, fp["shape_params"].shape[-1], fp["expression_params"], B)
+        _seg(segs, betas_h, n_shape_h, fp["expression_params"], B)
         _seg(segs, pose_h, 6, fp["jaw_params"], B)
         _seg(segs, pose_h, 9, fp["eye_pose_params"], B)
         n_shape = NBb - bp["exp"].shape[-1]
         _seg(segs, sc, 0, bp["shape"], B, width=min(n_shape, bp["shape"].shape[-1]))
         _seg(segs, sc, n_shape, bp["exp"], B)
+        for name, wd in (("global_pose", 3), ("body_pose", 63)):  # (EHM.py:107-114: no prefix is taken)
+            t_ = bp.get(name)
+            if t_ is not None and t_.numel() // max(1, t_.shape[0] if t_.dim() > 1 else 1) != wd:
+                raise ValueError(f"{name} must be {wd} columns wide")
         _seg(segs, pose, 0, bp.get("global_pose"), B, width=3)
         _seg(segs, pose, 3, bp.get("body_pose"), B, width=63)
         _seg(segs, pose, 75, bp["left_hand_pose"], B)

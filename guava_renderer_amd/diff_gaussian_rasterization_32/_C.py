@@ -269,9 +269,13 @@ class _Scratch:
         self.bufs = [torch.empty((0,), dtype=torch.uint8, device=device) for _ in range(3)]
         self.s = _lib.Scratch()
         self.sizes = {}
+        self._last = None
 
     def fit(self, L, P, W, H, bound):
         key = (P, W, H)
+        if key == self._last:  # the same shape as the previous call: the struct is current
+            return self.s
+        self._last = key
         need = self.sizes.get(key)
         if need is None:
             need = self.sizes[key] = (L.gsr_geometry_bytes(P, W, H), L.gsr_binning_bytes(bound),
@@ -289,6 +293,7 @@ class _Scratch:
 _SCRATCH = collections.OrderedDict()  # (device, stream handle) -> _Scratch, least recently used first
 _SCRATCH_MAX = 8
 _SCRATCH_FNS = None
+_BOUNDS = {}  # (P, W, H) -> the async bound when the no-sync forward applies, else None
 
 
 def clear_scratch():
@@ -314,13 +319,19 @@ def rasterize_inference(background, means3D, colors, opacity, scales, rotations,
     dev = means3D.device
     if P == 0 or dev.type != "cuda" or colors is None or colors.numel() == 0:
         return None
-    if means3D.get_device() != torch.cuda.current_device():
+    dix = means3D.get_device()
+    if dix != torch._C._cuda_getDevice():
         # the library sizes its persistent grids and raises LDS limits on the current device: the
         # general path enters the inputs' device first (no device switch on this hot path)
         return None
     L = _lib.load()
-    bound = L.gsr_forward_async_bound(P, W, H)
-    if bound >= 0x7FFFFFFF or L.gsr_binning_bytes(bound) > ASYNC_BINNING_MB << 20:
+    bound = _BOUNDS.get((P, W, H), 0)
+    if bound == 0:
+        bound = L.gsr_forward_async_bound(P, W, H)
+        if bound >= 0x7FFFFFFF or L.gsr_binning_bytes(bound) > ASYNC_BINNING_MB << 20:
+            bound = None
+        _BOUNDS[(P, W, H)] = bound
+    if bound is None:
         return None
     if numerics is None:
         numerics = DEFAULT_NUMERICS
@@ -337,8 +348,8 @@ def rasterize_inference(background, means3D, colors, opacity, scales, rotations,
         if cov.device != dev or cov.dtype != torch.float32:
             return None
         cov = cov.contiguous()
-    stream = torch.cuda.current_stream(dev)
-    key = (dev, stream.cuda_stream)
+    stream = torch._C._cuda_getCurrentRawStream(dix)  # (the handle; torch.cuda.current_stream builds an object)
+    key = (dix, stream)
     sc = _SCRATCH.get(key)
     if sc is None:
         sc = _SCRATCH[key] = _Scratch(dev)
@@ -360,7 +371,7 @@ def rasterize_inference(background, means3D, colors, opacity, scales, rotations,
                                    float(scale_modifier), _ptr(rotations), _ptr(cov), _ptr(viewmatrix),
                                    _ptr(projmatrix), None, float(tan_fovx), float(tan_fovy), 0,
                                    out_color.data_ptr(), out_invdepth.data_ptr(), int(bool(antialiasing)),
-                                   radii.data_ptr(), 0, None, int(numerics), ctypes.c_void_p(stream.cuda_stream)),
+                                   radii.data_ptr(), 0, None, int(numerics), stream),
                "rasterize_gaussians")
     return out_color, radii, out_invdepth
 

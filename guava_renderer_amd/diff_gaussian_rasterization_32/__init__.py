@@ -32,6 +32,7 @@ from . import _C
 
 # GSR_INFERENCE_PATH=0: inference calls take the autograd Function too (A/B of _C.rasterize_inference)
 _INFERENCE_PATH = os.environ.get("GSR_INFERENCE_PATH", "1") != "0"
+_EMPTY = torch.Tensor([])
 
 
 def cpu_deep_copy_tuple(input_tuple):
@@ -184,16 +185,18 @@ class GaussianRasterizer_32(nn.Module):
                 ((scales is not None or rotations is not None) and cov3D_precomp is not None):
             raise Exception('Please provide exactly one of either scale/rotation pair or precomputed 3D covariance!')
 
+        # (one shared empty CPU float tensor, as the reference's torch.Tensor([]): only read, never
+        # written, and not built again on every call of the per-frame loop)
         if shs is None:
-            shs = torch.Tensor([])
+            shs = _EMPTY
         if colors_precomp is None:
-            colors_precomp = torch.Tensor([])
+            colors_precomp = _EMPTY
         if scales is None:
-            scales = torch.Tensor([])
+            scales = _EMPTY
         if rotations is None:
-            rotations = torch.Tensor([])
+            rotations = _EMPTY
         if cov3D_precomp is None:
-            cov3D_precomp = torch.Tensor([])
+            cov3D_precomp = _EMPTY
 
         return rasterize_gaussians(means3D, means2D, shs, colors_precomp, opacities, scales,
                                    rotations, cov3D_precomp, raster_settings)

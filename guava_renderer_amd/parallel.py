@@ -160,3 +160,78 @@ def reduce_shared_grads(grads, group=None):
         grads[k].copy_(flat[off: off + n].view_as(grads[k]))
         off += n
     return grads
+
+
+def cu_masks(n_cus, prep_cus, mode="spread"):
+    """(prep mask, render mask) as lists of 32-bit words over n_cus CUs: the prep slice takes
+    prep_cus CUs -- CU i * step + (i mod 8) for step = n_cus / prep_cus ("spread": one share on each
+    XCD whether the mask's bit order interleaves the 8 XCDs or runs through them one after the
+    other) or the first prep_cus ("lo") -- and the render slice the rest.  prep_cus == 0: both masks
+    are every CU."""
+    n_words = (n_cus + 31) // 32
+    prep = [0] * n_words
+    if prep_cus <= 0:
+        full = [0] * n_words
+        for c in range(n_cus):
+            full[c // 32] |= 1 << (c % 32)
+        return full, list(full)
+    if not 0 < prep_cus < n_cus:
+        raise ValueError(f"prep_cus must be in (0, {n_cus})")
+    if mode == "spread":
+        blk = max(1, n_cus // 8)
+        chosen = set()
+        for t in range(prep_cus):  # share t: block t mod 8, residue mod 8 rotating with the block
+            b, w = t % 8, t // 8
+            c = b * blk + (w * 8 + b + w // max(1, blk // 8)) % blk
+            while c in chosen:
+                c = (c + 1) % n_cus
+            chosen.add(c)
+    elif mode == "lo":
+        chosen = set(range(prep_cus))
+    else:
+        raise ValueError(f"unknown mode {mode!r}")
+    render = [0] * n_words
+    for c in range(n_cus):
+        if c in chosen:
+            prep[c // 32] |= 1 << (c % 32)
+        else:
+            render[c // 32] |= 1 << (c % 32)
+    return prep, render
+
+
+class SplitPlacement:
+    """Batches in flight with the compositing kernel on its own CU slice (include/gsr.h
+    gsr_stream_create_cu_mask / gsr_set_render_stream): `n_prep` streams for the deform + binning
+    chains of the batches, each routed so its forwards' render kernels run on ONE shared render
+    stream.  prep_cus > 0 masks the prep streams to that many CUs and the render stream to the rest
+    (the persistent render grid is sized to them); prep_cus == 0 keeps every stream on every CU (the
+    routing alone).  `streams` are torch ExternalStreams of the prep streams (use with
+    torch.cuda.stream); close() destroys them."""
+
+    def __init__(self, n_prep, prep_cus, device, mode="spread"):
+        self.mode = mode
+        from . import _lib
+        L = self.L = _lib.load()
+        n_cus = torch.cuda.get_device_properties(device).multi_processor_count
+        pm, rm = cu_masks(n_cus, prep_cus, mode)
+        self.handles = []
+
+        def make(mask):
+            arr = (ctypes.c_uint32 * len(mask))(*mask)
+            h = ctypes.c_void_p()
+            _lib.check(L.gsr_stream_create_cu_mask(len(mask), arr, ctypes.byref(h)), "gsr_stream_create_cu_mask")
+            self.handles.append(h.value)
+            return h.value
+        self.render_handle = make(rm)
+        self.prep_handles = [make(pm) for _ in range(n_prep)]
+        for h in self.prep_handles:
+            _lib.check(L.gsr_set_render_stream(h, self.render_handle), "gsr_set_render_stream")
+        self.streams = [torch.cuda.ExternalStream(h, device=device) for h in self.prep_handles]
+        self.render_stream = torch.cuda.ExternalStream(self.render_handle, device=device)
+        self.prep_cus, self.render_cus = sum(bin(w).count("1") for w in pm), sum(bin(w).count("1") for w in rm)
+
+    def close(self):
+        torch.cuda.synchronize()
+        for h in self.handles:
+            self.L.gsr_stream_destroy(h)
+        self.handles = []

@@ -295,6 +295,18 @@ int gsr_batch_status(const char* workspace, int B, int P, int64_t* R_total, int*
 int gsr_frames_to8b(int B, int channels, int height, int width, const float* src, int64_t frame_stride,
                     uint8_t* dst, void* stream);
 
+/* Placement of the compositing kernel (no reference counterpart; the reference runs every stage on
+ * one stream).  gsr_stream_create_cu_mask makes a HIP stream whose kernels run only on the CUs set
+ * in cu_mask (n_words 32-bit words, bit i = CU i; hipExtStreamCreateWithCUMask); persistent render
+ * grids launched on it are sized to those CUs.  gsr_set_render_stream(stream, render_stream): batched
+ * and single-frame forwards enqueued on `stream` launch their compositing kernel on render_stream,
+ * after the binning on `stream` (event) and before `stream`'s later work (event), so the call stays
+ * stream-ordered for its caller; render_stream NULL (or == stream) removes the routing.
+ * gsr_stream_destroy removes the stream's routes and destroys it. */
+int gsr_stream_create_cu_mask(uint32_t n_words, const uint32_t* cu_mask, void** stream_out);
+int gsr_stream_destroy(void* stream);
+int gsr_set_render_stream(void* stream, void* render_stream);
+
 #ifdef __cplusplus
 }
 #endif

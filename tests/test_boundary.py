@@ -231,6 +231,15 @@ def test_ehm_abi_sizes_and_validation():
     prm[2].row_stride = 3
     prm[8].p, prm[8].width, prm[8].row_stride = 256, 60, 60  # body_pose needs 63 columns
     assert call() == -1 and b"body_pose 63" in L.gsr_last_error()
+    prm[8].width = prm[8].row_stride = 66  # ... exactly: no prefix of a wider row is taken (EHM.py:107-114)
+    assert call() == -1 and b"body_pose 63" in L.gsr_last_error()
+    prm[8].width = prm[8].row_stride = 63
+    prm[7].p, prm[7].width, prm[7].row_stride = 256, 6, 6  # global_pose exactly 3
+    assert call() == -1 and b"global_pose must be 3" in L.gsr_last_error()
+    prm[7].width = prm[7].row_stride = 3
+    prm[0].width = prm[0].row_stride = 301  # FLAME shape wider than n_shape = NB - expression width
+    assert call() == -1 and b"FLAME betas" in L.gsr_last_error()
+    prm[0].width = prm[0].row_stride = 300
     e.N_head = 7
     assert call() == -1 and b"N_head" in L.gsr_last_error()
 
