@@ -89,6 +89,12 @@ def _args():
                          "stream masked to the other CUs (0: the same routing without masks)")
     ap.add_argument("--cu-mode", default="spread", choices=["spread", "lo"],
                     help="which CUs the --cu-split slice takes (parallel.cu_masks)")
+    ap.add_argument("--render-streams", type=int, default=0,
+                    help="route the compositing kernels of the batches' streams to this many render streams "
+                         "(include/gsr.h gsr_set_render_stream; 0: each batch renders on its own stream)")
+    ap.add_argument("--prep-priority", type=int, default=0,
+                    help="HIP stream priority of the batches' streams when --render-streams is set "
+                         "(torch convention: lower is higher priority; the render streams keep 0)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-extras", action="store_true",
@@ -538,6 +544,12 @@ def main():
     if a.cu_split is not None and a.pipeline in ("avatar", "raster"):
         placement = parallel.SplitPlacement(n_inflight, a.cu_split, dev, mode=a.cu_mode)
         streams = placement.streams
+    elif a.render_streams > 0 and a.pipeline in ("avatar", "raster"):
+        streams = [torch.cuda.Stream(dev, priority=a.prep_priority) for _ in range(n_inflight)]
+        rstreams = [torch.cuda.Stream(dev) for _ in range(a.render_streams)]
+        for i, st in enumerate(streams):
+            _lib.check(_lib.load().gsr_set_render_stream(st.cuda_stream, rstreams[i % len(rstreams)].cuda_stream),
+                       "gsr_set_render_stream")
 
     # consumer boundary at N>1: every rank receives all ranks' frames as the consumer writes them
     # (8-bit RGB, main/test.py:85) over RCCL/xGMI, each batch's exchange overlapped with the next
@@ -736,7 +748,9 @@ def main():
                        ", gradient all-reduce per step" if world > 1 and a.pipeline == "train" else ""),
                    "batches_in_flight": n_inflight,
                    "placement": ({"prep_cus": placement.prep_cus, "render_cus": placement.render_cus,
-                                  "mode": placement.mode} if placement is not None else "shared"),
+                                  "mode": placement.mode} if placement is not None else
+                                 {"render_streams": a.render_streams, "prep_priority": a.prep_priority}
+                                 if a.render_streams > 0 else "shared"),
                    "exp": "hw" if a.fast_exp else "exact-poly",
                    "colour_accum": "split-bf16 mfma (<=1e-4)" if split_head else "f32 mfma (bit-exact)",
                    "instances_per_step": R_total, "visible_gaussians_per_frame": P_vis / B},

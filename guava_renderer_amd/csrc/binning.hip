@@ -882,7 +882,10 @@ void launch_tile_scan(const Dims& d, const GeomArena& g, const ImageArena& im, h
 // Non-finite or non-positive-definite conics keep every strip.  Host-callable for
 // tools/strip_mask_check.cpp (brute force over the strip's 64 pixels: no strip with a pixel at
 // Q <= K is ever cleared; 0.4% more strips kept than needed on random conics).
-__host__ __device__ __forceinline__ uint32_t strip_mask(float4 co, float4 pre, float2 m, int tx, int ty) {
+// strip_mask_loop: the four box_reach calls; strip_mask: the same bits from sub_reach4<8> (the 2 x 2
+// strips of a tile share their column and row terms, no divergent branches), checked equal to the
+// loop by tools/strip_mask_check.cpp (tests/test_cull.py)
+__host__ __device__ __forceinline__ uint32_t strip_mask_loop(float4 co, float4 pre, float2 m, int tx, int ty) {
     const uint32_t mode = __builtin_bit_cast(uint32_t, pre.w);
     if (mode == 1u) return 0u;
     if (mode == 2u) return (1u << kStrips) - 1u;
@@ -897,6 +900,17 @@ __host__ __device__ __forceinline__ uint32_t strip_mask(float4 co, float4 pre, f
             bits |= 1u << s;
     }
     return bits;
+}
+
+__host__ __device__ __forceinline__ uint32_t strip_mask(float4 co, float4 pre, float2 m, int tx, int ty) {
+    if constexpr (kStripW != 8 || kStripH != 8) {
+        return strip_mask_loop(co, pre, m, tx, ty);
+    } else {
+        const uint32_t mode = __builtin_bit_cast(uint32_t, pre.w);
+        if (mode == 1u) return 0u;
+        if (mode == 2u) return (1u << kStrips) - 1u;
+        return sub_reach4<8>(co.x, co.y, co.z, pre.x, pre.y, pre.z, m, (float)(tx * GSR_BX), (float)(ty * GSR_BY));
+    }
 }
 
 // Quad mask of one instance (single-frame arenas, BinArena.qmask): bit 4 s + q is set when strip s's

@@ -90,21 +90,23 @@ __host__ __device__ __forceinline__ uint32_t quad_bits_bbox(float4 bb, float sx0
     return bits;
 }
 
-// box_reach of the four 4x4 quads of an 8x8 strip at (sx0, sy0) at once, bit q = quad q (x offset
-// 4 (q & 1), y offset 4 (q >> 1)): the same expressions as box_reach / rect_qmin on each quad (so the
-// same bits), with the per-column and per-row terms shared between quads and rect_qmin's branches
-// turned into selects of the same values (no divergent paths per quad).
-__host__ __device__ __forceinline__ uint32_t quad_reach4(float a, float b, float c, float K, float ia, float ic,
-                                                         float2 m, float sx0, float sy0) {
+// box_reach of the four S x S sub-rectangles of the 2S x 2S block at (x0b, y0b) at once, bit q =
+// sub-rectangle q (x offset S (q & 1), y offset S (q >> 1)): the same expressions as box_reach /
+// rect_qmin on each (so the same bits), with the per-column and per-row terms shared between them
+// and rect_qmin's branches turned into selects of the same values (no divergent paths).  S = 4: the
+// quads of an 8x8 strip (quad_reach4); S = 8: the strips of a 16x16 tile (binning's strip_mask).
+template <int S>
+__host__ __device__ __forceinline__ uint32_t sub_reach4(float a, float b, float c, float K, float ia, float ic,
+                                                        float2 m, float x0b, float y0b) {
     float dxl[2], dxh[2], mx[2], dyl[2], dyh[2], my[2];
     bool xin[2], yin[2];
 #pragma unroll
     for (int h = 0; h < 2; h++) {
-        const float x0 = sx0 + 4.0f * (float)h, y0 = sy0 + 4.0f * (float)h;
-        dxl[h] = m.x - (x0 + (4.0f - 1.0f));
+        const float x0 = x0b + (float)S * (float)h, y0 = y0b + (float)S * (float)h;
+        dxl[h] = m.x - (x0 + ((float)S - 1.0f));
         dxh[h] = m.x - x0;
         mx[h] = fmaxf(fabsf(dxl[h]), fabsf(dxh[h]));
-        dyl[h] = m.y - (y0 + (4.0f - 1.0f));
+        dyl[h] = m.y - (y0 + ((float)S - 1.0f));
         dyh[h] = m.y - y0;
         my[h] = fmaxf(fabsf(dyl[h]), fabsf(dyh[h]));
         xin[h] = dxl[h] <= 0.f && dxh[h] >= 0.f;
@@ -128,6 +130,12 @@ __host__ __device__ __forceinline__ uint32_t quad_reach4(float a, float b, float
         bits |= (!(qm > K + slack)) ? (1u << q) : 0u;
     }
     return bits;
+}
+
+// the four 4x4 quads of the 8x8 strip at (sx0, sy0)
+__host__ __device__ __forceinline__ uint32_t quad_reach4(float a, float b, float c, float K, float ia, float ic,
+                                                         float2 m, float sx0, float sy0) {
+    return sub_reach4<4>(a, b, c, K, ia, ic, m, sx0, sy0);
 }
 
 }  // namespace gsr

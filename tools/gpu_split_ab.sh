@@ -2,7 +2,8 @@
 # Same-box sweep of the render placement (bench.py --cu-split K [--cu-mode M]) on the contract
 # workload with 4 batches in flight, R rounds interleaved:
 #   tools/gpu_split_ab.sh none 0 16 32 48 lo:32
-# "none" = the shared default; K = prep slice of K CUs ("spread"); lo:K = the first K CUs.
+# "none" = the shared default; K = prep slice of K CUs ("spread"); lo:K = the first K CUs;
+# rs:K/P = K render streams, the batches' streams at priority P (e.g. rs:2/-1).
 set -u
 cd "$GRAFT_REPO_ROOT"
 export TMPDIR=/tmp
@@ -13,6 +14,8 @@ for r in $(seq 1 ${R:-2}); do
     case "$V" in
       none) A="" ;;
       lo:*) A="--cu-split ${V#lo:} --cu-mode lo" ;;
+      rs:*) K=$(echo ${V#rs:} | cut -d/ -f1); PR=$(echo ${V#rs:} | cut -s -d/ -f2)
+            A="--render-streams $K --prep-priority ${PR:-0}" ;;
       *) A="--cu-split $V" ;;
     esac
     tag=$(echo "$V" | tr -c 'A-Za-z0-9_\n' '_')

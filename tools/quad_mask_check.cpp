@@ -1,9 +1,11 @@
-// Host check of the single-frame quad tests (gsr_cull.h): (1) quad_reach4 equals box_reach on each
-// 4x4 quad (the shared-term form computes the same values); (2) the quad masks binning stores
-// (binning.hip quad_mask: reach_bbox + quad_bits_bbox) never clear a quad with a pixel centre at
-// Q <= K = 2 ln(255 o) (float64 brute force over its 16 pixels) -- they only drop pairs the blend
-// skips anyway -- and report how many quads they keep beyond those.  Random conics around one strip,
-// including means inside, on the edges and far away, and thin rotated ellipses:
+// Host check of the single-frame quad tests (gsr_cull.h): (1) quad_reach4 -- the quad masks binning
+// stores (binning.hip k_quad_masks) -- equals box_reach on each 4x4 quad (the shared-term form
+// computes the same values) and never clears a quad with a pixel centre at Q <= K = 2 ln(255 o)
+// (float64 brute force over its 16 pixels): it only drops pairs the blend skips anyway; (2) the
+// conservative reach boxes (reach_bbox + quad_bits_bbox: A/B and analysis only, not stored by the
+// product) never clear such a quad either.  Random conics around strips near the origin and around
+// pixel (1600, 1024) (float slack at large coordinates), including means inside, on the edges and far
+// away, and thin rotated ellipses:
 //   hipcc -O2 -std=c++17 -ffp-contract=off --offload-arch=gfx950 -I guava_renderer_amd/csrc \
 //         tools/quad_mask_check.cpp -o /tmp/qmc && /tmp/qmc
 #include "gsr_cull.h"
@@ -17,7 +19,8 @@ int main() {
     std::uniform_real_distribution<float> U(0.f, 1.f);
     long n = 0, mismatch = 0, missed = 0, need = 0, kept = 0, bb_missed = 0, bb_kept = 0;
     for (int it = 0; it < 400000; it++) {
-        const float sx0 = 8.f * (float)(it % 5), sy0 = 8.f * (float)((it / 5) % 3);
+        const float sx0 = 8.f * (float)(it % 5) + ((it >> 4) & 1 ? 1600.f : 0.f),
+                    sy0 = 8.f * (float)((it / 5) % 3) + ((it >> 5) & 1 ? 1024.f : 0.f);
         const float s1 = std::exp(-3.f + 6.f * U(rng)), s2 = std::exp(-3.f + 6.f * U(rng));
         const float th = 6.2831853f * U(rng);
         const float cs = std::cos(th), sn = std::sin(th);

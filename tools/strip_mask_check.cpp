@@ -1,6 +1,7 @@
 // Host check of the scatter's strip test (binning.hip: strip_mask): it never clears a strip that
 // has a pixel centre with Q <= K = 2 ln(255 o) (brute force over the strip's 64 pixels, float64),
-// and how many strips it keeps beyond those.  Random conics around one tile:
+// and how many strips it keeps beyond those; and that strip_mask (sub_reach4<8>) gives the bits of the
+// four box_reach calls (strip_mask_loop).  Random conics around tiles near the origin and far from it:
 //   hipcc -O2 -std=c++17 -ffp-contract=off --offload-arch=gfx950 -I guava_renderer_amd/csrc \
 //         -I include tools/strip_mask_check.cpp -o /tmp/smc && /tmp/smc
 #include "../guava_renderer_amd/csrc/binning.hip"
@@ -17,9 +18,10 @@ int xcd_queue_map() { return 2; }
 int main() {
     std::mt19937 rng(7);
     std::uniform_real_distribution<float> U(0.f, 1.f);
-    long n = 0, kept = 0, missed = 0, need = 0;
-    const int tx = 3, ty = 5;
+    long n = 0, kept = 0, missed = 0, need = 0, mism = 0;
     for (int it = 0; it < 2000000; it++) {
+        // tiles near the origin and around pixel (1600, 1024): float slack at large coordinates
+        const int tx = (it & 1) ? 100 : 3, ty = (it & 2) ? 64 : 5;
         // conic of a 2D covariance with random axes and angle, mean near the tile
         const float s1 = 0.3f + 12.f * U(rng) * U(rng), s2 = 0.3f + 12.f * U(rng) * U(rng), th = 6.2831853f * U(rng);
         const float cs = cosf(th), sn = sinf(th);
@@ -30,6 +32,7 @@ int main() {
         const float2 m = make_float2(tx * 16 - 20.f + 56.f * U(rng), ty * 16 - 20.f + 56.f * U(rng));
         const float4 pre = gsr::strip_pre(co);
         const uint32_t a = gsr::strip_mask(co, pre, m, tx, ty);
+        mism += a != gsr::strip_mask_loop(co, pre, m, tx, ty);  // the shared-term form: same bits
         for (int s = 0; s < gsr::kStrips; s++) {
             int x0, y0;
             gsr::strip_origin(tx, ty, s, x0, y0);
@@ -45,6 +48,7 @@ int main() {
             missed += hit && !((a >> s) & 1);
         }
     }
-    printf("strips %ld, with a pixel at Q <= K %ld, kept %ld, wrongly cleared %ld\n", n, need, kept, missed);
-    return missed ? 1 : 0;
+    printf("strips %ld, with a pixel at Q <= K %ld, kept %ld, wrongly cleared %ld, mismatches vs the box_reach loop %ld\n",
+           n, need, kept, missed, mism);
+    return (missed || mism) ? 1 : 0;
 }
