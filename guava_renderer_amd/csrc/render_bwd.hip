@@ -558,7 +558,10 @@ void launch_render_bwd(const Dims& d, const Inputs& in_, const GeomArena& g, con
     hipLaunchKernelGGL(k_zero_bwd_queues, dim3(1), dim3(64), 0, s, g.ctrl);
     hipMemsetAsync(g.gterm, 0, (size_t)d.B * d.P * kGtWords * sizeof(float), s);
     const bool invd = gr.invd != 0;
-    const dim3 grid(min((nwaves + 3) / 4, persistent_grid(2))), blk(GSR_TILE_PIX);
+    // GSR_BWD_WG_PER_CU (A/B): 1 halves the residency (one wave per SIMD), what an LDS row cache
+    // for a tile-merged write-back would cost at this register and LDS budget
+    static const int wg_per_cu = tune_env("GSR_BWD_WG_PER_CU", 2);
+    const dim3 grid(min((nwaves + 3) / 4, persistent_grid(wg_per_cu))), blk(GSR_TILE_PIX);
 #ifdef GSR_TUNING
     // timing ablations (wrong gradients by construction): tools/build_ab.py builds only
     static const int ablate = tune_env("GSR_BWD_ABLATE", 0);

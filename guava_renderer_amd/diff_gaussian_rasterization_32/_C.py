@@ -335,12 +335,14 @@ def rasterize_inference(background, means3D, colors, opacity, scales, rotations,
         return None
     if numerics is None:
         numerics = DEFAULT_NUMERICS
-    ts = (background, means3D, colors, opacity, scales, rotations, viewmatrix, projmatrix)
-    for t_ in ts:
-        if t_ is not None and t_.numel() and (t_.device != dev or t_.dtype != torch.float32):
-            return None  # (the general path raises the reference's errors)
-    background, means3D, colors, opacity, scales, rotations, viewmatrix, projmatrix = (
-        t_.contiguous() if t_ is not None and t_.numel() else t_ for t_ in ts)
+    ts = [background, means3D, colors, opacity, scales, rotations, viewmatrix, projmatrix]
+    f32 = torch.float32
+    for i, t_ in enumerate(ts):  # (one pass: device / dtype check and contiguous rows)
+        if t_ is not None and t_.numel():
+            if t_.get_device() != dix or t_.dtype is not f32:
+                return None  # (the general path raises the reference's errors)
+            ts[i] = t_.contiguous()
+    background, means3D, colors, opacity, scales, rotations, viewmatrix, projmatrix = ts
     if colors.data_ptr() % 16:
         colors = colors.clone()
     cov = cov3D_precomp if (cov3D_precomp is not None and cov3D_precomp.numel()) else None

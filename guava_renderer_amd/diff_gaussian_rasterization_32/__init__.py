@@ -161,10 +161,33 @@ class GaussianRasterizationSettings(NamedTuple):
     antialiasing: bool
 
 
+def _module_state_factory():
+    """nn.Module.__init__'s instance attributes, as a function returning fresh containers: GUAVA builds
+    one GaussianRasterizer_32 per frame (gaussian_render.py:37-51), and nn.Module.__init__ (API-usage
+    logging, ~17 attribute sets through Module.__setattr__ paths) is a sizeable share of the
+    per-frame host time on the serial drop-in loop.  The attributes and their types are taken from a
+    real nn.Module of this torch version, so the instance is an ordinary nn.Module."""
+    proto = nn.Module().__dict__
+    scalars = {k: v for k, v in proto.items() if not isinstance(v, (dict, set, list))}
+    containers = [(k, type(v)) for k, v in proto.items() if isinstance(v, (dict, set, list))]
+
+    def fresh():
+        d = dict(scalars)
+        for k, ty in containers:
+            d[k] = ty()
+        return d
+    return fresh
+
+
+_module_state = _module_state_factory()
+
+
 class GaussianRasterizer_32(nn.Module):
     def __init__(self, raster_settings):
-        super().__init__()
-        self.raster_settings = raster_settings
+        # (nn.Module.__init__'s state, built directly: _module_state_factory)
+        d = self.__dict__
+        d.update(_module_state())
+        d["raster_settings"] = raster_settings
 
     def markVisible(self, positions):
         # Mark visible points (based on frustum culling for camera) with a boolean
