@@ -437,17 +437,48 @@ __global__ __launch_bounds__(1024) void k_bucket_scan(Dims d, GeomArena g) {
     if (threadIdx.x == 0) g.fstat[kFsWords * b + kFsVisible] = total;
 }
 
+// SCAN (one frame, NB + 1 words fitting the LDS): k_bucket_scan folded in -- every workgroup scans
+// the frame's bucket counts itself in LDS (the same runs and block scan as k_bucket_scan, so the same
+// starts), and workgroup 0 writes the starts back, lists the large buckets and the visible count:
+// one launch fewer per single-frame forward.
+template <bool SCAN = false>
 __global__ __launch_bounds__(kScanBlock) void k_bucket_scatter(Dims d, GeomArena g) {
+    extern __shared__ uint32_t btab[];  // SCAN: the frame's NB + 1 bucket starts
     if (g.ctrl[kCtrlOverflow]) return;
     const int b = blockIdx.y;
     const int i = blockIdx.x * kScanBlock + threadIdx.x;
+    uint32_t* bs = g.bstart + (int64_t)b * (d.NB + 1);
+    if constexpr (SCAN) {
+        __shared__ uint32_t sh[kScanBlock / 64 + 1];
+        const int n = d.NB + 1;
+        for (int k = threadIdx.x; k < n; k += kScanBlock) btab[k] = bs[k];
+        __syncthreads();
+        const int per = (n + kScanBlock - 1) / kScanBlock;
+        const int beg = threadIdx.x * per, end = min(n, beg + per);
+        uint32_t sum = 0;
+        for (int k = beg; k < end; k++) sum += btab[k];
+        uint32_t total;
+        uint32_t ex = block_excl_scan<uint32_t, kScanBlock>(sum, &total, sh);  // (barriers inside)
+        for (int k = beg; k < end; k++) {
+            const uint32_t c = btab[k];
+            btab[k] = ex;
+            if (blockIdx.x == 0 && c > (uint32_t)kTinyBucket)
+                g.big[atomicAdd(&g.ctrl[kCtrlNumBig], 1u)] = (uint32_t)(b * d.NB + k);
+            ex += c;
+        }
+        __syncthreads();
+        if (blockIdx.x == 0) {
+            for (int k = threadIdx.x; k < n; k += kScanBlock) bs[k] = btab[k];
+            if (threadIdx.x == 0) g.fstat[kFsWords * b + kFsVisible] = total;
+        }
+    }
     if (i >= d.P) return;
     const int64_t gid = (int64_t)b * d.P + i;
     if (!g.tiles[gid]) return;
     const uint32_t kmin = ~g.fstat[kFsWords * b + kFsNotKeyMax], kmax = g.fstat[kFsWords * b + kFsKeyMax];
     const uint32_t key = __float_as_uint(g.depth[gid]);
     const uint32_t bk = bucket_of(key, kmin, bucket_scale(kmin, kmax, d.NB), d.NB);
-    const uint32_t pos = g.bstart[(int64_t)b * (d.NB + 1) + bk] + g.bslot[gid];
+    const uint32_t pos = (SCAN ? btab[bk] : bs[bk]) + g.bslot[gid];
     g.skey[(int64_t)b * d.P + pos] = ((uint64_t)key << 32) | (uint32_t)i;
 }
 
@@ -544,8 +575,15 @@ void launch_depth_sort(const Dims& d, const GeomArena& g, hipStream_t s, int64_t
     } else {
         hipLaunchKernelGGL(k_bucket_count, dim3(d.nblk, d.B), dim3(kScanBlock), 0, s, d, g);
     }
-    hipLaunchKernelGGL(k_bucket_scan, dim3(d.B), dim3(1024), 0, s, d, g);
-    hipLaunchKernelGGL(k_bucket_scatter, dim3(d.nblk, d.B), dim3(kScanBlock), 0, s, d, g);
+    // GSR_B1_SCAN_FUSED=0: the single-frame bucket scan in its own launch (A/B)
+    static const bool scan_fused_on = tune_env("GSR_B1_SCAN_FUSED", 1) != 0;
+    if (d.B == 1 && scan_fused_on && (size_t)(d.NB + 1) * 4 <= 65536) {
+        hipLaunchKernelGGL(k_bucket_scatter<true>, dim3(d.nblk, d.B), dim3(kScanBlock), (size_t)(d.NB + 1) * 4, s, d,
+                           g);
+    } else {
+        hipLaunchKernelGGL(k_bucket_scan, dim3(d.B), dim3(1024), 0, s, d, g);
+        hipLaunchKernelGGL(k_bucket_scatter<false>, dim3(d.nblk, d.B), dim3(kScanBlock), 0, s, d, g);
+    }
     hipLaunchKernelGGL(k_bucket_rank, dim3(d.nblk, d.B), dim3(kScanBlock), 0, s, d, g);
     static bool attr = false;
     if (!attr) {
@@ -862,7 +900,57 @@ __global__ __launch_bounds__(1024) void k_tile_scan_place1(Dims d, GeomArena g, 
     }
 }
 
+// k_tile_scan_place1's work by one workgroup of NT threads (the single-frame ordered scatter's
+// workgroup 0, TS): ranges, the work-list histogram, the longest-first work list, the non-empty count
+template <int NT>
+__device__ void tile_scan_place_wg(const Dims& d, const GeomArena& g, const ImageArena& im) {
+    __shared__ uint32_t sh[NT / 64 + 1];
+    __shared__ uint32_t h[kLptBuckets];
+    const bool ovf = g.ctrl[kCtrlOverflow] != 0;
+    if (threadIdx.x < kLptBuckets) h[threadIdx.x] = 0;
+    const int per = (d.T + NT - 1) / NT;
+    const int beg = threadIdx.x * per, end = min(d.T, beg + per);
+    const uint32_t* cnt = im.tile_count;
+    uint32_t sum = 0;
+    if (!ovf)
+        for (int t = beg; t < end; t++) sum += cnt[t];
+    uint32_t total;
+    uint32_t ex = block_excl_scan<uint32_t, NT>(sum, &total, sh) + (ovf ? 0u : g.fstat[kFsRBase]);
+    for (int t = beg; t < end; t++) {
+        const uint32_t c = ovf ? 0u : cnt[t];
+        im.ranges[t] = c ? make_uint2(ex, ex + c) : make_uint2(0u, 0u);
+        atomicAdd(&h[c ? __clz(c) : kLptBuckets - 1], 1u);
+        ex += c;
+    }
+    __syncthreads();
+    if (threadIdx.x < kLptBuckets) im.lpt_hist[threadIdx.x] = h[threadIdx.x];
+    __syncthreads();
+    if (threadIdx.x == 0) {  // bucket starts, longest lists first, empty tiles last
+        uint32_t acc = 0;
+        for (int bk = 0; bk < kLptBuckets; bk++) {
+            const uint32_t t = h[bk];
+            if (bk == kLptBuckets - 1) g.ctrl[kCtrlNonEmpty] = acc;
+            h[bk] = acc;
+            acc += t;
+        }
+    }
+    __syncthreads();
+    for (int t = threadIdx.x; t < d.T; t += NT) {
+        const uint32_t c = ovf ? 0u : cnt[t];
+        im.work_list[atomicAdd(&h[c ? __clz(c) : kLptBuckets - 1], 1u)] = (uint32_t)t;
+    }
+}
+
+// the single-frame tile scan runs inside the ordered scatter (its workgroup 0, k_ordered_scatter TS;
+// the production scatter only: the A/B variants keep the separate launch)
+static bool tile_scan_in_scatter(const Dims& d) {
+    static const bool on = tune_env("GSR_B1_TILESCAN_FUSED", 1) != 0 && tune_env("GSR_SCATTER_ABLATE", 0) == 0 &&
+                           tune_env("GSR_SCATTER_WAVESEARCH", 1) != 0;  // 0: its own launch (A/B)
+    return on && d.B == 1 && d.P > 0;
+}
+
 void launch_tile_scan(const Dims& d, const GeomArena& g, const ImageArena& im, hipStream_t s) {
+    if (tile_scan_in_scatter(d)) return;
     if (d.B == 1) {
         hipLaunchKernelGGL(k_tile_scan_place1, dim3(1), dim3(1024), 0, s, d, g, im);
         return;
@@ -1034,7 +1122,10 @@ void launch_quad_masks(const Dims& d, const GeomArena& g, const ImageArena& im, 
 // (q0, q0 + i]) with o0 the owner of q0 (the previous step's last lane): every lane reads the end of
 // slot o0 + lane, marks it in a per-wave 64-entry LDS row when it falls in the window, and one
 // ballot of the row gives every lane its count -- in place of an 8-step binary search per instance.
-template <int ABL, bool WS>  // timing ablations (GSR_SCATTER_ABLATE): 1 = no strip test, 2 = no list store
+// TS (one frame): k_tile_scan_place1 folded in -- workgroup 0 writes the ranges and the render work
+// list (tile_scan_place_wg), and every workgroup takes its list positions from its own exclusive scan
+// of the tile counts (the same sums) instead of reading the ranges: one launch fewer per frame.
+template <int ABL, bool WS, bool TS = false>  // timing ablations (GSR_SCATTER_ABLATE): 1 = no strip test, 2 = no list store
 __global__ __launch_bounds__(kSlots) __attribute__((amdgpu_waves_per_eu(6))) void k_ordered_scatter(Dims d, GeomArena g, ImageArena im, BinArena bn, int xcd_order) {
     uint32_t sink = 0;
     __shared__ uint32_t s_mark[kSlots];  // WS: one 64-entry row per wave
@@ -1047,6 +1138,10 @@ __global__ __launch_bounds__(kSlots) __attribute__((amdgpu_waves_per_eu(6))) voi
     __shared__ float4 s_co[kSlots];
     __shared__ float4 s_pre[kSlots];
     __shared__ float2 s_m[kSlots];
+    if (TS && blockIdx.x == 0) {
+        tile_scan_place_wg<kSlots>(d, g, im);
+        __syncthreads();
+    }
     if (g.ctrl[kCtrlOverflow]) return;
     // XCD-aware order (GSR_SCATTER_XCD, default on): workgroup L runs on XCD L % 8, and XCD x takes
     // the x-th eighth of the (frame, chunk) items in chunk order, so consecutive chunks -- which
@@ -1072,8 +1167,21 @@ __global__ __launch_bounds__(kSlots) __attribute__((amdgpu_waves_per_eu(6))) voi
     uint32_t* base = (uint32_t*)(masks + 4 * (d.gx + d.gy));
     // list position of this chunk's first instance in every tile of the frame
     const uint32_t* tbl = g.table + ((int64_t)b * d.nchunk + c) * d.T;
-    const uint2* rg = im.ranges + (int64_t)b * d.T;
-    for (int t = tid; t < d.T; t += kSlots) base[t] = rg[t].x + tbl[t];
+    if constexpr (TS) {  // (one frame) the tile's list start from this workgroup's own scan of the counts
+        const int per = (d.T + kSlots - 1) / kSlots;
+        const int beg = tid * per, end = min(d.T, beg + per);
+        uint32_t sum = 0;
+        for (int t = beg; t < end; t++) sum += im.tile_count[t];
+        uint32_t total;
+        uint32_t ex = block_excl_scan<uint32_t, kSlots>(sum, &total, s_sh) + g.fstat[kFsRBase];
+        for (int t = beg; t < end; t++) {
+            base[t] = ex + tbl[t];
+            ex += im.tile_count[t];
+        }
+    } else {
+        const uint2* rg = im.ranges + (int64_t)b * d.T;
+        for (int t = tid; t < d.T; t += kSlots) base[t] = rg[t].x + tbl[t];
+    }
     for (int pass = 0; pass < d.chunk / kSlots; pass++) {
         const uint32_t j0 = (uint32_t)c * d.chunk + (uint32_t)pass * kSlots;
         if (j0 >= V) break;  // uniform
@@ -1185,7 +1293,7 @@ void launch_ordered_scatter(const Dims& d, const GeomArena& g, const ImageArena&
     static size_t attr = 0;
     if (lds > 65536 && attr < lds) {
         attr = lds;
-        for (const void* f : {(const void*)k_ordered_scatter<0, true>,
+        for (const void* f : {(const void*)k_ordered_scatter<0, true>, (const void*)k_ordered_scatter<0, true, true>,
 #ifdef GSR_TUNING
                               (const void*)k_ordered_scatter<1, true>, (const void*)k_ordered_scatter<2, true>,
                               (const void*)k_ordered_scatter<3, true>,
@@ -1207,6 +1315,7 @@ void launch_ordered_scatter(const Dims& d, const GeomArena& g, const ImageArena&
     (void)abl;
 #endif
     if (!ws) hipLaunchKernelGGL((k_ordered_scatter<0, false>), gr, bl, lds, s, d, g, im, b, xo);
+    else if (tile_scan_in_scatter(d)) hipLaunchKernelGGL((k_ordered_scatter<0, true, true>), gr, bl, lds, s, d, g, im, b, xo);
     else hipLaunchKernelGGL((k_ordered_scatter<0, true>), gr, bl, lds, s, d, g, im, b, xo);
 }
 

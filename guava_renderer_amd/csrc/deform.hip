@@ -427,31 +427,26 @@ __device__ __forceinline__ float blend_tiled_one(const float* __restrict__ coef,
 
 // pose (single-frame LBS, gsr_lbs_sp): the pose features are formed here from the frame's pose
 // (rodrigues_one, the same expressions as k_lbs_rodrigues) instead of read from a launch before
-__global__ __launch_bounds__(256) void k_lbs_blend_tiled1(int M, int NB, int NP, const float* __restrict__ vt,
-                                                          const float* __restrict__ betas,
-                                                          const float4* __restrict__ sd_tiled,
-                                                          const float* __restrict__ feat,
-                                                          const float4* __restrict__ pd_tiled,
-                                                          float* __restrict__ v_shaped,
-                                                          float* __restrict__ v_posed,
-                                                          const float* __restrict__ pose, int pose2rot) {
+__device__ __forceinline__ void blend_tiled1_block(const Blend1Job& j, int t) {
     __shared__ float red[2][4][64];
     __shared__ float sfeat[9 * (GSR_LBS_MAX_JOINTS - 1)];
+    const int M = j.M, NB = j.NB, NP = j.NP;
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, hi = lane >> 5, l32 = lane & 31;
-    const int t = blockIdx.x, m = t * 32 + l32;
-    if (pose && NP > 0 && v_posed) {
+    const int m = t * 32 + l32;
+    const float* feat = j.feat;
+    if (j.pose && NP > 0 && j.v_posed) {
         const int jn = NP / 9;  // J - 1 posed joints (pose_feature skips the root)
         if ((int)threadIdx.x < jn) {
             float R[9];
-            rodrigues_one(pose, (int)threadIdx.x + 1, pose2rot, R);
+            rodrigues_one(j.pose, (int)threadIdx.x + 1, j.pose2rot, R);
 #pragma unroll
             for (int e = 0; e < 9; e++) sfeat[9 * threadIdx.x + e] = R[e] - ((e % 4) == 0 ? 1.0f : 0.0f);
         }
         __syncthreads();
         feat = sfeat;
     }
-    red[0][w][lane] = NB > 0 ? blend_tiled_one(betas, sd_tiled, NB, t, w, hi, lane) : 0.f;
-    red[1][w][lane] = (NP > 0 && v_posed) ? blend_tiled_one(feat, pd_tiled, NP, t, w, hi, lane) : 0.f;
+    red[0][w][lane] = NB > 0 ? blend_tiled_one(j.betas, j.sd_tiled, NB, t, w, hi, lane) : 0.f;
+    red[1][w][lane] = (NP > 0 && j.v_posed) ? blend_tiled_one(feat, j.pd_tiled, NP, t, w, hi, lane) : 0.f;
     __syncthreads();
     if (w == 0 && hi == 0 && m < M) {
         float S = 0.f, Pz = 0.f;
@@ -460,10 +455,20 @@ __global__ __launch_bounds__(256) void k_lbs_blend_tiled1(int M, int NB, int NP,
             S += red[0][u][l32] + red[0][u][l32 + 32];
             Pz += red[1][u][l32] + red[1][u][l32 + 32];
         }
-        const float vs = NB > 0 ? vt[m] + S : vt[m];
-        v_shaped[m] = vs;
-        if (v_posed) v_posed[m] = Pz + vs;
+        const float vs = NB > 0 ? j.vt[m] + S : j.vt[m];
+        j.v_shaped[m] = vs;
+        if (j.v_posed) j.v_posed[m] = Pz + vs;
     }
+}
+
+__global__ __launch_bounds__(256) void k_lbs_blend_tiled1(Blend1Job j) { blend_tiled1_block(j, blockIdx.x); }
+
+// Two independent single-frame blends in one launch (EHM's FLAME head blend beside the body's shape
+// blend, gsr_ehm_forward at B = 1): workgroups [0, na) take job a, the rest job b.  One launch fewer
+// on the serial per-frame path, and the two partial grids share the chip instead of running in turn.
+__global__ __launch_bounds__(256) void k_lbs_blend_tiled1_pair(Blend1Job a, int na, Blend1Job b) {
+    if ((int)blockIdx.x < na) blend_tiled1_block(a, blockIdx.x);
+    else blend_tiled1_block(b, blockIdx.x - na);
 }
 
 // blend launcher: the matrix-core kernel for more than kLbsFrames frames, the streaming one otherwise
@@ -497,6 +502,19 @@ static void lbs_blend_attr(size_t lds) {
     }
 }
 
+Blend1Job blend1_job(int M, int NB, int NP, const float* vt, const float* betas, const float* feat, float* vs,
+                     float* vp, const GsrLbsSparse* sp, const float* pose, int pose2rot) {
+    return Blend1Job{M, NB, vp ? NP : 0, pose2rot, vt, betas, reinterpret_cast<const float4*>(sp->shapedirs_tiled),
+                     feat, reinterpret_cast<const float4*>(sp->posedirs_tiled), vs, vp, pose};
+}
+
+// whether launch_blend takes the single-frame tiled kernel (k_lbs_blend_tiled1) for these arguments
+bool blend_tiled1_applies(int B, int NB, int NP, const float* vp, const GsrLbsSparse* sp) {
+    static const bool tiled_on = tune_env("GSR_BLEND_TILED", 1) != 0;
+    return B == 1 && tiled_on && sp && (NB == 0 || sp->shapedirs_tiled) && (NP == 0 || !vp || sp->posedirs_tiled) &&
+           (NB > 0 || (NP > 0 && vp));
+}
+
 static void launch_blend(int B, int M, int NB, int NP, const float* vt, int64_t vt_stride, const float* betas,
                          const float* sd_t, const float* feat, const float* pd, float* vs, float* vp,
                          hipStream_t s, const GsrLbsSparse* sp, const float* pose, int pose2rot) {
@@ -520,9 +538,8 @@ static void launch_blend(int B, int M, int NB, int NP, const float* vt, int64_t 
         return;
     }
     if (tiled && B == 1) {
-        hipLaunchKernelGGL(k_lbs_blend_tiled1, dim3((M + 31) / 32), dim3(256), 0, s, M, NB, vp ? NP : 0, vt, betas,
-                           reinterpret_cast<const float4*>(sp->shapedirs_tiled), feat,
-                           reinterpret_cast<const float4*>(sp->posedirs_tiled), vs, vp, pose, pose2rot);
+        const Blend1Job j = blend1_job(M, NB, NP, vt, betas, feat, vs, vp, sp, pose, pose2rot);
+        hipLaunchKernelGGL(k_lbs_blend_tiled1, dim3((M + 31) / 32), dim3(256), 0, s, j);
         return;
     }
     if (B > kLbsFrames && !valu_only) {
@@ -1310,7 +1327,8 @@ int gsr::lbs_run(int B, int V, int J, int NB, const float* v_template, int64_t v
                  const float* lbs_weights_t, const float* joints_offset, float* verts,
                  float* joints_transformed, float* joints, float* vert_transforms,
                  float* joint_transforms, float* v_shaped, char* workspace, const GsrLbsSparse* sp,
-                 void* stream, bool skin) {
+                 void* stream, bool skin, const Blend1Job* companion, bool* companion_done) {
+    if (companion_done) *companion_done = false;
     if (B <= 0 || V <= 0) return api_fail(GSR_ERR_ARG, "gsr_lbs: B and V must be positive");
     if (int rc = check_sparse(sp, J, betas ? NB : 0, V, "gsr_lbs")) return rc;
     if (J < 1 || J > GSR_LBS_MAX_JOINTS) return api_fail(GSR_ERR_ARG, "gsr_lbs: J must be in [1, 64]");
@@ -1350,8 +1368,17 @@ int gsr::lbs_run(int B, int V, int J, int NB, const float* v_template, int64_t v
                            pose2rot, a.rot, a.feat);
         if (int rc = hip_check("lbs_rodrigues")) return rc;
     }
-    launch_blend(B, M, NB, NP, v_template, v_template_stride, betas, shapedirs_t, a.feat, posedirs, vs, a.vp, s, sp,
-                 fused ? pose : nullptr, pose2rot);
+    if (companion && companion_done && blend_tiled1_applies(B, NB, NP, a.vp, sp)) {
+        // this blend and the caller's independent one in one launch (k_lbs_blend_tiled1_pair)
+        const Blend1Job ja = blend1_job(M, NB, NP, v_template, betas, a.feat, vs, a.vp, sp, fused ? pose : nullptr,
+                                        pose2rot);
+        const int na = (M + 31) / 32, nb = (companion->M + 31) / 32;
+        hipLaunchKernelGGL(k_lbs_blend_tiled1_pair, dim3(na + nb), dim3(256), 0, s, ja, na, *companion);
+        *companion_done = true;
+    } else {
+        launch_blend(B, M, NB, NP, v_template, v_template_stride, betas, shapedirs_t, a.feat, posedirs, vs, a.vp, s,
+                     sp, fused ? pose : nullptr, pose2rot);
+    }
     if (int rc = hip_check("lbs_blend")) return rc;
     // single frame with the CSR regressor: the joints are regressed inside the chain's workgroup
     // (GSR_CHAIN_JOINTS=0: their own launch, A/B)
@@ -1487,6 +1514,17 @@ int gsr_blend_joints_sp(int B, int V, int J, int NB, const float* v_template, in
                         const float* betas, const float* shapedirs_t, const float* J_regressor,
                         const float* joints_offset, float* v_shaped, float* joints, const GsrLbsSparse* sp,
                         void* stream) {
+    return gsr::blend_joints_run(B, V, J, NB, v_template, v_template_stride, betas, shapedirs_t, J_regressor,
+                                 joints_offset, v_shaped, joints, sp, stream, false);
+}
+
+}  // extern "C"
+
+// gsr_blend_joints_sp; blend_done: the blend shapes were launched already (k_lbs_blend_tiled1_pair)
+int gsr::blend_joints_run(int B, int V, int J, int NB, const float* v_template, int64_t v_template_stride,
+                          const float* betas, const float* shapedirs_t, const float* J_regressor,
+                          const float* joints_offset, float* v_shaped, float* joints, const GsrLbsSparse* sp,
+                          void* stream, bool blend_done) {
     if (B <= 0 || V <= 0 || J < 1) return api_fail(GSR_ERR_ARG, "gsr_blend_joints: bad sizes");
     if (int rc = check_sparse(sp, 1, betas ? NB : 0, V, "gsr_blend_joints")) return rc;
     if (!v_template || !J_regressor || !v_shaped || !joints)
@@ -1499,11 +1537,16 @@ int gsr_blend_joints_sp(int B, int V, int J, int NB, const float* v_template, in
     if (lbs_blend_lds(NB, 0, kLbsFrames, kLbsSplit) > 160 * 1024) return api_fail(GSR_ERR_ARG, "gsr_blend_joints: NB too large for LDS");
     hipStream_t s = (hipStream_t)stream;
     const int M = V * 3;
-    launch_blend(B, M, NB, 0, v_template, v_template_stride, betas, shapedirs_t, nullptr, nullptr, v_shaped, nullptr, s, sp);
-    if (int rc = hip_check("blend_shapes")) return rc;
+    if (!blend_done) {
+        launch_blend(B, M, NB, 0, v_template, v_template_stride, betas, shapedirs_t, nullptr, nullptr, v_shaped, nullptr,
+                     s, sp);
+        if (int rc = hip_check("blend_shapes")) return rc;
+    }
     launch_joints(B, V, J, J_regressor, sp, v_shaped, joints_offset, joints, s);
     return hip_check("vertices2joints");
 }
+
+extern "C" {
 
 size_t gsr_lbs_tiled_floats(int K, int M) {
     if (K <= 0 || M <= 0) return 0;

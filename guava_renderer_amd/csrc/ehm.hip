@@ -212,13 +212,22 @@ int gsr_ehm_forward(const GsrEhm* ehm, int B, const GsrEhmParam* params, const G
     // into the splice below (ELL weights; GSR_EHM_SKIN_SPLICE=0: separate, A/B)
     static const bool skin_splice_on = tune_env("GSR_EHM_SKIN_SPLICE", 1) != 0;
     const bool fuse = skin_splice_on && e.flame.sparse && e.flame.sparse->skin_k > 0;
+    // one frame: the body's shape blend (independent of the head) rides in the head blend's launch
+    Blend1Job body_shape{};
+    static const bool pair_on = tune_env("GSR_EHM_PAIR", 1) != 0;  // 0: separate launches (A/B)
+    const bool pair = pair_on && B == 1 && blend_tiled1_applies(1, NBb, 0, nullptr, e.body.sparse);
+    if (pair)
+        body_shape = blend1_job(Vb * 3, NBb, 0, e.body.v_template, a.betas_b, nullptr, a.vt, nullptr, e.body.sparse,
+                                nullptr, 1);
+    bool body_blended = false;
     int rc = lbs_run(B, Vh, Jh, NBh, e.flame.v_template, 0, a.betas_h, e.flame.shapedirs_t, a.pose_h, 1,
                      e.flame.posedirs, e.flame.J_regressor, e.flame.parents_host, e.flame.lbs_weights_t, nullptr,
-                     a.hv, a.hj, nullptr, nullptr, nullptr, nullptr, a.ws_h, e.flame.sparse, stream, !fuse);
+                     a.hv, a.hj, nullptr, nullptr, nullptr, nullptr, a.ws_h, e.flame.sparse, stream, !fuse,
+                     pair ? &body_shape : nullptr, &body_blended);
     if (rc) return rc;
     // body template: blend shapes + joints (+ offset) (EHM.py:114-118)
-    rc = gsr_blend_joints_sp(B, Vb, Jb, NBb, e.body.v_template, 0, a.betas_b, e.body.shapedirs_t, e.body.J_regressor,
-                             joff, a.vt, a.tj, e.body.sparse, stream);
+    rc = blend_joints_run(B, Vb, Jb, NBb, e.body.v_template, 0, a.betas_b, e.body.shapedirs_t, e.body.J_regressor,
+                          joff, a.vt, a.tj, e.body.sparse, stream, body_blended);
     if (rc) return rc;
     // head splice (EHM.py:72-75, :121-124)
     if (fuse)
