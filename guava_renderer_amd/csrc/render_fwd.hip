@@ -787,10 +787,10 @@ struct QSlot {
 #endif
 constexpr int kQRch = GSR_QUAD_RCH;
 constexpr int kQRing = kQRch <= 4 ? 512 : 1024;  // ring entries per wave
-// live entries: a refill (ensure) runs while fewer than 4 GSR_QUAD_SLOTS are queued and adds at most
+// live entries: a refill (ensure) runs while fewer than 8 GSR_QUAD_SLOTS are queued and adds at most
 // 64 kQRch; behind the head, up to 4 GSR_QUAD_SLOTS entries of the steps whose operands are in flight;
 // past the tail, 4 GSR_QUAD_SLOTS null entries once the list is exhausted
-static_assert(kQRing >= 64 * kQRch + 12 * GSR_QUAD_SLOTS, "quad ring too small for a refill beside the slots in flight");
+static_assert(kQRing >= 64 * kQRch + 16 * GSR_QUAD_SLOTS, "quad ring too small for a refill beside the slots in flight");
 constexpr uint32_t kQNull = 0x07FFFFFFu;  // the null Gaussian: record / feature offsets out of range
 
 // TL (gsr_render_timeline): per quad item, (start, end) in 100 MHz ticks, steps | refills << 16, list
@@ -892,17 +892,22 @@ __global__ __launch_bounds__(GSR_TILE_PIX) __attribute__((amdgpu_waves_per_eu(GS
             const uint32_t* __restrict__ qm = bn.qmask + range.x;
             int base = 0;                  // first list position of the next refill
             uint32_t head = 0, tail = 0;   // ring counters (head advances by 4: entries never wrap in a step)
-            uint32_t ec[kQRch], mc[kQRch], en[kQRch], mn[kQRch];
+            uint32_t ec[kQRch], mc[kQRch];
+            // list entries and quad masks through buffer resources over the tile's list: a position past
+            // its end reads 0 (nothing kept) without a branch -- a conditional load merged into its
+            // register compiled to a copy that waited for the load at once, i.e. for every operand load
+            // in flight, at every refill
+            const __amdgpu_buffer_rsrc_t lrs = __builtin_amdgcn_make_buffer_rsrc((void*)plist, 0, n * 4, 0x00020000);
+            const __amdgpu_buffer_rsrc_t mrs = __builtin_amdgcn_make_buffer_rsrc((void*)qm, 0, n * 4, 0x00020000);
             auto load_chunks = [&](int b0, uint32_t (&e)[kQRch], uint32_t (&m)[kQRch]) {
 #pragma unroll
                 for (int u = 0; u < kQRch; u++) {
-                    const int p = b0 + 64 * u + lane;
-                    e[u] = p < n ? plist[p] : 0u;
-                    m[u] = p < n ? (uint32_t)qm[p] : 0u;  // (zero past the list's end: nothing kept)
+                    const int off = (b0 + 64 * u + lane) * 4;
+                    e[u] = __builtin_amdgcn_raw_buffer_load_b32(lrs, off, 0, 0);
+                    m[u] = __builtin_amdgcn_raw_buffer_load_b32(mrs, off, 0, 0);
                 }
             };
             load_chunks(0, ec, mc);
-            load_chunks(64 * kQRch, en, mn);
             auto refill = [&]() {
 #pragma unroll
                 for (int u = 0; u < kQRch; u++) {
@@ -919,21 +924,33 @@ __global__ __launch_bounds__(GSR_TILE_PIX) __attribute__((amdgpu_waves_per_eu(GS
                 }
                 base += 64 * kQRch;
                 if (TL) n_refills++;
-#pragma unroll
-                for (int u = 0; u < kQRch; u++) {
-                    ec[u] = en[u];
-                    mc[u] = mn[u];
-                }
-                load_chunks(base + 64 * kQRch, en, mn);
+                // the next refill's chunk into the same registers (one set, loaded one refill ahead: a
+                // second set rotated into this one compiled to copies that waited for the loads just issued)
+                load_chunks(base, ec, mc);
                 __builtin_amdgcn_wave_barrier();
             };
             // fill so that entries [head, head + 4 GSR_QUAD_SLOTS) exist; once the list is
             // exhausted, the ring slots past its last entry hold the null Gaussian (an index whose record and feature
             // offsets are out of range: zeros, opacity 0, nothing taken), so the step operands are read
             // without a validity branch
+            // ensure() runs once per group of GSR_QUAD_SLOTS steps (the unrolled step loop), so between a
+            // refill's chunk loads and the next refill's use of them a group's operand loads (4 per step)
+            // are issued, and the memory-counter wait there counts past the operand loads in flight
+            // instead of draining them (only a back-to-back refill, whose ring ran short, waits for its
+            // chunk).  It keeps two groups' entries queued (one group runs, the other is read
+            // GSR_QUAD_SLOTS - 1 steps ahead).
             bool nulled = false;
             auto ensure = [&]() {
-                while (tail - head < 4u * GSR_QUAD_SLOTS && base < n) refill();
+                if (tail - head < 8u * GSR_QUAD_SLOTS && base < n) {
+                    refill();
+                    // a back-to-back refill waits for the chunk just loaded (the newest loads: vmcnt(0)),
+                    // explicitly, so that this loop stays apart from the first refill, whose wait then
+                    // counts from the group's operand loads alone
+                    while (tail - head < 8u * GSR_QUAD_SLOTS && base < n) {
+                        __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0) expcnt(7) lgkmcnt(15)
+                        refill();
+                    }
+                }
                 if (base >= n && !nulled) {
                     nulled = true;
                     if (lane < 4 * GSR_QUAD_SLOTS) {
@@ -988,9 +1005,8 @@ __global__ __launch_bounds__(GSR_TILE_PIX) __attribute__((amdgpu_waves_per_eu(GS
                 // alpha (its records' wait), this step's blend + MFMAs)
                 uint64_t c0 = 0, c1 = 0, c2 = 0;
                 if (TL) { __builtin_amdgcn_sched_barrier(0); c0 = __builtin_amdgcn_s_memtime(); __builtin_amdgcn_sched_barrier(0); }
-                // the operands of step i + NS - 1 first (their loads run under this step and the next ones)
-                ensure();
-                __builtin_amdgcn_wave_barrier();
+                // the operands of step i + NS - 1 first (their loads run under this step and the next ones;
+                // the ring holds them: ensure() at the top of the step group)
                 records(head + 4u * (NS - 1), pr0[ld], pr1[ld], pf0[ld], pf1[ld]);
                 const uint4 np4 = positions(head + 4u);
                 if (TL) { __builtin_amdgcn_sched_barrier(0); c1 = __builtin_amdgcn_s_memtime(); __builtin_amdgcn_sched_barrier(0); }
@@ -1039,6 +1055,8 @@ __global__ __launch_bounds__(GSR_TILE_PIX) __attribute__((amdgpu_waves_per_eu(GS
             };
             static_assert(NS >= 3 && NS <= 8, "GSR_QUAD_SLOTS");
             while (head < tail) {
+                ensure();
+                __builtin_amdgcn_wave_barrier();
                 if (!step(QSlot<0>{})) break;
                 if (!step(QSlot<1>{})) break;
                 if (!step(QSlot<2>{})) break;
@@ -1058,6 +1076,13 @@ __global__ __launch_bounds__(GSR_TILE_PIX) __attribute__((amdgpu_waves_per_eu(GS
                     if (!step(QSlot<7 % NS>{})) break;
                 }
             }
+            // the slot registers are read after the loop (an empty asm use: one wait per item), so every
+            // path out of a step uses its operand loads and the compiler keeps them in the step that
+            // issues them -- otherwise it sank them past the break tests to the loop's back edge, where
+            // a whole group's loads were issued at once and waited for within the next group
+#pragma unroll
+            for (int k = 0; k < NS; k++)
+                asm volatile("" ::"v"(pr0[k].x), "v"(pr1[k].x), "v"(pf0[k]), "v"(pf1[k]));
             if (TL) n_walk = (uint32_t)min(base, n);
         }
         if (TL && lane == 0 && item < (o.timeline_cap & 0x7FFFFFFFu)) {
