@@ -615,7 +615,10 @@ static int forward_batch_impl(int B, int P, int width, int height, const float* 
     in.bg = backgrounds; in.s_bg = bg_stride;
     in.scale_mod = scale_modifier;
     in.prefiltered = 0; in.antialiasing = antialiasing;
-    in.fwd_only = (numerics & GSR_FORWARD_ONLY) != 0;
+    in.fwd_only = (numerics & GSR_FORWARD_ONLY) != 0 || dg != nullptr;
+    // recorded before any launch or early return: a workspace whose address the allocator reuses, or
+    // whose forward failed partway, carries this forward's flag, not an older one
+    note_workspace(workspace, in.fwd_only != 0);
     Outputs o{out_color, out_invdepth, radii, g_render_counters, g_timeline, g_timeline_cap};
     if (refine) {
         o.rb = refine->bias;
@@ -631,8 +634,7 @@ static int forward_batch_impl(int B, int P, int width, int height, const float* 
     // forward (its culling-error word is set during that kernel) or an empty one (no kernel)
     in.zero_ctrl = !in.prefiltered && d.P > 0 && d.B > 0;
     if (!in.zero_ctrl) HIP_TRY(hipMemsetAsync(g.ctrl, 0, ctrl_words(d) * 4, s));
-    if (dg) {
-        in.fwd_only = 1;  // (the deformed attributes are not kept: no backward can use the workspace)
+    if (dg) {  // (forward-only: the deformed attributes are not kept, no backward can use the workspace)
         StageTimer st_(0, s);
         launch_deform_preprocess(d, in, g, o, *dg, s);
     } else {
@@ -648,7 +650,6 @@ static int forward_batch_impl(int B, int P, int width, int height, const float* 
     }
     int rc = run_binning_and_render(d, in, g, im, bn, o, numerics, 0, s);
     if (rc < 0) return rc;
-    note_workspace(workspace, in.fwd_only != 0);
     return 0;
 }
 
