@@ -57,6 +57,27 @@ def test_quad_list_lengths_around_slot_and_refill_boundaries():
         _compare_exact(d)
 
 
+@pytest.mark.parametrize("qx,qy,seed", [(0, 0, 11), (3, 2, 12)])
+def test_quad_sparse_and_dense_walks(qx, qy, seed):
+    """One 16x16 tile whose list is long (~2k entries) but whose Gaussians are small and packed into
+    one 4x4 quad: that quad's wave walks a dense ring, every other quad's wave finds few entries per
+    192-entry refill, so its ring runs short and refills back to back (the refill loop apart from
+    the step group's first refill), and every walk ends on the null padding -- bit-exact."""
+    import oracle
+    d = make_scene("random", 20000, 16, 16, seed=seed)
+    d["scales"] = (d["scales"] * 0.15).astype(np.float32)
+    st = oracle.preprocess(d["means3D"], d["scales"], d["rotations"], d["opacities"], None, d["viewmatrix"],
+                           d["projmatrix"], d["image_width"], d["image_height"], d["tanfovx"], d["tanfovy"])
+    m = st["means2D"].reshape(-1, 2)
+    inq = (m[:, 0] >= 4 * qx) & (m[:, 0] < 4 * qx + 4) & (m[:, 1] >= 4 * qy) & (m[:, 1] < 4 * qy + 4)
+    keep = inq | (np.random.default_rng(seed).random(m.shape[0]) < 0.04)
+    for k in ("means3D", "colors", "opacities", "scales", "rotations"):
+        d[k] = np.ascontiguousarray(d[k][keep])
+    assert inq.sum() > 600 and (keep & ~inq).sum() > 300
+    gs, _ = _compare_exact(d)
+    assert gs["R"] > 1000
+
+
 def test_forward_antialiasing_bit_exact():
     d = make_scene("random", 4000, 96, 80, seed=5)
     _compare_exact(d, antialiasing=True)
